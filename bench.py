@@ -1,0 +1,209 @@
+#!/usr/bin/env python3
+"""Benchmark of the LSB bit-plane embed+extract hot path on MI355X.
+
+One step = encode (codec_plan: histogram/decision/block-search scan + stego copy,
+codec_embed: window writes + location maps) + decode (codec_extract: cover restore
+stream + payload gather) over one batch of synthetic uint16 slices that are already
+resident in HBM, plus (N > 1) the RCCL all-gather of the per-slice records and
+location maps.  Prints ONE JSON line (rank 0).
+
+    python bench.py                              # N=1, 256 x 2048^2 ct12, K=20, W=3
+    torchrun --nproc-per-node N bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "Mpixels/s PEE embed+extract, 2048² uint16 batch; % HBM roofline"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="slices per GPU")
+    ap.add_argument("--size", type=int, default=2048)
+    ap.add_argument("--kind", default="ct12", choices=["ct12", "u16"])
+    ap.add_argument("--payload-chars", type=int, default=1024)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (0 = skip)")
+    ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event pass")
+    return ap.parse_args()
+
+
+def make_covers(torch, kind, b, h, w, device, seed):
+    """Synthetic slices generated on the device (no host->device GBs)."""
+    if kind == "u16":
+        g = torch.Generator(device=device)
+        g.manual_seed(seed)
+        x = torch.randint(0, 65536, (b, h, w), generator=g, device=device, dtype=torch.int32)
+        return x.to(torch.uint16)
+    ys = torch.arange(h, device=device, dtype=torch.float32).view(1, h, 1)
+    xs = torch.arange(w, device=device, dtype=torch.float32).view(1, 1, w)
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    out = torch.empty((b, h, w), dtype=torch.uint16, device=device)
+    for i in range(b):
+        base = (torch.sin(xs / 97.0 + (seed + i)) + torch.cos(ys / 61.0) + 2.0) / 4.0 * 4095.0 * 0.8
+        noise = torch.randn((1, h, w), generator=g, device=device) * 16.0
+        out[i] = torch.clamp(torch.round(base + noise), 0, 4095).to(torch.int32).to(torch.uint16)[0]
+    return out
+
+
+def cpu_baseline(size: int, kind: str, chars: int, budget_s: float):
+    """The oracle (numpy restatement of the reference, bit-identical to it) timed on this
+    host: decomposition + hybrid embed + merge + extract_local_planes + decode_message
+    (SURVEY §8(d)), single process, on distinct synthetic slices until the budget is used."""
+    from codec_tcc_amd import synth
+    from oracle import ref_cpu as R
+    gen = synth.GENERATORS[kind]
+    px = 0
+    n = 0
+    t_work = 0.0
+    t_start = time.perf_counter()
+    while n == 0 or (time.perf_counter() - t_start) < budget_s:
+        img = gen(size, size, 1000 + n)
+        bits = R.message_to_bits(synth.payload(chars, 7 + n))
+        t0 = time.perf_counter()
+        enc = R.encode_slice(img, bits, beta=0.4, sb=16)
+        R.decode_slice(enc["stego"], enc["bitmaps"], enc["s"], enc["segments_lengths"], enc["segment_indices"])
+        t_work += time.perf_counter() - t0
+        px += img.size
+        n += 1
+    return {
+        "value": round(px / t_work / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
+        "sample": f"{n} x {size}x{size} {kind} uint16 slices, {chars}-char payloads, numpy oracle "
+                  f"(decompose+hybrid embed+merge+extract_local_planes+decode_message), 1 process",
+        "seconds": round(t_work, 2),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import codec_tcc_amd as ct
+    from codec_tcc_amd import _lib, synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else torch.cuda.current_device())
+    B, H, W = args.batch, args.size, args.size
+
+    covers = make_covers(torch, args.kind, B, H, W, dev, seed=rank * B)
+    msgs = [synth.payload(args.payload_chars, 7 + rank * B + i) for i in range(B)]
+    codec = ct.Codec(B, H, W, dtype="uint16", beta=0.4, block=16, device=dev)
+    pl = ct.make_payloads(msgs, dev)
+    # preallocated outputs (the step allocates nothing)
+    stego = torch.empty((B, H, W), dtype=torch.uint16, device=dev)
+    maps = torch.empty((B, pl.map_words), dtype=torch.int64, device=dev)
+    meta = torch.empty((B, _lib.META_BYTES), dtype=torch.uint8, device=dev)
+    cover_out = torch.empty((B, H, W), dtype=torch.uint16, device=dev)
+    payload_out = torch.empty((B, pl.payload_words), dtype=torch.int64, device=dev)
+    rec_words = (_lib.META_BYTES + 7) // 8 + pl.map_words
+    gathered = torch.empty((world * B, rec_words), dtype=torch.int64, device=dev) if world > 1 else None
+    record = torch.empty((B, rec_words), dtype=torch.int64, device=dev) if world > 1 else None
+
+    def step():
+        codec.encode(covers, pl, stego=stego, maps=maps, meta=meta)
+        codec.decode(stego, maps, meta, payload_words=pl.payload_words, map_words=pl.map_words,
+                     cover=cover_out, payload=payload_out)
+        if world > 1:
+            # per-slice fixed-size records: slice meta + packed location map -> every rank
+            record[:, : (_lib.META_BYTES + 7) // 8].view(torch.uint8)[:, : _lib.META_BYTES].copy_(meta)
+            record[:, (_lib.META_BYTES + 7) // 8:].copy_(maps)
+            dist.all_gather_into_tensor(gathered, record)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness spot check of the warm state (cheap, outside the timed region)
+    ok = bool(torch.equal(cover_out.view(torch.int16), covers.view(torch.int16)))
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- per-kernel device time (HIP events on the launch stream), separate timed pass
+    kernels = {}
+    if not args.no_profile:
+        lib = _lib.load()
+        cap = 64 * args.steps
+        _lib.check(lib.codec_profile_begin(cap), "codec_profile_begin")
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        import ctypes as C
+        ms = (C.c_float * cap)()
+        tags = (C.c_int32 * cap)()
+        n = lib.codec_profile_end(ms, tags, cap)
+        for i in range(max(n, 0)):
+            kernels.setdefault(_lib.KERNEL_TAGS.get(tags[i], str(tags[i])), []).append(ms[i])
+
+    npx_rank = B * H * W
+    total_px = npx_rank * world
+    ms_step = elapsed / args.steps * 1e3
+    value = total_px * args.steps / elapsed / 1e6
+
+    recs = ct.meta_records(meta)
+    s_vals = sorted({r.s for r in recs})
+    roof = None
+    if "k_scan_fast" in kernels:
+        t_scan = float(np.mean(kernels["k_scan_fast"])) / 1e3
+        bytes_scan = npx_rank * (2 + 2)              # read cover + write stego (uint16)
+        ach = bytes_scan / t_scan / 1e9
+        roof = {"bound": "hbm", "kernel": "k_scan_fast", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "algorithmic_bytes_per_launch": bytes_scan, "avg_launch_ms": round(t_scan * 1e3, 4)}
+    step_bytes = npx_rank * 8                        # cover r + stego w + stego r + cover w
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "Mpixels/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u16",
+            "data": "synthetic",
+            "config": {"workload": f"{args.kind} {H}x{W} uint16 x {B} slices/GPU, {args.payload_chars}-char "
+                                   f"payload/slice, beta=0.4, block=16; encode(plan+embed)+decode(restore+gather)"
+                                   + (" + RCCL all-gather of slice records/maps" if world > 1 else ""),
+                       "global_batch": B * world, "slice": f"{H}x{W}", "parallelism": f"slices/{world} GPUs"},
+            "roofline": roof,
+            "step_hbm_gbs": round(step_bytes * world / (elapsed / args.steps) / 1e9 / world, 1),
+            "kernels_ms": {k: round(float(np.mean(v)), 4) for k, v in kernels.items()},
+            "s_values": s_vals,
+            "roundtrip_ok": ok,
+        }
+        if args.cpu_seconds > 0 and world == 1:
+            out["cpu_baseline"] = cpu_baseline(args.size, args.kind, args.payload_chars, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

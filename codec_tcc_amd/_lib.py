@@ -1,0 +1,111 @@
+"""ctypes binding of libcodec_hip.so (include/codec_tcc.h).
+
+The library is built in-tree (codec_tcc_amd/libcodec_hip.so, see build.py).  There is no
+CPU fallback: if the library cannot be loaded, every entry point raises RuntimeError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcodec_hip.so")
+
+MAX_PLANES = 16
+MODE_HYBRID = 0
+MODE_MULTI = 1
+FLAG_OVERLAP = 1
+FLAG_LOSSY = 2
+FLAG_BADLUT = 4
+
+I16 = C.c_int32 * MAX_PLANES
+D16 = C.c_double * MAX_PLANES
+
+
+class Params(C.Structure):
+    _fields_ = [
+        ("B", C.c_int32), ("H", C.c_int32), ("W", C.c_int32),
+        ("in_bytes", C.c_int32), ("out_bytes", C.c_int32), ("nbits", C.c_int32),
+        ("block", C.c_int32), ("align", C.c_int32), ("mode", C.c_int32),
+        ("fixed_s", C.c_int32), ("fixed_offset", C.c_int32), ("all_mi", C.c_int32),
+        ("payload_words", C.c_int32), ("map_words", C.c_int32), ("n_classes", C.c_int32),
+        ("reserved", C.c_int32), ("beta", C.c_double),
+    ]
+
+
+class Layout(C.Structure):
+    _fields_ = [("sizes", I16), ("perm", I16), ("src", I16), ("len", I16)]
+
+
+class SliceMeta(C.Structure):
+    _fields_ = [
+        ("s", C.c_int32), ("start_offset", C.c_int32), ("total_used", C.c_int32),
+        ("flags", C.c_uint32), ("npix", C.c_int32), ("nbits", C.c_int32),
+        ("status", C.c_int32), ("nonzero_bins", C.c_int32),
+        ("perm", I16), ("sizes", I16), ("n", I16), ("src", I16), ("off", I16), ("cat", I16),
+        ("entropy", C.c_double), ("target", C.c_double), ("cum_info", C.c_double),
+        ("reserved_d", C.c_double), ("mi", D16),
+    ]
+
+
+META_BYTES = C.sizeof(SliceMeta)
+LAYOUT_BYTES = C.sizeof(Layout)
+
+_VP = C.c_void_p
+_SIGS = {
+    "codec_abi_version": (C.c_int, []),
+    "codec_last_error": (C.c_char_p, []),
+    "codec_workspace_bytes": (C.c_size_t, [C.POINTER(Params)]),
+    "codec_plan": (C.c_int, [C.POINTER(Params), _VP, _VP, _VP, C.c_int64, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),
+    "codec_embed": (C.c_int, [C.POINTER(Params), _VP, _VP, _VP, _VP, _VP, _VP]),
+    "codec_extract": (C.c_int, [C.POINTER(Params), _VP, _VP, _VP, _VP, _VP, _VP]),
+    "codec_refdecode": (C.c_int, [C.POINTER(Params), _VP, _VP, _VP, _VP, C.c_int32, _VP, _VP]),
+    "codec_refdecode_dense": (C.c_int, [C.POINTER(Params), _VP, C.c_int32, _VP, C.c_int32, _VP, _VP,
+                                        C.c_int32, _VP, _VP]),
+    "codec_expand_maps": (C.c_int, [C.POINTER(Params), _VP, _VP, _VP, C.c_int32, _VP]),
+    "codec_restore_dense": (C.c_int, [C.POINTER(Params), _VP, _VP, C.c_int32, _VP, _VP, _VP]),
+    "codec_unpack_planes": (C.c_int, [C.POINTER(Params), _VP, C.c_int32, C.c_int32, _VP, C.c_int32, _VP]),
+    "codec_merge_planes": (C.c_int, [C.POINTER(Params), _VP, C.c_int32, C.c_int32, _VP, _VP]),
+    "codec_profile_begin": (C.c_int, [C.c_int32]),
+    "codec_profile_end": (C.c_int, [_VP, _VP, C.c_int32]),
+}
+KERNEL_TAGS = {1: "k_scan_fast", 2: "k_scan_generic", 3: "k_block_exact", 4: "k_decide",
+               5: "k_embed", 6: "k_restore", 7: "k_gather", 8: "other"}
+EXPORTS = tuple(_SIGS)
+
+_lib = None
+_load_error = None
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and return the library; raise RuntimeError if it is missing."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"libcodec_hip.so not found at {path}: build it with "
+                           f"`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback)")
+    try:
+        lib = C.CDLL(path)
+    except OSError as e:  # pragma: no cover - environment specific
+        _load_error = e
+        raise RuntimeError(f"cannot load {path}: {e}") from e
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.codec_abi_version() != 1:
+        raise RuntimeError("libcodec_hip.so ABI mismatch")
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().codec_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t) -> int | None:
+    """Raw device pointer of a torch tensor (or None)."""
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,57 @@
+"""In-tree build of libcodec_hip.so for gfx950 (no torch extension machinery: the
+library is a plain C-ABI shared object loaded with ctypes).
+
+    python -m codec_tcc_amd.build            # or __graft_entry__.build()
+
+-ffp-contract=off is REQUIRED: the decision kernel reproduces numpy's float64 sums bit
+for bit and must not fuse multiplies into adds.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+SRC = os.path.join(HERE, "csrc", "codec_hip.hip")
+OUT = os.path.join(HERE, "libcodec_hip.so")
+INC = os.path.join(REPO, "include")
+ARCH = os.environ.get("CODEC_OFFLOAD_ARCH", "gfx950")
+
+FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", f"--offload-arch={ARCH}",
+         "-Wall", "-Wno-unused-function"]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = [SRC, os.path.join(INC, "codec_tcc.h"), __file__]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_build():
+        return OUT
+    tmp = OUT + ".tmp"
+    cmd = [hipcc(), *FLAGS, f"-I{INC}", SRC, "-o", tmp]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-6000:]}")
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,1524 @@
+// codec_hip.hip -- CDNA4 (gfx950 / MI355X) kernels and the C ABI for the LSB bit-plane
+// embed/extract path of wesleyfn/codec-tcc (reference: src/codec.py).  See DESIGN.md.
+//
+// Pipeline per batch of B slices ([B][H][W] uint8/uint16 in HBM):
+//   k_scan_fast / k_scan_generic : ONE streaming read of the cover -> value histogram
+//                                  (LDS-privatised), full-block LSB popcounts -> packed
+//                                  argmax key, and the cover->stego copy.
+//   k_block_exact                : numpy-exact np.var for partial / non-power-of-two blocks.
+//   k_decide                     : per slice (one workgroup): bit-exact numpy entropy and
+//                                  mutual information (8192-chunked pairwise sums emulated,
+//                                  log2 from a numpy-built table), the s decision, the start
+//                                  offset and the segment windows -> codec_slice_meta.
+//   k_embed                      : one thread per embedded bit: window write + packed
+//                                  location map via wave ballot.
+//   k_restore + k_gather         : extraction: stream stego->cover with the map XOR-ed back,
+//                                  and the payload bits (ballot-packed).
+// Numerics: this file MUST be compiled with -ffp-contract=off (no FMA contraction) so the
+// float64 sums reproduce numpy's bit for bit.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "codec_tcc.h"
+
+typedef unsigned long long u64;
+
+// ------------------------------------------------------------------ error reporting
+static thread_local char g_err[512] = "";
+
+static int set_err(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define CODEC_EINVAL (-1000)
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return set_err(-(int)e_, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_),      \
+                           __FILE__, __LINE__);                                           \
+    } while (0)
+#define LAUNCH_CHECK(name)                                                                \
+    do {                                                                                  \
+        hipError_t e_ = hipGetLastError();                                                \
+        if (e_ != hipSuccess)                                                             \
+            return set_err(-(int)e_, "launch %s: %s", name, hipGetErrorString(e_));       \
+    } while (0)
+
+// ------------------------------------------------------------------ profiling hooks
+struct ProfWin {
+    hipEvent_t* ev = nullptr;
+    int32_t* tag = nullptr;
+    int cap = 0, n = 0;
+};
+static ProfWin g_prof;
+
+struct ProfScope {   // records a start event now and the end event at scope exit
+    hipStream_t st;
+    int slot = -1;
+    ProfScope(hipStream_t s, int tag) : st(s) {
+        if (g_prof.ev && g_prof.n < g_prof.cap) {
+            slot = g_prof.n++;
+            g_prof.tag[slot] = tag;
+            hipEventRecord(g_prof.ev[2 * slot], st);
+        }
+    }
+    ~ProfScope() {
+        if (slot >= 0) hipEventRecord(g_prof.ev[2 * slot + 1], st);
+    }
+};
+
+// ------------------------------------------------------------------ numpy float emulation
+// numpy's add.reduce over a contiguous float64 array (np.sum) walks it in buffers of
+// 8192 elements, each summed by pairwise_sum (<8: serial; <=128: 8 accumulators;
+// else split at n/2 rounded down to a multiple of 8), and adds the buffer sums
+// serially.  Verified against numpy 2.2 on lengths 0..200000 (tests/test_numpy_semantics).
+#define NP_CHUNK 8192
+#define NP_LEAF 128
+
+template <class F>
+__device__ __forceinline__ double np_leaf(const F& f, int a, int n) {
+    if (n < 8) {
+        double r = -0.0;
+        for (int i = 0; i < n; ++i) r += f(a + i);
+        return r;
+    }
+    double r0 = f(a + 0), r1 = f(a + 1), r2 = f(a + 2), r3 = f(a + 3);
+    double r4 = f(a + 4), r5 = f(a + 5), r6 = f(a + 6), r7 = f(a + 7);
+    int i = 8;
+    const int lim = n - (n % 8);
+    for (; i < lim; i += 8) {
+        r0 += f(a + i + 0); r1 += f(a + i + 1); r2 += f(a + i + 2); r3 += f(a + i + 3);
+        r4 += f(a + i + 4); r5 += f(a + i + 5); r6 += f(a + i + 6); r7 += f(a + i + 7);
+    }
+    double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    for (; i < n; ++i) res += f(a + i);
+    return res;
+}
+
+// serial pairwise_sum over [a, a+n), n <= NP_CHUNK, explicit stack (depth <= 8)
+template <class F>
+__device__ double np_pairwise_serial(const F& f, int a, int n) {
+    if (n <= NP_LEAF) return np_leaf(f, a, n);
+    int sa[12], sn[12], st[12];
+    double sv[12];
+    int sp = 0, vp = 0;
+    sa[0] = a; sn[0] = n; st[0] = 0; sp = 1;
+    while (sp > 0) {
+        int k = sp - 1;
+        int na = sa[k], nn = sn[k];
+        if (nn <= NP_LEAF) {
+            sv[vp++] = np_leaf(f, na, nn);
+            --sp;
+            continue;
+        }
+        int n2 = (nn >> 1) & ~7;
+        if (st[k] == 0) {
+            st[k] = 1;
+            sa[sp] = na; sn[sp] = n2; st[sp] = 0; ++sp;
+        } else if (st[k] == 1) {
+            st[k] = 2;
+            sa[sp] = na + n2; sn[sp] = nn - n2; st[sp] = 0; ++sp;
+        } else {
+            double r = sv[--vp];
+            double l = sv[--vp];
+            sv[vp++] = l + r;
+            --sp;
+        }
+    }
+    return sv[0];
+}
+
+// np.sum semantics, serial (small n: partial-block variance)
+template <class F>
+__device__ double np_sum_serial(const F& f, int n) {
+    double res = -0.0;
+    for (int a = 0; a < n; a += NP_CHUNK) {
+        int len = min(NP_CHUNK, n - a);
+        res += np_pairwise_serial(f, a, len);
+    }
+    return res;
+}
+
+// size of node (d, j) of the chunk tree of a chunk holding r elements
+__device__ __forceinline__ int np_node_size(int r, int d, int j, int* start) {
+    int a = 0, n = r;
+    for (int l = d - 1; l >= 0; --l) {
+        const int bit = (j >> l) & 1;
+        if (n > NP_LEAF) {
+            const int n2 = (n >> 1) & ~7;
+            if (bit) { a += n2; n -= n2; } else { n = n2; }
+        } else if (bit) {
+            n = 0;
+        }
+    }
+    *start = a;
+    return n;
+}
+
+// np.sum semantics over m <= 65536 elements, computed by a 1024-thread block:
+// thread t owns chunk t/128 and bottom slot t%128 of that chunk's (depth-7) tree.
+// Leaves reached above depth 7 are carried down the left spine; internal nodes are
+// re-summed bottom-up exactly in numpy's order.  Returns the sum to every thread.
+template <class F>
+__device__ double np_sum_block1024(const F& f, int m, double* vals /*[1024]*/) {
+    const int t = threadIdx.x;
+    const int c = t >> 7, j = t & 127;
+    const int cstart = c * NP_CHUNK;
+    const int r = min(NP_CHUNK, max(0, m - cstart));
+    double v = 0.0;
+    if (r > 0) {
+        int a;
+        const int n = np_node_size(r, 7, j, &a);
+        if (n > 0) v = np_leaf(f, cstart + a, n);
+    }
+    vals[t] = v;
+    __syncthreads();
+    for (int d = 6; d >= 0; --d) {
+        const bool act = (r > 0) && (j < (1 << d));
+        double nv = 0.0;
+        if (act) {
+            int a;
+            const int n = np_node_size(r, d, j, &a);
+            const double L = vals[c * 128 + 2 * j];
+            const double R = vals[c * 128 + 2 * j + 1];
+            nv = (n > NP_LEAF) ? (L + R) : L;
+        }
+        __syncthreads();
+        if (act) vals[c * 128 + j] = nv;
+        __syncthreads();
+    }
+    double res = -0.0;
+    const int nchunks = (m + NP_CHUNK - 1) / NP_CHUNK;
+    for (int k = 0; k < nchunks; ++k) res += vals[k * 128];
+    __syncthreads();
+    return res;
+}
+
+// ------------------------------------------------------------------ block primitives
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+
+// exclusive scan over the block (NT threads); sh needs NT/64+1 words
+template <int NT>
+__device__ uint32_t block_excl_scan(uint32_t x, uint32_t* sh, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan(x);
+    if (lane == 63) sh[wv] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int w = 0; w < NT / 64; ++w) {
+            const uint32_t tmp = sh[w];
+            sh[w] = acc;
+            acc += tmp;
+        }
+        sh[NT / 64] = acc;
+    }
+    __syncthreads();
+    const uint32_t r = sh[wv] + inc - x;
+    *total = sh[NT / 64];
+    __syncthreads();
+    return r;
+}
+
+template <int NT>
+__device__ uint32_t block_sum_u32(uint32_t x, uint32_t* sh) {
+    uint32_t tot;
+    block_excl_scan<NT>(x, sh, &tot);
+    return tot;
+}
+
+template <int NT>
+__device__ int block_max_i32(int x, int* sh) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x = max(x, __shfl_xor(x, o, 64));
+    if (lane == 0) sh[wv] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int m = sh[0];
+        for (int w = 1; w < NT / 64; ++w) m = max(m, sh[w]);
+        sh[NT / 64] = m;
+    }
+    __syncthreads();
+    const int r = sh[NT / 64];
+    __syncthreads();
+    return r;
+}
+
+// ------------------------------------------------------------------ histogram helpers
+// uint16 covers: 65536 bins kept as 16-bit halves of 32768 LDS words (128 KiB).  An add
+// whose returned old value shows a half wrapping is rare; its exact effect on the two
+// fields is recorded in the global histogram, so the per-workgroup pixel count is
+// unbounded (final bin = LDS field + recorded adjustments, modulo 2^32).
+__device__ __forceinline__ void hist16_add(uint32_t* lds, uint32_t* ghist, uint32_t v, uint32_t cnt) {
+    const uint32_t w = v >> 1;
+    if (v & 1u) {
+        const uint32_t old = atomicAdd(&lds[w], cnt << 16);
+        if ((old >> 16) + cnt > 0xFFFFu) atomicAdd(&ghist[v], 0x10000u);
+    } else {
+        const uint32_t old = atomicAdd(&lds[w], cnt);
+        if ((old & 0xFFFFu) + cnt > 0xFFFFu) {
+            atomicAdd(&ghist[v], 0x10000u);
+            uint32_t adj = 0xFFFFFFFFu;                     // -1: spurious carry into v+1
+            if ((old >> 16) == 0xFFFFu) adj += 0x10000u;    // ...which wrapped that field
+            atomicAdd(&ghist[v + 1], adj);
+        }
+    }
+}
+
+template <typename T> struct HistCfg;
+template <> struct HistCfg<uint16_t> {
+    static constexpr int kBins = 65536;
+    static constexpr int kLdsWords = 32768;
+};
+template <> struct HistCfg<uint8_t> {
+    static constexpr int kBins = 256;
+    static constexpr int kLdsWords = 16 * 256;   // one private copy per wave (16 waves)
+};
+
+template <typename T>
+__device__ __forceinline__ void hist_add(uint32_t* lds, uint32_t* ghist, uint32_t v, uint32_t cnt);
+template <>
+__device__ __forceinline__ void hist_add<uint16_t>(uint32_t* lds, uint32_t* ghist, uint32_t v, uint32_t cnt) {
+    hist16_add(lds, ghist, v, cnt);
+}
+template <>
+__device__ __forceinline__ void hist_add<uint8_t>(uint32_t* lds, uint32_t*, uint32_t v, uint32_t cnt) {
+    atomicAdd(&lds[((threadIdx.x >> 6) << 8) + v], cnt);
+}
+
+template <typename T>
+__device__ void hist_flush(uint32_t* lds, uint32_t* ghist);
+template <>
+__device__ void hist_flush<uint16_t>(uint32_t* lds, uint32_t* ghist) {
+    u64* g64 = reinterpret_cast<u64*>(ghist);
+    for (int w = threadIdx.x; w < 32768; w += blockDim.x) {
+        const uint32_t x = lds[w];
+        if (x) atomicAdd(&g64[w], (u64)(x & 0xFFFFu) | ((u64)(x >> 16) << 32));
+    }
+}
+template <>
+__device__ void hist_flush<uint8_t>(uint32_t* lds, uint32_t* ghist) {
+    for (int v = threadIdx.x; v < 256; v += blockDim.x) {
+        uint32_t acc = 0;
+        for (int c = 0; c < 16; ++c) acc += lds[(c << 8) + v];
+        if (acc) atomicAdd(&ghist[v], acc);
+    }
+}
+
+// 8 pixels of a vector (16 B of uint16 / 8 B of uint8), run-merged histogram adds
+template <typename T, typename V>
+__device__ __forceinline__ void hist_add8(uint32_t* lds, uint32_t* ghist, const V& vec) {
+    uint32_t px[8];
+    if constexpr (sizeof(T) == 2) {
+        px[0] = vec.x & 0xFFFFu; px[1] = vec.x >> 16; px[2] = vec.y & 0xFFFFu; px[3] = vec.y >> 16;
+        px[4] = vec.z & 0xFFFFu; px[5] = vec.z >> 16; px[6] = vec.w & 0xFFFFu; px[7] = vec.w >> 16;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { px[k] = (vec.x >> (8 * k)) & 0xFFu; px[4 + k] = (vec.y >> (8 * k)) & 0xFFu; }
+    }
+    uint32_t run = 1;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        if (px[k + 1] == px[k]) {
+            ++run;
+        } else {
+            hist_add<T>(lds, ghist, px[k], run);
+            run = 1;
+        }
+    }
+    hist_add<T>(lds, ghist, px[7], run);
+}
+
+template <typename T> struct Vec8;
+template <> struct Vec8<uint16_t> { typedef uint4 type; };
+template <> struct Vec8<uint8_t> { typedef uint2 type; };
+
+__device__ __forceinline__ uint32_t lsb_count(const uint4& v) {
+    return __popc(v.x & 0x00010001u) + __popc(v.y & 0x00010001u) + __popc(v.z & 0x00010001u) +
+           __popc(v.w & 0x00010001u);
+}
+__device__ __forceinline__ uint32_t lsb_count(const uint2& v) {
+    return __popc(v.x & 0x01010101u) + __popc(v.y & 0x01010101u);
+}
+
+// ------------------------------------------------------------------ K1: scan + copy (fast)
+// Requirements (checked on the host): W % 8 == 0, SB in {8,16,32,64}, stego dtype ==
+// cover dtype with every bit kept, 16-B (u16) / 8-B (u8) aligned buffers.
+// Work item = (band of SB rows, 8-pixel column chunk); a wave covers 64 consecutive
+// chunks of one band, so every load instruction reads 1 KiB (u16) contiguously; the
+// SB/8 lanes of one block column combine their LSB counts with shuffles.
+template <typename T, int SB>
+__global__ __launch_bounds__(1024) void k_scan_fast(const T* __restrict__ cover, T* __restrict__ stego,
+                                                    int H, int W, int bands_per_wg,
+                                                    uint32_t* __restrict__ ghist_all,
+                                                    u64* __restrict__ gkey) {
+    typedef typename Vec8<T>::type V;
+    constexpr int G = SB / 8;
+    constexpr uint32_t NPB = (uint32_t)SB * SB;
+    __shared__ uint32_t lds[HistCfg<T>::kLdsWords];
+    __shared__ u64 wkey;
+    const int b = blockIdx.y;
+    const size_t npx = (size_t)H * W;
+    const T* src = cover + (size_t)b * npx;
+    T* dst = stego ? stego + (size_t)b * npx : nullptr;
+    uint32_t* ghist = ghist_all + (size_t)b * HistCfg<T>::kBins;
+
+    for (int i = threadIdx.x; i < HistCfg<T>::kLdsWords; i += 1024) lds[i] = 0;
+    if (threadIdx.x == 0) wkey = 0;
+    __syncthreads();
+
+    const int nbands = (H + SB - 1) / SB;
+    const int band0 = blockIdx.x * bands_per_wg;
+    const int band1 = min(nbands, band0 + bands_per_wg);
+    const int CR = W / 8;
+    const int CRp = (CR + G - 1) / G * G;
+    const int nbx = (W + SB - 1) / SB;
+    const int fullbx = W / SB, fullby = H / SB;
+    const int nitems = max(0, band1 - band0) * CRp;
+    const int lane = threadIdx.x & 63;
+    u64 best = 0;
+
+    for (int base = (threadIdx.x & ~63); base < nitems; base += 1024) {
+        const int it = base + lane;
+        const bool valid = it < nitems;
+        const int band = band0 + (valid ? it / CRp : 0);
+        const int c = valid ? it % CRp : CRp;
+        const bool inrow = valid && c < CR;
+        uint32_t ones = 0;
+        if (inrow) {
+            const int rows = min(SB, H - band * SB);
+            const size_t rowpix = (size_t)band * SB * W + (size_t)c * 8;
+            const V* s = reinterpret_cast<const V*>(src + rowpix);
+            V* d = dst ? reinterpret_cast<V*>(dst + rowpix) : nullptr;
+            const int stride = W / 8;   // vectors per row
+            int r = 0;
+            for (; r + 4 <= rows; r += 4) {
+                V v0 = s[(size_t)(r + 0) * stride];
+                V v1 = s[(size_t)(r + 1) * stride];
+                V v2 = s[(size_t)(r + 2) * stride];
+                V v3 = s[(size_t)(r + 3) * stride];
+                if (d) {
+                    d[(size_t)(r + 0) * stride] = v0;
+                    d[(size_t)(r + 1) * stride] = v1;
+                    d[(size_t)(r + 2) * stride] = v2;
+                    d[(size_t)(r + 3) * stride] = v3;
+                }
+                ones += lsb_count(v0) + lsb_count(v1) + lsb_count(v2) + lsb_count(v3);
+                hist_add8<T>(lds, ghist, v0);
+                hist_add8<T>(lds, ghist, v1);
+                hist_add8<T>(lds, ghist, v2);
+                hist_add8<T>(lds, ghist, v3);
+            }
+            for (; r < rows; ++r) {
+                V v0 = s[(size_t)r * stride];
+                if (d) d[(size_t)r * stride] = v0;
+                ones += lsb_count(v0);
+                hist_add8<T>(lds, ghist, v0);
+            }
+        }
+#pragma unroll
+        for (int o = 1; o < G; o <<= 1) ones += __shfl_xor(ones, o, 64);
+        const bool full = inrow && band < fullby && (c / G) < fullbx && (lane % G) == 0;
+        if (full) {
+            const uint32_t score = ones * (NPB - ones);
+            const uint32_t idx = (uint32_t)band * nbx + (uint32_t)(c / G);
+            const u64 key = ((u64)score << 32) | (u64)(0xFFFFFFFFu - idx);
+            best = best > key ? best : key;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const u64 other = __shfl_xor(best, o, 64);
+        best = best > other ? best : other;
+    }
+    if (lane == 0 && best) atomicMax(&wkey, best);
+    __syncthreads();
+    hist_flush<T>(lds, ghist);
+    if (threadIdx.x == 0 && wkey) atomicMax(&gkey[b], wkey);
+}
+
+// ------------------------------------------------------------------ K1': scan + copy (generic)
+// Any W, any block size, dtype conversion / plane masking (nbits != dtype bits).
+template <typename Tin, typename Tout>
+__global__ __launch_bounds__(1024) void k_scan_generic(const Tin* __restrict__ cover, Tout* __restrict__ stego,
+                                                       long long npx, long long px_per_wg, uint32_t keep,
+                                                       uint32_t* __restrict__ ghist_all) {
+    __shared__ uint32_t lds[HistCfg<Tin>::kLdsWords];
+    const int b = blockIdx.y;
+    const Tin* src = cover + (size_t)b * npx;
+    Tout* dst = stego ? stego + (size_t)b * npx : nullptr;
+    uint32_t* ghist = ghist_all + (size_t)b * HistCfg<Tin>::kBins;
+    for (int i = threadIdx.x; i < HistCfg<Tin>::kLdsWords; i += 1024) lds[i] = 0;
+    __syncthreads();
+    const long long q0 = (long long)blockIdx.x * px_per_wg;
+    const long long q1 = min(npx, q0 + px_per_wg);
+    for (long long q = q0 + threadIdx.x; q < q1; q += 1024) {
+        const uint32_t v = src[q];
+        if (dst) dst[q] = (Tout)(v & keep);
+        hist_add<Tin>(lds, ghist, v, 1u);
+    }
+    __syncthreads();
+    hist_flush<Tin>(lds, ghist);
+}
+
+// ------------------------------------------------------------------ K2: exact block variance
+__device__ __forceinline__ int exact_count(int H, int W, int sb, int edge_only) {
+    const int nby = (H + sb - 1) / sb, nbx = (W + sb - 1) / sb;
+    if (!edge_only) return nby * nbx;
+    const int ncol = (W % sb) ? nby : 0;
+    const int nrow = (H % sb) ? (nbx - ((W % sb) ? 1 : 0)) : 0;
+    return ncol + nrow;
+}
+
+__device__ __forceinline__ void exact_block(int e, int H, int W, int sb, int edge_only, int* by, int* bx) {
+    const int nby = (H + sb - 1) / sb, nbx = (W + sb - 1) / sb;
+    if (!edge_only) { *by = e / nbx; *bx = e % nbx; return; }
+    const int ncol = (W % sb) ? nby : 0;
+    if (e < ncol) { *by = e; *bx = nbx - 1; return; }
+    *by = nby - 1;
+    *bx = e - ncol;
+}
+
+// float(np.var(plane0[y:y1, x:x1])) exactly as numpy computes it (codec.py:446):
+// mean = c/n; x - mean per element; squares; np.sum (pairwise, row-major); / n.
+template <typename T>
+__global__ __launch_bounds__(256) void k_block_exact(const T* __restrict__ img, int H, int W, int sb, int edge_only,
+                                                     double* __restrict__ scores, int cap) {
+    const int b = blockIdx.y;
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    const int cnt = exact_count(H, W, sb, edge_only);
+    if (e >= cnt) return;
+    int by, bx;
+    exact_block(e, H, W, sb, edge_only, &by, &bx);
+    const int y0 = by * sb, x0 = bx * sb;
+    const int bh = min(sb, H - y0), bw = min(sb, W - x0);
+    const int n = bh * bw;
+    const T* base = img + (size_t)b * H * W + (size_t)y0 * W + x0;
+    int c = 0;
+    for (int y = 0; y < bh; ++y)
+        for (int x = 0; x < bw; ++x) c += base[(size_t)y * W + x] & 1;
+    const double mean = (double)c / (double)n;
+    const double a0 = (0.0 - mean) * (0.0 - mean);
+    const double a1 = (1.0 - mean) * (1.0 - mean);
+    auto elem = [&](int k) -> double {
+        const int y = k / bw, x = k - y * bw;
+        return (base[(size_t)y * W + x] & 1) ? a1 : a0;
+    };
+    const double sum = np_sum_serial(elem, n);
+    scores[(size_t)b * cap + e] = sum / (double)n;
+}
+
+// ------------------------------------------------------------------ K3: decide
+struct TermFn {
+    const uint32_t* hist;
+    const uint16_t* list;
+    const double* lut;
+    double N;
+    __device__ __forceinline__ double operator()(int k) const {
+        const uint32_t c = hist[list[k]];
+        const double p = (double)c / N;
+        return p * lut[c - 1];
+    }
+};
+
+__device__ __forceinline__ double plogp(const double* lut, uint32_t c, double N) {
+    const double p = (double)c / N;
+    return p * lut[c - 1];
+}
+
+// builds, in LDS `list`, the non-zero bins in the order of the joint bincount of
+// calculate_mutual_information (codec.py:546-551): bins with bit `plane` = 0 ascending,
+// then bins with bit 1 ascending.  plane < 0: plain ascending order (calculate_entropy).
+template <int BPT, int R>
+__device__ void build_order(const uint32_t* hist, int plane, uint16_t* list, uint32_t* sh) {
+    const int v0 = threadIdx.x * BPT;
+    uint32_t zc = 0, oc = 0;
+    for (int k = 0; k < BPT; ++k) {
+        const int v = v0 + k;
+        if (v < R && hist[v]) {
+            if (plane >= 0 && ((v >> plane) & 1)) ++oc; else ++zc;
+        }
+    }
+    uint32_t ztot, otot;
+    uint32_t zp = block_excl_scan<1024>(zc, sh, &ztot);
+    uint32_t op = block_excl_scan<1024>(oc, sh, &otot);
+    op += ztot;
+    for (int k = 0; k < BPT; ++k) {
+        const int v = v0 + k;
+        if (v < R && hist[v]) {
+            if (plane >= 0 && ((v >> plane) & 1)) list[op++] = (uint16_t)v; else list[zp++] = (uint16_t)v;
+        }
+    }
+    __syncthreads();
+}
+
+template <typename T>
+__global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t* __restrict__ ghist_all,
+                                                 const u64* __restrict__ gkey, const double* __restrict__ exact,
+                                                 int exact_cap, int exact_edge_only, int fast_blocks,
+                                                 const double* __restrict__ lut, long long lut_len,
+                                                 const codec_layout* __restrict__ table,
+                                                 const int32_t* __restrict__ slice_class,
+                                                 codec_slice_meta* __restrict__ meta_all) {
+    constexpr int R = HistCfg<T>::kBins;
+    constexpr int BPT = R >= 1024 ? R / 1024 : 1;
+    __shared__ uint16_t list[R];
+    __shared__ double vals[1024];
+    __shared__ uint32_t sh[20];
+    __shared__ int shi[20];
+    __shared__ uint32_t pops_sh[16];
+    __shared__ double best_sc[16];
+    __shared__ int best_ix[16];
+
+    const int b = blockIdx.x;
+    const int t = threadIdx.x;
+    const uint32_t* hist = ghist_all + (size_t)b * R;
+    const long long npx = (long long)P.H * P.W;
+    const double Nd = (double)npx;
+    codec_slice_meta* M = meta_all + b;
+
+    // ---- pass 1: distinct values, max value, per-plane popcounts (codec.py:571 planes)
+    uint32_t nz = 0, pop[16];
+    int vmax = -1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) pop[i] = 0;
+    {
+        const int v0 = t * BPT;
+        for (int k = 0; k < BPT; ++k) {
+            const int v = v0 + k;
+            if (v < R) {
+                const uint32_t c = hist[v];
+                if (c) {
+                    ++nz;
+                    vmax = v;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        if ((v >> i) & 1) pop[i] += c;
+                }
+            }
+        }
+    }
+    const uint32_t m = block_sum_u32<1024>(nz, sh);
+    (void)block_max_i32<1024>(vmax, shi);
+    if (t < 16) pops_sh[t] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        uint32_t x = pop[i];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+        if ((t & 63) == 0 && x) atomicAdd(&pops_sh[i], x);
+    }
+    __syncthreads();
+
+    const bool lut_ok = lut_len >= npx;
+
+    // ---- calculate_entropy (codec.py:489-502) = H(Y) in calculate_mutual_information
+    double Hy = 0.0;
+    if (lut_ok) {
+        build_order<BPT, R>(hist, -1, list, sh);
+        TermFn f{hist, list, lut, Nd};
+        Hy = -np_sum_block1024(f, (int)m, vals);
+    }
+    const double target = P.beta * Hy;
+
+    // ---- the s decision (codec.py:580-593)
+    int s = 1;
+    bool decided = false;
+    double cum = 0.0;
+    double mis[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) mis[i] = 0.0;
+    const bool need_decision = (P.fixed_s <= 0);
+    for (int i = 0; i < P.nbits && i < 16 && lut_ok; ++i) {
+        if (!(need_decision && !decided) && !P.all_mi) break;
+        const uint32_t pp = pops_sh[i];
+        double mi = 0.0;
+        if (m > 1 && pp != 0 && (long long)pp != npx) {          // codec.py:520-523
+            build_order<BPT, R>(hist, i, list, sh);
+            TermFn f{hist, list, lut, Nd};
+            const double hxy = -np_sum_block1024(f, (int)m, vals);
+            const double hx = -(plogp(lut, (uint32_t)(npx - pp), Nd) + plogp(lut, pp, Nd));
+            mi = (hx + Hy) - hxy;                                // codec.py:554
+            if (!(mi > 0.0)) mi = 0.0;                           // max(0.0, mi)
+        }
+        mis[i] = mi;
+        if (need_decision && !decided) {
+            cum += mi;
+            if (cum >= target) { s = i + 1; decided = true; }
+        }
+    }
+    if (!need_decision) s = P.fixed_s;
+
+    // ---- start offset: first maximal float(np.var) block in raster order (codec.py:441-453)
+    const int sb = P.block;
+    const int nbx = (P.W + sb - 1) / sb;
+    double bsc = -1.0;
+    int bix = 0x7FFFFFFF;
+    if (P.fixed_offset < 0 && P.mode == CODEC_MODE_HYBRID) {
+        const int cnt = exact_count(P.H, P.W, sb, exact_edge_only);
+        for (int e = t; e < cnt; e += 1024) {
+            int by, bx;
+            exact_block(e, P.H, P.W, sb, exact_edge_only, &by, &bx);
+            const double sc = exact[(size_t)b * exact_cap + e];
+            const int ix = by * nbx + bx;
+            if (sc > bsc || (sc == bsc && ix < bix)) { bsc = sc; bix = ix; }
+        }
+        if (t == 0 && fast_blocks) {
+            const u64 key = gkey[b];
+            if (key) {
+                const uint32_t score = (uint32_t)(key >> 32);
+                const int ix = (int)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFu));
+                const double n2 = (double)sb * sb * (double)sb * sb;
+                const double sc = (double)score / n2;
+                if (sc > bsc || (sc == bsc && ix < bix)) { bsc = sc; bix = ix; }
+            }
+        }
+        // block argmax (score desc, raster index asc)
+        const int lane = t & 63, wv = t >> 6;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const double os = __shfl_xor(bsc, o, 64);
+            const int oi = __shfl_xor(bix, o, 64);
+            if (os > bsc || (os == bsc && oi < bix)) { bsc = os; bix = oi; }
+        }
+        if (lane == 0) { best_sc[wv] = bsc; best_ix[wv] = bix; }
+        __syncthreads();
+        if (t == 0) {
+            for (int w = 1; w < 16; ++w)
+                if (best_sc[w] > bsc || (best_sc[w] == bsc && best_ix[w] < bix)) { bsc = best_sc[w]; bix = best_ix[w]; }
+        }
+    }
+
+    if (t != 0) return;
+    int offset = 0;
+    if (P.fixed_offset >= 0) offset = P.fixed_offset;
+    else if (P.mode == CODEC_MODE_HYBRID) offset = (bix / nbx) * sb * P.W + (bix % nbx) * sb;
+
+    // ---- segment windows (codec.py:455-485 / 288-316)
+    const codec_layout& L = table[(size_t)slice_class[b] * 16 + (s - 1)];
+    uint32_t flags = 0;
+    int pos = offset, cat = 0;
+    for (int j = 0; j < s; ++j) {
+        const int p = L.perm[j];
+        const int len = L.len[p];
+        const int n = (int)min((long long)len, npx);
+        if (len != L.sizes[p] || n != len) flags |= CODEC_FLAG_LOSSY;
+        M->perm[j] = p;
+        M->n[p] = n;
+        M->src[p] = L.src[p];
+        M->cat[p] = cat;
+        cat += n;
+        if (P.mode == CODEC_MODE_MULTI) {
+            M->off[p] = 0;
+            M->sizes[p] = n;                                   // codec.py:315
+        } else {
+            M->off[p] = pos;
+            M->sizes[p] = L.sizes[p];                          // codec.py:425,487
+            if (!P.align) pos = (int)(((long long)pos + n) % npx);
+        }
+    }
+    for (int p = s; p < 16; ++p) { M->perm[p] = -1; M->n[p] = 0; M->src[p] = 0; M->cat[p] = cat; M->off[p] = 0; M->sizes[p] = 0; }
+    if ((P.mode == CODEC_MODE_MULTI && s > 1) || (P.align && s > 1) || (long long)cat > npx) flags |= CODEC_FLAG_OVERLAP;
+    if (!lut_ok) flags |= CODEC_FLAG_BADLUT;
+    M->s = s;
+    M->start_offset = (P.mode == CODEC_MODE_HYBRID) ? offset : 0;
+    M->total_used = cat;
+    M->flags = flags;
+    M->npix = (int)npx;
+    M->nbits = P.nbits;
+    M->status = lut_ok ? 0 : 1;
+    M->nonzero_bins = (int)m;
+    M->entropy = Hy;
+    M->target = target;
+    M->cum_info = cum;
+    M->reserved_d = 0.0;
+    for (int i = 0; i < 16; ++i) M->mi[i] = mis[i];
+}
+
+// ------------------------------------------------------------------ per-slice window cache
+struct SliceWin {
+    int s, tot, npix;
+    uint32_t flags;
+    int perm[16], off[16], n[16], cat[16], src[16], sizes[16];
+};
+
+__device__ __forceinline__ void load_win(const codec_slice_meta* M, SliceWin* W) {
+    if (threadIdx.x == 0) {
+        W->s = M->s; W->tot = M->total_used; W->npix = M->npix; W->flags = M->flags;
+        for (int i = 0; i < 16; ++i) {
+            W->perm[i] = M->perm[i]; W->off[i] = M->off[i]; W->n[i] = M->n[i];
+            W->cat[i] = M->cat[i]; W->src[i] = M->src[i]; W->sizes[i] = M->sizes[i];
+        }
+    }
+    __syncthreads();
+}
+
+// plane owning location-map bit j (segments are concatenated in perm order)
+__device__ __forceinline__ int plane_of(const SliceWin& W, int j) {
+    for (int k = 0; k < W.s; ++k) {
+        const int p = W.perm[k];
+        if (j < W.cat[p] + W.n[p]) return p;
+    }
+    return -1;
+}
+
+// ------------------------------------------------------------------ K4: embed (window writes)
+template <typename Tin, typename Tout>
+__global__ __launch_bounds__(256) void k_embed(const Tin* __restrict__ cover, Tout* __restrict__ stego,
+                                               long long npx, uint32_t keep, const u64* __restrict__ payload,
+                                               int pw, const codec_slice_meta* __restrict__ meta,
+                                               u64* __restrict__ maps, int mw) {
+    __shared__ SliceWin W;
+    const int b = blockIdx.y;
+    load_win(meta + b, &W);
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if ((j & ~63) >= W.tot) return;   // whole wave past the end (uniform)
+    uint32_t mapbit = 0;
+    if (j < W.tot) {
+        const int p = plane_of(W, j);
+        const int i = j - W.cat[p];
+        long long q = (long long)W.off[p] + i;
+        if (q >= npx) q -= npx;
+        const long long sbit = (long long)W.src[p] + i;
+        const uint32_t mb = (uint32_t)(payload[(size_t)b * pw + (sbit >> 6)] >> (sbit & 63)) & 1u;
+        const uint32_t orig = cover[(size_t)b * npx + q];
+        mapbit = ((orig >> p) & 1u) ^ mb;
+        if (!(W.flags & CODEC_FLAG_OVERLAP)) {
+            stego[(size_t)b * npx + q] = (Tout)(((orig & keep) & ~(1u << p)) | (mb << p));
+        } else {
+            const size_t byte = ((size_t)b * npx + q) * sizeof(Tout);
+            uint32_t* word = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(stego) + (byte & ~(size_t)3));
+            const uint32_t bit = 1u << ((byte & 3) * 8 + p);
+            if (mb) atomicOr(word, bit); else atomicAnd(word, ~bit);
+        }
+    }
+    const u64 bal = __ballot(mapbit);
+    if ((threadIdx.x & 63) == 0) maps[(size_t)b * mw + (j >> 6)] = bal;
+}
+
+// ------------------------------------------------------------------ K5: extraction
+struct Range { int q0, q1, p, j0; };   // pixels [q0,q1) of plane p, map bit of q0 = j0
+
+__device__ int build_ranges(const SliceWin& W, Range* R) {
+    int k = 0;
+    for (int jj = 0; jj < W.s; ++jj) {
+        const int p = W.perm[jj];
+        const int n = W.n[p];
+        if (n <= 0) continue;
+        const int off = W.off[p];
+        const long long end = (long long)off + n;
+        if (end <= W.npix) {
+            R[k++] = Range{off, (int)end, p, W.cat[p]};
+        } else {
+            R[k++] = Range{off, W.npix, p, W.cat[p]};
+            R[k++] = Range{0, (int)(end - W.npix), p, W.cat[p] + (W.npix - off)};
+        }
+    }
+    return k;
+}
+
+__device__ __forceinline__ uint32_t map_bit(const u64* maps, long long j) {
+    return (uint32_t)(maps[j >> 6] >> (j & 63)) & 1u;
+}
+
+// cover = stego with every window bit XOR-ed with its location-map bit (stream copy)
+template <typename T>
+__global__ __launch_bounds__(256) void k_restore(const T* __restrict__ stego, T* __restrict__ cover, long long npx,
+                                                 const codec_slice_meta* __restrict__ meta,
+                                                 const u64* __restrict__ maps_all, int mw, long long chunks_per_wg) {
+    typedef typename Vec8<T>::type V;
+    __shared__ SliceWin W;
+    __shared__ Range rg[32];
+    __shared__ int nrg;
+    const int b = blockIdx.y;
+    load_win(meta + b, &W);
+    if (threadIdx.x == 0) nrg = build_ranges(W, rg);
+    __syncthreads();
+    const int nr = nrg;
+    const u64* maps = maps_all + (size_t)b * mw;
+    const long long nchunks = npx / 8;
+    const long long c0 = (long long)blockIdx.x * chunks_per_wg;
+    const long long c1 = min(nchunks, c0 + chunks_per_wg);
+    const V* src = reinterpret_cast<const V*>(stego + (size_t)b * npx);
+    V* dst = reinterpret_cast<V*>(cover + (size_t)b * npx);
+    for (long long ch = c0 + threadIdx.x; ch < c1; ch += 256) {
+        V v = src[ch];
+        const long long q0 = ch * 8;
+        for (int k = 0; k < nr; ++k) {
+            const Range r = rg[k];
+            if (q0 + 8 <= r.q0 || q0 >= r.q1) continue;
+            uint32_t px[8];
+            if constexpr (sizeof(T) == 2) {
+                px[0] = v.x & 0xFFFFu; px[1] = v.x >> 16; px[2] = v.y & 0xFFFFu; px[3] = v.y >> 16;
+                px[4] = v.z & 0xFFFFu; px[5] = v.z >> 16; px[6] = v.w & 0xFFFFu; px[7] = v.w >> 16;
+            } else {
+                for (int e = 0; e < 4; ++e) { px[e] = (v.x >> (8 * e)) & 0xFFu; px[4 + e] = (v.y >> (8 * e)) & 0xFFu; }
+            }
+            for (int e = 0; e < 8; ++e) {
+                const long long q = q0 + e;
+                if (q >= r.q0 && q < r.q1) px[e] ^= map_bit(maps, r.j0 + (q - r.q0)) << r.p;
+            }
+            if constexpr (sizeof(T) == 2) {
+                v.x = px[0] | (px[1] << 16); v.y = px[2] | (px[3] << 16);
+                v.z = px[4] | (px[5] << 16); v.w = px[6] | (px[7] << 16);
+            } else {
+                v.x = px[0] | (px[1] << 8) | (px[2] << 16) | (px[3] << 24);
+                v.y = px[4] | (px[5] << 8) | (px[6] << 16) | (px[7] << 24);
+            }
+        }
+        dst[ch] = v;
+    }
+    // scalar tail (npx % 8) handled by the last workgroup
+    if (blockIdx.x == gridDim.x - 1) {
+        for (long long q = nchunks * 8 + threadIdx.x; q < npx; q += 256) {
+            uint32_t px = stego[(size_t)b * npx + q];
+            for (int k = 0; k < nr; ++k) {
+                const Range r = rg[k];
+                if (q >= r.q0 && q < r.q1) px ^= map_bit(maps, r.j0 + (q - r.q0)) << r.p;
+            }
+            cover[(size_t)b * npx + q] = (T)px;
+        }
+    }
+}
+
+// scalar variant for slices whose rows are not 8-pixel aligned
+template <typename T>
+__global__ __launch_bounds__(256) void k_restore_scalar(const T* __restrict__ stego, T* __restrict__ cover,
+                                                        long long npx, const codec_slice_meta* __restrict__ meta,
+                                                        const u64* __restrict__ maps_all, int mw) {
+    __shared__ SliceWin W;
+    __shared__ Range rg[32];
+    __shared__ int nrg;
+    const int b = blockIdx.y;
+    load_win(meta + b, &W);
+    if (threadIdx.x == 0) nrg = build_ranges(W, rg);
+    __syncthreads();
+    const u64* maps = maps_all + (size_t)b * mw;
+    const long long stride = (long long)gridDim.x * 256;
+    for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < npx; q += stride) {
+        uint32_t px = stego[(size_t)b * npx + q];
+        for (int k = 0; k < nrg; ++k) {
+            const Range r = rg[k];
+            if (q >= r.q0 && q < r.q1) px ^= map_bit(maps, r.j0 + (q - r.q0)) << r.p;
+        }
+        cover[(size_t)b * npx + q] = (T)px;
+    }
+}
+
+// payload bits in segment order: bit j = stego bit p at the j-th window pixel
+template <typename T>
+__global__ __launch_bounds__(256) void k_gather(const T* __restrict__ stego, long long npx,
+                                                const codec_slice_meta* __restrict__ meta,
+                                                u64* __restrict__ out, int pw) {
+    __shared__ SliceWin W;
+    const int b = blockIdx.y;
+    load_win(meta + b, &W);
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if ((j & ~63) >= W.tot) return;
+    uint32_t bit = 0;
+    if (j < W.tot) {
+        const int p = plane_of(W, j);
+        const int i = j - W.cat[p];
+        long long q = (long long)W.off[p] + i;
+        if (q >= npx) q -= npx;
+        bit = (stego[(size_t)b * npx + q] >> p) & 1u;
+    }
+    const u64 bal = __ballot(bit);
+    if ((threadIdx.x & 63) == 0) out[(size_t)b * pw + (j >> 6)] = bal;
+}
+
+// ------------------------------------------------------------------ K6: reference decode
+// python `seq[:k]` length for a sequence of length `count`
+__device__ __forceinline__ int pyslice_take(int count, int k) {
+    if (k >= 0) return min(count, k);
+    return max(0, count + k);
+}
+
+// decode_message (codec.py:752-787) from packed maps: one workgroup per slice
+template <typename T>
+__global__ __launch_bounds__(256) void k_refdecode(const T* __restrict__ stego, long long npx,
+                                                   const codec_slice_meta* __restrict__ meta,
+                                                   const u64* __restrict__ maps_all, int mw,
+                                                   uint8_t* __restrict__ out_all, int cap,
+                                                   int32_t* __restrict__ counts) {
+    __shared__ SliceWin W;
+    __shared__ uint32_t sh[8];
+    const int b = blockIdx.x;
+    load_win(meta + b, &W);
+    const u64* maps = maps_all + (size_t)b * mw;
+    uint8_t* out = out_all + (size_t)b * cap;
+    const T* img = stego + (size_t)b * npx;
+    int outpos = 0;
+    for (int p = 0; p < W.s; ++p) {                        // plane-index order (codec.py:776)
+        const int n = W.n[p];
+        uint32_t local = 0;
+        for (int i = threadIdx.x; i < n; i += 256) local += map_bit(maps, (long long)W.cat[p] + i);
+        const uint32_t count = block_sum_u32<256>(local, sh);
+        const int K = pyslice_take((int)count, W.sizes[p]);   // [:segments_lengths[p]]
+        const int rs = ((long long)W.off[p] + n > npx) ? (int)(npx - W.off[p]) : 0;
+        uint32_t running = 0;
+        for (int base = 0; base < n && (int)running < K; base += 256) {
+            const int r = base + threadIdx.x;
+            uint32_t bit = 0;
+            int i = 0;
+            if (r < n) {
+                i = r + rs;
+                if (i >= n) i -= n;
+                bit = map_bit(maps, (long long)W.cat[p] + i);
+            }
+            uint32_t tot;
+            const uint32_t rank = running + block_excl_scan<256>(bit, sh, &tot);
+            if (bit && (int)rank < K && outpos + (int)rank < cap) {
+                long long q = (long long)W.off[p] + i;
+                if (q >= npx) q -= npx;
+                out[outpos + rank] = (uint8_t)((img[q] >> p) & 1u);
+            }
+            running += tot;
+        }
+        outpos += K;
+    }
+    if (threadIdx.x == 0) counts[b] = outpos;
+}
+
+// dense variant, phase A: non-zero count per (slice, plane)
+__global__ __launch_bounds__(1024) void k_dense_count(const uint8_t* __restrict__ dense, int smax, long long npx,
+                                                      const codec_slice_meta* __restrict__ meta,
+                                                      int32_t* __restrict__ nzcount) {
+    __shared__ uint32_t sh[20];
+    const int p = blockIdx.x, b = blockIdx.y;
+    if (p >= meta[b].s) return;
+    const uint8_t* d = dense + ((size_t)b * smax + p) * npx;
+    uint32_t local = 0;
+    for (long long q = threadIdx.x; q < npx; q += 1024) local += d[q] != 0;
+    const uint32_t tot = block_sum_u32<1024>(local, sh);
+    if (threadIdx.x == 0) nzcount[b * 16 + p] = (int32_t)tot;
+}
+
+// dense variant, phase B: ordered compaction of the first K non-zero positions
+template <typename T>
+__global__ __launch_bounds__(1024) void k_dense_emit(const T* __restrict__ src, int src_is_planes,
+                                                     const uint8_t* __restrict__ dense, int smax, long long npx,
+                                                     const codec_slice_meta* __restrict__ meta,
+                                                     const int32_t* __restrict__ nzcount,
+                                                     uint8_t* __restrict__ out_all, int cap,
+                                                     int32_t* __restrict__ counts) {
+    __shared__ uint32_t sh[20];
+    const int p = blockIdx.x, b = blockIdx.y;
+    const codec_slice_meta* M = meta + b;
+    const int s = M->s;
+    if (p >= s) return;
+    int outpos = 0, K = 0, total = 0;
+    for (int pp = 0; pp < s; ++pp) {
+        const int k = pyslice_take(nzcount[b * 16 + pp], M->sizes[pp]);
+        if (pp < p) outpos += k;
+        if (pp == p) K = k;
+        total += k;
+    }
+    if (p == s - 1 && threadIdx.x == 0) counts[b] = total;
+    const uint8_t* d = dense + ((size_t)b * smax + p) * npx;
+    uint8_t* out = out_all + (size_t)b * cap;
+    uint32_t running = 0;
+    for (long long base = 0; base < npx && (int)running < K; base += 1024) {
+        const long long q = base + threadIdx.x;
+        const uint32_t bit = (q < npx && d[q] != 0) ? 1u : 0u;
+        uint32_t tot;
+        const uint32_t rank = running + block_excl_scan<1024>(bit, sh, &tot);
+        if (bit && (int)rank < K && outpos + (int)rank < cap) {
+            uint32_t v;
+            if (src_is_planes) v = src[((size_t)b * smax + p) * npx + q] & 1u;
+            else v = (src[(size_t)b * npx + q] >> p) & 1u;
+            out[outpos + rank] = (uint8_t)v;
+        }
+        running += tot;
+    }
+}
+
+// ------------------------------------------------------------------ K7: dense helpers
+__global__ __launch_bounds__(256) void k_expand(const u64* __restrict__ maps_all, int mw,
+                                                const codec_slice_meta* __restrict__ meta,
+                                                uint8_t* __restrict__ dense, int smax, long long npx) {
+    __shared__ SliceWin W;
+    __shared__ Range rg[32];
+    __shared__ int nrg;
+    const int p = blockIdx.y, b = blockIdx.z;
+    load_win(meta + b, &W);
+    if (threadIdx.x == 0) {
+        Range all[32];
+        const int k = build_ranges(W, all);
+        int c = 0;
+        for (int i = 0; i < k; ++i)
+            if (all[i].p == p) rg[c++] = all[i];
+        nrg = c;
+    }
+    __syncthreads();
+    const u64* maps = maps_all + (size_t)b * mw;
+    uint8_t* d = dense + ((size_t)b * smax + p) * npx;
+    const long long stride = (long long)gridDim.x * 256;
+    for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < npx; q += stride) {
+        uint8_t v = 0;
+        if (p < W.s) {
+            for (int k = 0; k < nrg; ++k)
+                if (q >= rg[k].q0 && q < rg[k].q1) v = (uint8_t)map_bit(maps, rg[k].j0 + (q - rg[k].q0));
+        }
+        d[q] = v;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_restore_dense(const T* __restrict__ stego, const uint8_t* __restrict__ dense,
+                                                       int smax, long long npx,
+                                                       const codec_slice_meta* __restrict__ meta,
+                                                       T* __restrict__ cover) {
+    const int b = blockIdx.y;
+    const int s = meta[b].s;
+    const long long stride = (long long)gridDim.x * 256;
+    for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < npx; q += stride) {
+        uint32_t v = stego[(size_t)b * npx + q];
+        for (int p = 0; p < s; ++p) v ^= (uint32_t)(dense[((size_t)b * smax + p) * npx + q] & 1u) << p;
+        cover[(size_t)b * npx + q] = (T)v;
+    }
+}
+
+template <typename Tin, typename Tout>
+__global__ __launch_bounds__(256) void k_unpack(const Tin* __restrict__ img, long long npx, int first, int count,
+                                                Tout* __restrict__ planes) {
+    const int b = blockIdx.y;
+    const long long stride = (long long)gridDim.x * 256;
+    for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < npx; q += stride) {
+        const uint32_t v = img[(size_t)b * npx + q];
+        for (int k = 0; k < count; ++k) {
+            const int sh = first + k;
+            planes[((size_t)b * count + k) * npx + q] = (Tout)(sh < 32 ? (v >> sh) & 1u : 0u);
+        }
+    }
+}
+
+template <typename Tp, typename Tout>
+__global__ __launch_bounds__(256) void k_merge(const Tp* __restrict__ planes, int nplanes, long long npx,
+                                               Tout* __restrict__ out) {
+    const int b = blockIdx.y;
+    const long long stride = (long long)gridDim.x * 256;
+    for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < npx; q += stride) {
+        uint32_t acc = 0;
+        for (int k = 0; k < nplanes && k < 8 * (int)sizeof(Tout); ++k) {
+            const uint32_t pv = (Tout)planes[((size_t)b * nplanes + k) * npx + q];
+            acc |= (uint32_t)(Tout)(pv << k);
+        }
+        out[(size_t)b * npx + q] = (Tout)acc;
+    }
+}
+
+// ====================================================================== host side
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+static int check_params(const codec_params* P) {
+    if (!P) return set_err(CODEC_EINVAL, "params is NULL");
+    if (P->B < 1 || P->H < 1 || P->W < 1) return set_err(CODEC_EINVAL, "bad shape B=%d H=%d W=%d", P->B, P->H, P->W);
+    if ((long long)P->H * P->W > 0x7FFFFFFFLL) return set_err(CODEC_EINVAL, "H*W must fit int32");
+    if (P->in_bytes != 1 && P->in_bytes != 2) return set_err(CODEC_EINVAL, "in_bytes must be 1 or 2");
+    if (P->out_bytes != 1 && P->out_bytes != 2) return set_err(CODEC_EINVAL, "out_bytes must be 1 or 2");
+    if (P->nbits < 1 || P->nbits > 16) return set_err(CODEC_EINVAL, "nbits must be in 1..16");
+    if (P->block < 1) return set_err(CODEC_EINVAL, "block must be >= 1");
+    if (P->mode != CODEC_MODE_HYBRID && P->mode != CODEC_MODE_MULTI) return set_err(CODEC_EINVAL, "bad mode");
+    if (P->fixed_s > 16) return set_err(CODEC_EINVAL, "fixed_s must be <= 16");
+    if (P->fixed_offset >= 0 && (long long)P->fixed_offset >= (long long)P->H * P->W)
+        return set_err(CODEC_EINVAL, "fixed_offset out of range");
+    return 0;
+}
+
+static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+static bool pow2_fast_block(int b) { return b == 8 || b == 16 || b == 32 || b == 64; }
+
+static bool use_fast_scan(const codec_params* P, const void* cover, const void* stego) {
+    const size_t va = P->in_bytes == 2 ? 16 : 8;
+    return (P->W % 8) == 0 && pow2_fast_block(P->block) && P->in_bytes == P->out_bytes &&
+           P->nbits >= 8 * P->in_bytes && ((uintptr_t)cover % va) == 0 && ((uintptr_t)stego % va) == 0;
+}
+
+static int host_exact_count(const codec_params* P, bool edge_only) {
+    const int sb = P->block;
+    const int nby = (P->H + sb - 1) / sb, nbx = (P->W + sb - 1) / sb;
+    if (!edge_only) return nby * nbx;
+    const int ncol = (P->W % sb) ? nby : 0;
+    const int nrow = (P->H % sb) ? (nbx - ((P->W % sb) ? 1 : 0)) : 0;
+    return ncol + nrow;
+}
+
+struct WsLayout {
+    size_t hist, keys, exact, total;
+    int exact_cap;
+};
+
+static WsLayout ws_layout(const codec_params* P) {
+    WsLayout L;
+    const size_t R = P->in_bytes == 2 ? 65536 : 256;
+    // capacity for the worst case (generic path: every block exact)
+    const int cap = host_exact_count(P, false);
+    L.exact_cap = cap > 0 ? cap : 1;
+    L.hist = 0;
+    L.keys = align_up(L.hist + (size_t)P->B * R * 4, 256);
+    L.exact = align_up(L.keys + (size_t)P->B * 8, 256);
+    L.total = align_up(L.exact + (size_t)P->B * L.exact_cap * 8, 256);
+    return L;
+}
+
+extern "C" {
+
+int codec_abi_version(void) { return CODEC_ABI_VERSION; }
+
+int codec_profile_begin(int32_t capacity) {
+    if (g_prof.ev) return set_err(CODEC_EINVAL, "profile window already open");
+    if (capacity < 1) return set_err(CODEC_EINVAL, "capacity must be >= 1");
+    g_prof.ev = new hipEvent_t[2 * (size_t)capacity];
+    g_prof.tag = new int32_t[capacity];
+    for (int i = 0; i < 2 * capacity; ++i) HIP_TRY(hipEventCreate(&g_prof.ev[i]));
+    g_prof.cap = capacity;
+    g_prof.n = 0;
+    return 0;
+}
+
+int codec_profile_end(float* ms, int32_t* tag, int32_t capacity) {
+    if (!g_prof.ev) return set_err(CODEC_EINVAL, "no profile window open");
+    const int n = g_prof.n < capacity ? g_prof.n : capacity;
+    int rc = 0;
+    for (int i = 0; i < n; ++i) {
+        float t = 0.f;
+        hipError_t e = hipEventElapsedTime(&t, g_prof.ev[2 * i], g_prof.ev[2 * i + 1]);
+        if (e != hipSuccess && rc == 0) rc = set_err(-(int)e, "hipEventElapsedTime: %s", hipGetErrorString(e));
+        if (ms) ms[i] = t;
+        if (tag) tag[i] = g_prof.tag[i];
+    }
+    for (int i = 0; i < 2 * g_prof.cap; ++i) hipEventDestroy(g_prof.ev[i]);
+    delete[] g_prof.ev;
+    delete[] g_prof.tag;
+    g_prof = ProfWin();
+    return rc ? rc : n;
+}
+
+const char* codec_last_error(void) { return g_err; }
+
+size_t codec_workspace_bytes(const codec_params* P) {
+    if (check_params(P)) return 0;
+    return ws_layout(P).total;
+}
+
+}  // extern "C"
+
+template <typename T>
+static int launch_scan_fast(const codec_params* P, const void* cover, void* stego, uint32_t* hist, u64* keys,
+                            hipStream_t st) {
+    const int sb = P->block;
+    const int nb = (P->H + sb - 1) / sb;
+    const int target = sizeof(T) == 2 ? 256 : 1024;
+    int wgps = (target + P->B - 1) / P->B;
+    wgps = wgps < 1 ? 1 : (wgps > nb ? nb : wgps);
+    const int bpw = (nb + wgps - 1) / wgps;
+    wgps = (nb + bpw - 1) / bpw;
+    dim3 grid(wgps, P->B);
+    const T* c = static_cast<const T*>(cover);
+    T* s = static_cast<T*>(stego);
+    ProfScope prof(st, CODEC_K_SCAN_FAST);
+    switch (sb) {
+        case 8: hipLaunchKernelGGL((k_scan_fast<T, 8>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys); break;
+        case 16: hipLaunchKernelGGL((k_scan_fast<T, 16>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys); break;
+        case 32: hipLaunchKernelGGL((k_scan_fast<T, 32>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys); break;
+        default: hipLaunchKernelGGL((k_scan_fast<T, 64>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys); break;
+    }
+    LAUNCH_CHECK("k_scan_fast");
+    return 0;
+}
+
+template <typename Tin, typename Tout>
+static int launch_scan_generic(const codec_params* P, const void* cover, void* stego, uint32_t* hist, hipStream_t st) {
+    const long long npx = (long long)P->H * P->W;
+    const int target = sizeof(Tin) == 2 ? 256 : 1024;
+    long long wgps = (target + P->B - 1) / P->B;
+    long long per = (npx + wgps - 1) / wgps;
+    if (per < 4096) per = 4096;
+    wgps = (npx + per - 1) / per;
+    const uint32_t keep = P->nbits >= 32 ? 0xFFFFFFFFu : ((1u << P->nbits) - 1u);
+    ProfScope prof(st, CODEC_K_SCAN_GENERIC);
+    hipLaunchKernelGGL((k_scan_generic<Tin, Tout>), dim3((unsigned)wgps, P->B), dim3(1024), 0, st,
+                       static_cast<const Tin*>(cover), static_cast<Tout*>(stego), npx, per, keep, hist);
+    LAUNCH_CHECK("k_scan_generic");
+    return 0;
+}
+
+extern "C" {
+
+int codec_plan(const codec_params* P, const void* cover, void* stego, const double* log2_lut, int64_t lut_len,
+               const codec_layout* table, const int32_t* slice_class, codec_slice_meta* meta, void* workspace,
+               size_t workspace_bytes, void* stream) {
+    int rc = check_params(P);
+    if (rc) return rc;
+    if (!cover || !log2_lut || !table || !slice_class || !meta || !workspace)
+        return set_err(CODEC_EINVAL, "codec_plan: NULL pointer argument");
+    const WsLayout L = ws_layout(P);
+    if (workspace_bytes < L.total) return set_err(CODEC_EINVAL, "workspace too small (%zu < %zu)", workspace_bytes, L.total);
+    if (lut_len < (int64_t)P->H * P->W) return set_err(CODEC_EINVAL, "log2 table shorter than H*W");
+    if (P->n_classes < 1) return set_err(CODEC_EINVAL, "n_classes must be >= 1");
+    hipStream_t st = as_stream(stream);
+    char* ws = static_cast<char*>(workspace);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(ws + L.hist);
+    u64* keys = reinterpret_cast<u64*>(ws + L.keys);
+    double* exact = reinterpret_cast<double*>(ws + L.exact);
+    HIP_TRY(hipMemsetAsync(ws, 0, L.exact, st));   // histograms + block keys
+
+    const bool fast = use_fast_scan(P, cover, stego ? stego : cover);
+    if (fast) {
+        rc = P->in_bytes == 2 ? launch_scan_fast<uint16_t>(P, cover, stego, hist, keys, st)
+                              : launch_scan_fast<uint8_t>(P, cover, stego, hist, keys, st);
+    } else if (P->in_bytes == 2) {
+        rc = P->out_bytes == 2 ? launch_scan_generic<uint16_t, uint16_t>(P, cover, stego, hist, st)
+                               : launch_scan_generic<uint16_t, uint8_t>(P, cover, stego, hist, st);
+    } else {
+        rc = P->out_bytes == 2 ? launch_scan_generic<uint8_t, uint16_t>(P, cover, stego, hist, st)
+                               : launch_scan_generic<uint8_t, uint8_t>(P, cover, stego, hist, st);
+    }
+    if (rc) return rc;
+
+    const bool need_blocks = P->mode == CODEC_MODE_HYBRID && P->fixed_offset < 0;
+    const int edge_only = fast ? 1 : 0;
+    const int ecount = need_blocks ? host_exact_count(P, fast) : 0;
+    if (ecount > 0) {
+        dim3 grid((ecount + 255) / 256, P->B);
+        ProfScope prof(st, CODEC_K_BLOCK_EXACT);
+        if (P->in_bytes == 2)
+            hipLaunchKernelGGL(k_block_exact<uint16_t>, grid, dim3(256), 0, st, static_cast<const uint16_t*>(cover),
+                               P->H, P->W, P->block, edge_only, exact, L.exact_cap);
+        else
+            hipLaunchKernelGGL(k_block_exact<uint8_t>, grid, dim3(256), 0, st, static_cast<const uint8_t*>(cover),
+                               P->H, P->W, P->block, edge_only, exact, L.exact_cap);
+        LAUNCH_CHECK("k_block_exact");
+    }
+    const codec_params Pv = *P;
+    ProfScope prof(st, CODEC_K_DECIDE);
+    if (P->in_bytes == 2)
+        hipLaunchKernelGGL(k_decide<uint16_t>, dim3(P->B), dim3(1024), 0, st, Pv, hist, keys, exact, L.exact_cap,
+                           edge_only, fast ? 1 : 0, log2_lut, (long long)lut_len, table, slice_class, meta);
+    else
+        hipLaunchKernelGGL(k_decide<uint8_t>, dim3(P->B), dim3(1024), 0, st, Pv, hist, keys, exact, L.exact_cap,
+                           edge_only, fast ? 1 : 0, log2_lut, (long long)lut_len, table, slice_class, meta);
+    LAUNCH_CHECK("k_decide");
+    return 0;
+}
+
+int codec_embed(const codec_params* P, const void* cover, void* stego, const uint64_t* payload,
+                const codec_slice_meta* meta, uint64_t* maps, void* stream) {
+    int rc = check_params(P);
+    if (rc) return rc;
+    if (!cover || !stego || !payload || !meta || !maps) return set_err(CODEC_EINVAL, "codec_embed: NULL pointer argument");
+    if (P->payload_words < 1 || P->map_words < 1) return set_err(CODEC_EINVAL, "payload_words/map_words must be >= 1");
+    if ((uintptr_t)stego % 4) return set_err(CODEC_EINVAL, "stego must be 4-byte aligned");
+    const long long npx = (long long)P->H * P->W;
+    // every embedded bit has a map bit: total_used <= map_words*64 (host-sized)
+    const long long maxbits = (long long)P->map_words * 64;
+    dim3 grid((unsigned)((maxbits + 255) / 256), P->B);
+    const uint32_t keep = (1u << P->nbits) - 1u;
+    hipStream_t st = as_stream(stream);
+    ProfScope prof(st, CODEC_K_EMBED);
+#define EMB(TI, TO)                                                                                       \
+    hipLaunchKernelGGL((k_embed<TI, TO>), grid, dim3(256), 0, st, static_cast<const TI*>(cover),          \
+                       static_cast<TO*>(stego), npx, keep, reinterpret_cast<const u64*>(payload), P->payload_words, meta, reinterpret_cast<u64*>(maps), P->map_words)
+    if (P->in_bytes == 2 && P->out_bytes == 2) EMB(uint16_t, uint16_t);
+    else if (P->in_bytes == 2) EMB(uint16_t, uint8_t);
+    else if (P->out_bytes == 2) EMB(uint8_t, uint16_t);
+    else EMB(uint8_t, uint8_t);
+#undef EMB
+    LAUNCH_CHECK("k_embed");
+    return 0;
+}
+
+int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps, const codec_slice_meta* meta,
+                  void* cover_out, uint64_t* payload_out, void* stream) {
+    int rc = check_params(P);
+    if (rc) return rc;
+    if (!stego || !maps || !meta) return set_err(CODEC_EINVAL, "codec_extract: NULL pointer argument");
+    if (P->in_bytes != P->out_bytes) return set_err(CODEC_EINVAL, "codec_extract: stego and cover share a dtype");
+    const long long npx = (long long)P->H * P->W;
+    hipStream_t st = as_stream(stream);
+    if (cover_out) {
+        const size_t va = P->in_bytes == 2 ? 16 : 8;
+        if ((uintptr_t)stego % va || (uintptr_t)cover_out % va || ((npx * P->in_bytes) % va)) {
+            long long gx = (npx + 255) / 256;
+            if (gx > 2048) gx = 2048;
+            dim3 grid((unsigned)gx, P->B);
+            if (P->in_bytes == 2)
+                hipLaunchKernelGGL(k_restore_scalar<uint16_t>, grid, dim3(256), 0, st, static_cast<const uint16_t*>(stego),
+                                   static_cast<uint16_t*>(cover_out), npx, meta, reinterpret_cast<const u64*>(maps), P->map_words);
+            else
+                hipLaunchKernelGGL(k_restore_scalar<uint8_t>, grid, dim3(256), 0, st, static_cast<const uint8_t*>(stego),
+                                   static_cast<uint8_t*>(cover_out), npx, meta, reinterpret_cast<const u64*>(maps), P->map_words);
+            LAUNCH_CHECK("k_restore_scalar");
+        } else {
+        const long long nchunks = npx / 8;
+        long long wgps = (2048 + P->B - 1) / P->B;
+        long long per = (nchunks + wgps - 1) / wgps;
+        if (per < 1024) per = 1024;
+        wgps = (nchunks + per - 1) / per;
+        if (wgps < 1) wgps = 1;
+        dim3 grid((unsigned)wgps, P->B);
+        ProfScope prof(st, CODEC_K_RESTORE);
+        if (P->in_bytes == 2)
+            hipLaunchKernelGGL(k_restore<uint16_t>, grid, dim3(256), 0, st, static_cast<const uint16_t*>(stego),
+                               static_cast<uint16_t*>(cover_out), npx, meta, reinterpret_cast<const u64*>(maps), P->map_words, per);
+        else
+            hipLaunchKernelGGL(k_restore<uint8_t>, grid, dim3(256), 0, st, static_cast<const uint8_t*>(stego),
+                               static_cast<uint8_t*>(cover_out), npx, meta, reinterpret_cast<const u64*>(maps), P->map_words, per);
+        LAUNCH_CHECK("k_restore");
+        }
+    }
+    if (payload_out) {
+        if (P->payload_words < 1) return set_err(CODEC_EINVAL, "payload_words must be >= 1");
+        const long long maxbits = (long long)P->payload_words * 64;
+        dim3 grid((unsigned)((maxbits + 255) / 256), P->B);
+        HIP_TRY(hipMemsetAsync(payload_out, 0, (size_t)P->B * P->payload_words * 8, st));
+        ProfScope prof(st, CODEC_K_GATHER);
+        if (P->in_bytes == 2)
+            hipLaunchKernelGGL(k_gather<uint16_t>, grid, dim3(256), 0, st, static_cast<const uint16_t*>(stego), npx,
+                               meta, reinterpret_cast<u64*>(payload_out), P->payload_words);
+        else
+            hipLaunchKernelGGL(k_gather<uint8_t>, grid, dim3(256), 0, st, static_cast<const uint8_t*>(stego), npx,
+                               meta, reinterpret_cast<u64*>(payload_out), P->payload_words);
+        LAUNCH_CHECK("k_gather");
+    }
+    return 0;
+}
+
+int codec_refdecode(const codec_params* P, const void* stego, const uint64_t* maps, const codec_slice_meta* meta,
+                    uint8_t* bits_out, int32_t bits_cap, int32_t* counts_out, void* stream) {
+    int rc = check_params(P);
+    if (rc) return rc;
+    if (!stego || !maps || !meta || !bits_out || !counts_out || bits_cap < 1)
+        return set_err(CODEC_EINVAL, "codec_refdecode: bad arguments");
+    const long long npx = (long long)P->H * P->W;
+    hipStream_t st = as_stream(stream);
+    if (P->out_bytes == 2)
+        hipLaunchKernelGGL(k_refdecode<uint16_t>, dim3(P->B), dim3(256), 0, st, static_cast<const uint16_t*>(stego), npx,
+                           meta, reinterpret_cast<const u64*>(maps), P->map_words, bits_out, bits_cap, counts_out);
+    else
+        hipLaunchKernelGGL(k_refdecode<uint8_t>, dim3(P->B), dim3(256), 0, st, static_cast<const uint8_t*>(stego), npx,
+                           meta, reinterpret_cast<const u64*>(maps), P->map_words, bits_out, bits_cap, counts_out);
+    LAUNCH_CHECK("k_refdecode");
+    return 0;
+}
+
+int codec_refdecode_dense(const codec_params* P, const void* src, int32_t src_is_planes, const uint8_t* dense,
+                          int32_t smax, const codec_slice_meta* meta, uint8_t* bits_out, int32_t bits_cap,
+                          int32_t* counts_out, void* stream) {
+    int rc = check_params(P);
+    if (rc) return rc;
+    if (!src || !dense || !meta || !bits_out || !counts_out || bits_cap < 1 || smax < 1 || smax > 16)
+        return set_err(CODEC_EINVAL, "codec_refdecode_dense: bad arguments");
+    const long long npx = (long long)P->H * P->W;
+    hipStream_t st = as_stream(stream);
+    // counts_out holds B*17 int32: [0,B) bit counts, then B*16 per-plane non-zero counts (scratch)
+    int32_t* nz = counts_out + P->B;
+    hipLaunchKernelGGL(k_dense_count, dim3(smax, P->B), dim3(1024), 0, st, dense, smax, npx, meta, nz);
+    LAUNCH_CHECK("k_dense_count");
+    if (P->in_bytes == 2)
+        hipLaunchKernelGGL(k_dense_emit<uint16_t>, dim3(smax, P->B), dim3(1024), 0, st, static_cast<const uint16_t*>(src),
+                           src_is_planes, dense, smax, npx, meta, nz, bits_out, bits_cap, counts_out);
+    else
+        hipLaunchKernelGGL(k_dense_emit<uint8_t>, dim3(smax, P->B), dim3(1024), 0, st, static_cast<const uint8_t*>(src),
+                           src_is_planes, dense, smax, npx, meta, nz, bits_out, bits_cap, counts_out);
+    LAUNCH_CHECK("k_dense_emit");
+    return 0;
+}
+
+int codec_expand_maps(const codec_params* P, const uint64_t* maps, const codec_slice_meta* meta, uint8_t* dense,
+                      int32_t smax, void* stream) {
+    int rc = check_params(P);
+    if (rc) return rc;
+    if (!maps || !meta || !dense || smax < 1 || smax > 16) return set_err(CODEC_EINVAL, "codec_expand_maps: bad arguments");
+    const long long npx = (long long)P->H * P->W;
+    long long gx = (npx + 255) / 256;
+    if (gx > 1024) gx = 1024;
+    hipLaunchKernelGGL(k_expand, dim3((unsigned)gx, smax, P->B), dim3(256), 0, as_stream(stream), reinterpret_cast<const u64*>(maps), P->map_words,
+                       meta, dense, smax, npx);
+    LAUNCH_CHECK("k_expand");
+    return 0;
+}
+
+int codec_restore_dense(const codec_params* P, const void* stego, const uint8_t* dense, int32_t smax,
+                        const codec_slice_meta* meta, void* cover_out, void* stream) {
+    int rc = check_params(P);
+    if (rc) return rc;
+    if (!stego || !dense || !meta || !cover_out || smax < 1 || smax > 16)
+        return set_err(CODEC_EINVAL, "codec_restore_dense: bad arguments");
+    const long long npx = (long long)P->H * P->W;
+    long long gx = (npx + 255) / 256;
+    if (gx > 2048) gx = 2048;
+    dim3 grid((unsigned)gx, P->B);
+    if (P->in_bytes == 2)
+        hipLaunchKernelGGL(k_restore_dense<uint16_t>, grid, dim3(256), 0, as_stream(stream),
+                           static_cast<const uint16_t*>(stego), dense, smax, npx, meta, static_cast<uint16_t*>(cover_out));
+    else
+        hipLaunchKernelGGL(k_restore_dense<uint8_t>, grid, dim3(256), 0, as_stream(stream),
+                           static_cast<const uint8_t*>(stego), dense, smax, npx, meta, static_cast<uint8_t*>(cover_out));
+    LAUNCH_CHECK("k_restore_dense");
+    return 0;
+}
+
+int codec_unpack_planes(const codec_params* P, const void* img, int32_t first, int32_t count, void* planes,
+                        int32_t plane_bytes, void* stream) {
+    if (!P || P->B < 1 || P->H < 1 || P->W < 1 || (P->in_bytes != 1 && P->in_bytes != 2))
+        return set_err(CODEC_EINVAL, "codec_unpack_planes: bad params");
+    if (!img || !planes || first < 0 || count < 1 || (plane_bytes != 1 && plane_bytes != 2))
+        return set_err(CODEC_EINVAL, "codec_unpack_planes: bad arguments");
+    const long long npx = (long long)P->H * P->W;
+    long long gx = (npx + 255) / 256;
+    if (gx > 2048) gx = 2048;
+    dim3 grid((unsigned)gx, P->B);
+    hipStream_t st = as_stream(stream);
+#define UNP(TI, TO) hipLaunchKernelGGL((k_unpack<TI, TO>), grid, dim3(256), 0, st, static_cast<const TI*>(img), npx, first, count, static_cast<TO*>(planes))
+    if (P->in_bytes == 2 && plane_bytes == 2) UNP(uint16_t, uint16_t);
+    else if (P->in_bytes == 2) UNP(uint16_t, uint8_t);
+    else if (plane_bytes == 2) UNP(uint8_t, uint16_t);
+    else UNP(uint8_t, uint8_t);
+#undef UNP
+    LAUNCH_CHECK("k_unpack");
+    return 0;
+}
+
+int codec_merge_planes(const codec_params* P, const void* planes, int32_t nplanes, int32_t plane_bytes, void* out,
+                       void* stream) {
+    if (!P || P->B < 1 || P->H < 1 || P->W < 1 || (P->out_bytes != 1 && P->out_bytes != 2))
+        return set_err(CODEC_EINVAL, "codec_merge_planes: bad params");
+    if (!planes || !out || nplanes < 1 || (plane_bytes != 1 && plane_bytes != 2))
+        return set_err(CODEC_EINVAL, "codec_merge_planes: bad arguments");
+    const long long npx = (long long)P->H * P->W;
+    long long gx = (npx + 255) / 256;
+    if (gx > 2048) gx = 2048;
+    dim3 grid((unsigned)gx, P->B);
+    hipStream_t st = as_stream(stream);
+#define MRG(TP, TO) hipLaunchKernelGGL((k_merge<TP, TO>), grid, dim3(256), 0, st, static_cast<const TP*>(planes), nplanes, npx, static_cast<TO*>(out))
+    if (plane_bytes == 2 && P->out_bytes == 2) MRG(uint16_t, uint16_t);
+    else if (plane_bytes == 2) MRG(uint16_t, uint8_t);
+    else if (P->out_bytes == 2) MRG(uint8_t, uint16_t);
+    else MRG(uint8_t, uint8_t);
+#undef MRG
+    LAUNCH_CHECK("k_merge");
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,180 @@
+/*
+ * codec_tcc.h -- C ABI of libcodec_hip.so, the MI355X (gfx950) implementation of the
+ * reference's LSB bit-plane embed/extract pixel path (wesleyfn/codec-tcc, src/codec.py).
+ *
+ * Boundary contract (mirrors the reference's Python function boundary):
+ *   - every pointer argument is a DEVICE pointer owned by the caller (torch tensors);
+ *     `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream);
+ *   - every call is asynchronous on `stream`, stateless and thread-safe given distinct
+ *     streams and buffers; nothing is allocated inside (workspace is caller-provided);
+ *   - return value: 0 on success, < 0 on error (argument error or negated hipError_t);
+ *     codec_last_error() returns a thread-local message.  The Python host layer turns a
+ *     non-zero status into an exception, as the reference raises ValueError (codec.py:34-37).
+ *
+ * Pixel layout in HBM: a batch of B slices, each H x W row-major, slices contiguous
+ * ([B][H][W]), uint8 or uint16 little-endian.  Location maps and payloads are packed
+ * bitstrings, LSB-first inside uint64 words, one fixed-size row of words per slice.
+ */
+#ifndef CODEC_TCC_H
+#define CODEC_TCC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CODEC_ABI_VERSION 1
+#define CODEC_MAX_PLANES 16
+
+/* Embedder variants (reference functions they reproduce). */
+#define CODEC_MODE_HYBRID 0 /* lsb_embed_block_then_multiplane, codec.py:412-487 */
+#define CODEC_MODE_MULTI 1  /* lsb_embed_multi_plane,           codec.py:276-318 */
+
+/* codec_slice_meta.flags */
+#define CODEC_FLAG_OVERLAP 1u   /* windows of different planes may share pixels   */
+#define CODEC_FLAG_LOSSY 2u     /* segments do not tile the payload (T < s, clamp) */
+#define CODEC_FLAG_BADLUT 4u    /* log2 table shorter than H*W (status error)      */
+
+/* Call parameters (one batch: all slices share shape and dtype). */
+typedef struct codec_params {
+    int32_t B, H, W;
+    int32_t in_bytes;      /* cover dtype: 1 = uint8, 2 = uint16                         */
+    int32_t out_bytes;     /* stego dtype: merge_modalities rule, codec.py:221           */
+    int32_t nbits;         /* bit planes examined, codec.py:567 (1..16)                  */
+    int32_t block;         /* search_block_size, codec.py:412,435 (>= 1)                 */
+    int32_t align;         /* align_across_planes, codec.py:412,484                      */
+    int32_t mode;          /* CODEC_MODE_*                                               */
+    int32_t fixed_s;       /* > 0: use this s instead of the decision (codec.py:584-593) */
+    int32_t fixed_offset;  /* >= 0: use this start offset instead of the block search    */
+    int32_t all_mi;        /* 1: evaluate MI of every plane (diagnostics), s unchanged   */
+    int32_t payload_words; /* uint64 words per slice in payload buffers                  */
+    int32_t map_words;     /* uint64 words per slice in location-map buffers             */
+    int32_t n_classes;     /* rows of the layout table / 16                              */
+    int32_t reserved;
+    double beta;           /* retention target, codec.py:561,575                         */
+} codec_params;
+
+/* Segment plan for one (payload length T, plane count s), built on the host by the
+ * reference's own rule (distribute_message_segments, codec.py:242-274). Indexed by
+ * destination plane p except perm, which is the segment order (segment_indices). */
+typedef struct codec_layout {
+    int32_t sizes[CODEC_MAX_PLANES]; /* distributed_sizes[p]  (codec.py:253-259)          */
+    int32_t perm[CODEC_MAX_PLANES];  /* segment_indices[j]    (codec.py:262-264)          */
+    int32_t src[CODEC_MAX_PLANES];   /* first payload bit of plane p's segment (slice)    */
+    int32_t len[CODEC_MAX_PLANES];   /* len(segment) of plane p (python slice semantics) */
+} codec_layout;
+
+/* Per-slice result record (fixed size; this is what the multi-GPU path all-gathers). */
+typedef struct codec_slice_meta {
+    int32_t s;            /* number of local planes                                  */
+    int32_t start_offset; /* raster offset of the best block, codec.py:453          */
+    int32_t total_used;   /* sum of embedded bits, codec.py:480                      */
+    uint32_t flags;       /* CODEC_FLAG_*                                            */
+    int32_t npix;         /* H*W                                                     */
+    int32_t nbits;
+    int32_t status;       /* 0 ok                                                    */
+    int32_t nonzero_bins; /* distinct pixel values                                   */
+    int32_t perm[CODEC_MAX_PLANES];  /* segment_indices                             */
+    int32_t sizes[CODEC_MAX_PLANES]; /* segments_lengths as the reference returns them */
+    int32_t n[CODEC_MAX_PLANES];     /* bits embedded in plane p (window length)     */
+    int32_t src[CODEC_MAX_PLANES];   /* payload bit index of plane p's first bit     */
+    int32_t off[CODEC_MAX_PLANES];   /* raster start of plane p's window             */
+    int32_t cat[CODEC_MAX_PLANES];   /* position of plane p's bits in the location map */
+    double entropy;       /* calculate_entropy(cover), bit-exact (codec.py:489-502)  */
+    double target;        /* beta * entropy                                          */
+    double cum_info;      /* cumulative MI at the decision                           */
+    double reserved_d;
+    double mi[CODEC_MAX_PLANES]; /* calculate_mutual_information per plane, evaluated ones */
+} codec_slice_meta;
+
+int codec_abi_version(void);
+const char* codec_last_error(void);
+
+/* Bytes of scratch `codec_plan` needs for these parameters. */
+size_t codec_workspace_bytes(const codec_params* P);
+
+/* Decomposition + block search + segment plan, and the cover->stego copy:
+ *   replaces adaptive_modalities_decomposition (codec.py:561-599, incl. calculate_entropy
+ *   :489-502 and calculate_mutual_information :504-559), the block-variance search of
+ *   lsb_embed_block_then_multiplane (codec.py:431-453) and the merge of untouched planes
+ *   (merge_modalities, codec.py:215-237).
+ * cover[B][H][W] (in_bytes) -> stego[B][H][W] (out_bytes; may be NULL: plan only),
+ * meta[B].  log2_lut[c-1] = numpy.log2(c / (H*W)) for c = 1..H*W (lut_len >= H*W);
+ * table[n_classes*16 + (s-1)] is the layout for payload class slice_class[b] and s. */
+int codec_plan(const codec_params* P, const void* cover, void* stego, const double* log2_lut,
+               int64_t lut_len, const codec_layout* table, const int32_t* slice_class,
+               codec_slice_meta* meta, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Window writes + location map: the embed loop of lsb_embed_block_then_multiplane
+ * (codec.py:455-485) / lsb_embed_multi_plane (codec.py:288-316).  stego must already
+ * hold the copy written by codec_plan.  payload[B][payload_words] (bit b of slice =
+ * message bit b), maps[B][map_words] receives bit j = (cover bit ^ message bit) of the
+ * j-th embedded bit in segment order (the non-zero region of the reference bitmaps). */
+int codec_embed(const codec_params* P, const void* cover, void* stego, const uint64_t* payload,
+                const codec_slice_meta* meta, uint64_t* maps, void* stream);
+
+/* True extraction: payload bits in segment order + cover restore (inverse of the above).
+ * cover_out may be NULL (payload only).  payload_out[B][payload_words]. */
+int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps,
+                  const codec_slice_meta* meta, void* cover_out, uint64_t* payload_out,
+                  void* stream);
+
+/* decode_message (codec.py:752-787) bit stream, from the packed location maps: per plane
+ * the stego LSBs at the first segments_lengths[p] flipped positions in ascending raster
+ * order, planes concatenated in index order.  bits_out[B][bits_cap] one byte per bit,
+ * counts_out[B] = number of bits written. */
+int codec_refdecode(const codec_params* P, const void* stego, const uint64_t* maps,
+                    const codec_slice_meta* meta, uint8_t* bits_out, int32_t bits_cap,
+                    int32_t* counts_out, void* stream);
+
+/* decode_message from DENSE reference bitmaps (codec.py:767-772 on np.split blobs,
+ * codec.py:820-821).  src is either the stego image (src_is_planes = 0; plane p is bit p)
+ * or stacked planes [B][smax][H*W] of dtype in_bytes (src_is_planes = 1; value & 1).
+ * dense[B][smax][H*W] uint8.  meta supplies s, perm and sizes (segments_lengths).
+ * counts_out must hold B*17 int32: [0,B) bits written per slice, the rest is scratch. */
+int codec_refdecode_dense(const codec_params* P, const void* src, int32_t src_is_planes,
+                          const uint8_t* dense, int32_t smax, const codec_slice_meta* meta,
+                          uint8_t* bits_out, int32_t bits_cap, int32_t* counts_out, void* stream);
+
+/* Dense reference bitmaps from packed maps: dense[B][smax][H*W] uint8 (codec.py:462-476,
+ * np.stack at codec.py:888).  Planes >= s are zero. */
+int codec_expand_maps(const codec_params* P, const uint64_t* maps, const codec_slice_meta* meta,
+                      uint8_t* dense, int32_t smax, void* stream);
+
+/* Cover restore from DENSE bitmaps: cover = stego ^ sum_p (dense[p] & 1) << p, p < s. */
+int codec_restore_dense(const codec_params* P, const void* stego, const uint8_t* dense,
+                        int32_t smax, const codec_slice_meta* meta, void* cover_out,
+                        void* stream);
+
+/* Bit-plane unpack, (img >> i) & 1 in the image dtype for i in [first, first+count):
+ * codec.py:571 and extract_local_planes codec.py:789-793.  planes[B][count][H*W]. */
+int codec_unpack_planes(const codec_params* P, const void* img, int32_t first, int32_t count,
+                        void* planes, int32_t plane_bytes, void* stream);
+
+/* merge_modalities (codec.py:215-237): out = OR_k (out_t)(planes[k]) << k, k < nplanes,
+ * planes stacked LSB-first [B][nplanes][H*W] of plane_bytes each. */
+int codec_merge_planes(const codec_params* P, const void* planes, int32_t nplanes,
+                       int32_t plane_bytes, void* out, void* stream);
+
+/* ---- measurement hooks (bench.py): while a profile window is open, every launcher
+ * records a hipEvent pair around each kernel it launches, tagged with a CODEC_K_* id.
+ * Events are created/destroyed here, outside any launch function. */
+#define CODEC_K_SCAN_FAST 1
+#define CODEC_K_SCAN_GENERIC 2
+#define CODEC_K_BLOCK_EXACT 3
+#define CODEC_K_DECIDE 4
+#define CODEC_K_EMBED 5
+#define CODEC_K_RESTORE 6
+#define CODEC_K_GATHER 7
+#define CODEC_K_OTHER 8
+int codec_profile_begin(int32_t capacity);
+/* after the stream has been synchronised: fills ms[i], tag[i] for the recorded pairs and
+ * returns their count (closes the window and frees the events). */
+int codec_profile_end(float* ms, int32_t* tag, int32_t capacity);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CODEC_TCC_H */
