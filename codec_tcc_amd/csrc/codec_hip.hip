@@ -350,6 +350,9 @@ template <typename T> struct Vec8;
 template <> struct Vec8<uint16_t> { typedef uint4 type; };
 template <> struct Vec8<uint8_t> { typedef uint2 type; };
 
+__device__ __forceinline__ uint32_t vor_of(const uint4& v) { return v.x | v.y | v.z | v.w; }
+__device__ __forceinline__ uint32_t vor_of(const uint2& v) { return v.x | v.y; }
+
 __device__ __forceinline__ uint32_t lsb_count(const uint4& v) {
     return __popc(v.x & 0x00010001u) + __popc(v.y & 0x00010001u) + __popc(v.z & 0x00010001u) +
            __popc(v.w & 0x00010001u);
@@ -368,7 +371,7 @@ template <typename T, int SB>
 __global__ __launch_bounds__(1024) void k_scan_fast(const T* __restrict__ cover, T* __restrict__ stego,
                                                     int H, int W, int bands_per_wg,
                                                     uint32_t* __restrict__ ghist_all,
-                                                    u64* __restrict__ gkey) {
+                                                    u64* __restrict__ gkey, uint32_t* __restrict__ gor) {
     typedef typename Vec8<T>::type V;
     constexpr int G = SB / 8;
     constexpr uint32_t NPB = (uint32_t)SB * SB;
@@ -394,6 +397,7 @@ __global__ __launch_bounds__(1024) void k_scan_fast(const T* __restrict__ cover,
     const int nitems = max(0, band1 - band0) * CRp;
     const int lane = threadIdx.x & 63;
     u64 best = 0;
+    uint32_t vor = 0;   // OR of every pixel: bounds the histogram range the decision scans
 
     for (int base = (threadIdx.x & ~63); base < nitems; base += 1024) {
         const int it = base + lane;
@@ -421,6 +425,7 @@ __global__ __launch_bounds__(1024) void k_scan_fast(const T* __restrict__ cover,
                     d[(size_t)(r + 3) * stride] = v3;
                 }
                 ones += lsb_count(v0) + lsb_count(v1) + lsb_count(v2) + lsb_count(v3);
+                vor |= vor_of(v0) | vor_of(v1) | vor_of(v2) | vor_of(v3);
                 hist_add8<T>(lds, ghist, v0);
                 hist_add8<T>(lds, ghist, v1);
                 hist_add8<T>(lds, ghist, v2);
@@ -430,6 +435,7 @@ __global__ __launch_bounds__(1024) void k_scan_fast(const T* __restrict__ cover,
                 V v0 = s[(size_t)r * stride];
                 if (d) d[(size_t)r * stride] = v0;
                 ones += lsb_count(v0);
+                vor |= vor_of(v0);
                 hist_add8<T>(lds, ghist, v0);
             }
         }
@@ -449,6 +455,11 @@ __global__ __launch_bounds__(1024) void k_scan_fast(const T* __restrict__ cover,
         best = best > other ? best : other;
     }
     if (lane == 0 && best) atomicMax(&wkey, best);
+    if constexpr (sizeof(T) == 2) vor = (vor | (vor >> 16)) & 0xFFFFu;
+    else vor = (vor | (vor >> 8) | (vor >> 16) | (vor >> 24)) & 0xFFu;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) vor |= __shfl_xor(vor, o, 64);
+    if (lane == 0 && vor) atomicOr(&gor[b], vor);
     __syncthreads();
     hist_flush<T>(lds, ghist);
     if (threadIdx.x == 0 && wkey) atomicMax(&gkey[b], wkey);
@@ -459,7 +470,7 @@ __global__ __launch_bounds__(1024) void k_scan_fast(const T* __restrict__ cover,
 template <typename Tin, typename Tout>
 __global__ __launch_bounds__(1024) void k_scan_generic(const Tin* __restrict__ cover, Tout* __restrict__ stego,
                                                        long long npx, long long px_per_wg, uint32_t keep,
-                                                       uint32_t* __restrict__ ghist_all) {
+                                                       uint32_t* __restrict__ ghist_all, uint32_t* __restrict__ gor) {
     __shared__ uint32_t lds[HistCfg<Tin>::kLdsWords];
     const int b = blockIdx.y;
     const Tin* src = cover + (size_t)b * npx;
@@ -469,11 +480,16 @@ __global__ __launch_bounds__(1024) void k_scan_generic(const Tin* __restrict__ c
     __syncthreads();
     const long long q0 = (long long)blockIdx.x * px_per_wg;
     const long long q1 = min(npx, q0 + px_per_wg);
+    uint32_t vor = 0;
     for (long long q = q0 + threadIdx.x; q < q1; q += 1024) {
         const uint32_t v = src[q];
         if (dst) dst[q] = (Tout)(v & keep);
+        vor |= v;
         hist_add<Tin>(lds, ghist, v, 1u);
     }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) vor |= __shfl_xor(vor, o, 64);
+    if ((threadIdx.x & 63) == 0 && vor) atomicOr(&gor[blockIdx.y], vor);
     __syncthreads();
     hist_flush<Tin>(lds, ghist);
 }
@@ -526,51 +542,46 @@ __global__ __launch_bounds__(256) void k_block_exact(const T* __restrict__ img, 
 }
 
 // ------------------------------------------------------------------ K3: decide
-struct TermFn {
-    const uint32_t* hist;
+// identity order: element k is the k-th non-zero bin's term p*log2(p)
+struct RankTerm {
+    const double* terms;
+    __device__ __forceinline__ double operator()(int k) const { return terms[k]; }
+};
+// permuted order: list[k] is the identity rank of the k-th element
+struct ListTerm {
+    const double* terms;
     const uint16_t* list;
-    const double* lut;
-    double N;
-    __device__ __forceinline__ double operator()(int k) const {
-        const uint32_t c = hist[list[k]];
-        const double p = (double)c / N;
-        return p * lut[c - 1];
-    }
+    __device__ __forceinline__ double operator()(int k) const { return terms[list[k]]; }
 };
 
 __device__ __forceinline__ double plogp(const double* lut, uint32_t c, double N) {
-    const double p = (double)c / N;
-    return p * lut[c - 1];
+    const double p = (double)c / N;       // counts[counts > 0] / size   (codec.py:498)
+    return p * lut[c - 1];                // probabilities * np.log2(probabilities)  (:501)
 }
 
-// builds, in LDS `list`, the non-zero bins in the order of the joint bincount of
-// calculate_mutual_information (codec.py:546-551): bins with bit `plane` = 0 ascending,
-// then bins with bit 1 ascending.  plane < 0: plain ascending order (calculate_entropy).
-template <int BPT, int R>
-__device__ void build_order(const uint32_t* hist, int plane, uint16_t* list, uint32_t* sh) {
-    const int v0 = threadIdx.x * BPT;
-    uint32_t zc = 0, oc = 0;
-    for (int k = 0; k < BPT; ++k) {
-        const int v = v0 + k;
-        if (v < R && hist[v]) {
-            if (plane >= 0 && ((v >> plane) & 1)) ++oc; else ++zc;
-        }
-    }
+// The order of the joint bincount of calculate_mutual_information (codec.py:546-551):
+// index = bit * (max_val+1) + value, so the non-zero joint bins are the image's non-zero
+// bins with bit `plane` = 0 (ascending value) followed by those with bit 1.  Each thread
+// owns `bpt` consecutive bins (non-zero ones flagged in `nzmask`, identity ranks from
+// `rank0`); `list` receives identity ranks in joint order.
+__device__ void build_joint_order(u64 nzmask, int v0, uint32_t rank0, int plane, uint16_t* list, uint32_t* sh) {
+    uint32_t oc = 0;
+    for (u64 msk = nzmask; msk; msk &= msk - 1) oc += ((v0 + __ffsll((long long)msk) - 1) >> plane) & 1;
+    const uint32_t zc = (uint32_t)__popcll(nzmask) - oc;
     uint32_t ztot, otot;
     uint32_t zp = block_excl_scan<1024>(zc, sh, &ztot);
-    uint32_t op = block_excl_scan<1024>(oc, sh, &otot);
-    op += ztot;
-    for (int k = 0; k < BPT; ++k) {
-        const int v = v0 + k;
-        if (v < R && hist[v]) {
-            if (plane >= 0 && ((v >> plane) & 1)) list[op++] = (uint16_t)v; else list[zp++] = (uint16_t)v;
-        }
+    uint32_t op = block_excl_scan<1024>(oc, sh, &otot) + ztot;
+    uint32_t r = rank0;
+    for (u64 msk = nzmask; msk; msk &= msk - 1, ++r) {
+        const int v = v0 + __ffsll((long long)msk) - 1;
+        if ((v >> plane) & 1) list[op++] = (uint16_t)r; else list[zp++] = (uint16_t)r;
     }
     __syncthreads();
 }
 
 template <typename T>
 __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t* __restrict__ ghist_all,
+                                                 const uint32_t* __restrict__ gor, double* __restrict__ gterms,
                                                  const u64* __restrict__ gkey, const double* __restrict__ exact,
                                                  int exact_cap, int exact_edge_only, int fast_blocks,
                                                  const double* __restrict__ lut, long long lut_len,
@@ -578,11 +589,9 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
                                                  const int32_t* __restrict__ slice_class,
                                                  codec_slice_meta* __restrict__ meta_all) {
     constexpr int R = HistCfg<T>::kBins;
-    constexpr int BPT = R >= 1024 ? R / 1024 : 1;
     __shared__ uint16_t list[R];
     __shared__ double vals[1024];
     __shared__ uint32_t sh[20];
-    __shared__ int shi[20];
     __shared__ uint32_t pops_sh[16];
     __shared__ double best_sc[16];
     __shared__ int best_ix[16];
@@ -590,35 +599,37 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     const int b = blockIdx.x;
     const int t = threadIdx.x;
     const uint32_t* hist = ghist_all + (size_t)b * R;
+    double* terms = gterms + (size_t)b * R;
     const long long npx = (long long)P.H * P.W;
     const double Nd = (double)npx;
     codec_slice_meta* M = meta_all + b;
 
-    // ---- pass 1: distinct values, max value, per-plane popcounts (codec.py:571 planes)
-    uint32_t nz = 0, pop[16];
-    int vmax = -1;
+    // ---- bins that can be non-zero: [0, Rp), Rp = next power of two above OR(pixels)
+    const uint32_t orv = gor[b];
+    int Rp = orv ? (1 << (32 - __clz((int)orv))) : 1;
+    if (Rp > R) Rp = R;
+    const int bpt = Rp > 1024 ? Rp / 1024 : 1;     // <= 64 bins per thread
+    const int v0 = t * bpt;
+
+    // ---- pass 1: non-zero bins (bitmask), per-plane popcounts (the planes of codec.py:571)
+    u64 nzmask = 0;
+    uint32_t pop[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) pop[i] = 0;
-    {
-        const int v0 = t * BPT;
-        for (int k = 0; k < BPT; ++k) {
-            const int v = v0 + k;
-            if (v < R) {
-                const uint32_t c = hist[v];
-                if (c) {
-                    ++nz;
-                    vmax = v;
+    for (int k = 0; k < bpt; ++k) {
+        const int v = v0 + k;
+        if (v < Rp) {
+            const uint32_t c = hist[v];
+            if (c) {
+                nzmask |= 1ull << k;
 #pragma unroll
-                    for (int i = 0; i < 16; ++i)
-                        if ((v >> i) & 1) pop[i] += c;
-                }
+                for (int i = 0; i < 16; ++i) pop[i] += ((v >> i) & 1) ? c : 0u;
             }
         }
     }
-    const uint32_t m = block_sum_u32<1024>(nz, sh);
-    (void)block_max_i32<1024>(vmax, shi);
     if (t < 16) pops_sh[t] = 0;
-    __syncthreads();
+    uint32_t m;
+    const uint32_t rank0 = block_excl_scan<1024>((uint32_t)__popcll(nzmask), sh, &m);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         uint32_t x = pop[i];
@@ -626,17 +637,20 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
         for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
         if ((t & 63) == 0 && x) atomicAdd(&pops_sh[i], x);
     }
+    const bool lut_ok = lut_len >= npx;
+    // terms of the non-zero bins in ascending value order, computed once
+    if (lut_ok) {
+        uint32_t r = rank0;
+        for (u64 msk = nzmask; msk; msk &= msk - 1, ++r) {
+            const int v = v0 + __ffsll((long long)msk) - 1;
+            terms[r] = plogp(lut, hist[v], Nd);
+        }
+    }
     __syncthreads();
 
-    const bool lut_ok = lut_len >= npx;
-
-    // ---- calculate_entropy (codec.py:489-502) = H(Y) in calculate_mutual_information
+    // ---- calculate_entropy (codec.py:489-502) = H(Y) inside calculate_mutual_information
     double Hy = 0.0;
-    if (lut_ok) {
-        build_order<BPT, R>(hist, -1, list, sh);
-        TermFn f{hist, list, lut, Nd};
-        Hy = -np_sum_block1024(f, (int)m, vals);
-    }
+    if (lut_ok) Hy = -np_sum_block1024(RankTerm{terms}, (int)m, vals);
     const double target = P.beta * Hy;
 
     // ---- the s decision (codec.py:580-593)
@@ -652,9 +666,8 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
         const uint32_t pp = pops_sh[i];
         double mi = 0.0;
         if (m > 1 && pp != 0 && (long long)pp != npx) {          // codec.py:520-523
-            build_order<BPT, R>(hist, i, list, sh);
-            TermFn f{hist, list, lut, Nd};
-            const double hxy = -np_sum_block1024(f, (int)m, vals);
+            build_joint_order(nzmask, v0, rank0, i, list, sh);
+            const double hxy = -np_sum_block1024(ListTerm{terms, list}, (int)m, vals);
             const double hx = -(plogp(lut, (uint32_t)(npx - pp), Nd) + plogp(lut, pp, Nd));
             mi = (hx + Hy) - hxy;                                // codec.py:554
             if (!(mi > 0.0)) mi = 0.0;                           // max(0.0, mi)
@@ -1164,7 +1177,7 @@ static int host_exact_count(const codec_params* P, bool edge_only) {
 }
 
 struct WsLayout {
-    size_t hist, keys, exact, total;
+    size_t hist, keys, orv, exact, terms, total;
     int exact_cap;
 };
 
@@ -1176,8 +1189,10 @@ static WsLayout ws_layout(const codec_params* P) {
     L.exact_cap = cap > 0 ? cap : 1;
     L.hist = 0;
     L.keys = align_up(L.hist + (size_t)P->B * R * 4, 256);
-    L.exact = align_up(L.keys + (size_t)P->B * 8, 256);
-    L.total = align_up(L.exact + (size_t)P->B * L.exact_cap * 8, 256);
+    L.orv = align_up(L.keys + (size_t)P->B * 8, 256);
+    L.exact = align_up(L.orv + (size_t)P->B * 4, 256);       // [0, exact) is zeroed per call
+    L.terms = align_up(L.exact + (size_t)P->B * L.exact_cap * 8, 256);
+    L.total = align_up(L.terms + (size_t)P->B * R * 8, 256);
     return L;
 }
 
@@ -1225,7 +1240,7 @@ size_t codec_workspace_bytes(const codec_params* P) {
 
 template <typename T>
 static int launch_scan_fast(const codec_params* P, const void* cover, void* stego, uint32_t* hist, u64* keys,
-                            hipStream_t st) {
+                            uint32_t* orv, hipStream_t st) {
     const int sb = P->block;
     const int nb = (P->H + sb - 1) / sb;
     const int target = sizeof(T) == 2 ? 256 : 1024;
@@ -1238,17 +1253,18 @@ static int launch_scan_fast(const codec_params* P, const void* cover, void* steg
     T* s = static_cast<T*>(stego);
     ProfScope prof(st, CODEC_K_SCAN_FAST);
     switch (sb) {
-        case 8: hipLaunchKernelGGL((k_scan_fast<T, 8>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys); break;
-        case 16: hipLaunchKernelGGL((k_scan_fast<T, 16>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys); break;
-        case 32: hipLaunchKernelGGL((k_scan_fast<T, 32>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys); break;
-        default: hipLaunchKernelGGL((k_scan_fast<T, 64>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys); break;
+        case 8: hipLaunchKernelGGL((k_scan_fast<T, 8>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
+        case 16: hipLaunchKernelGGL((k_scan_fast<T, 16>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
+        case 32: hipLaunchKernelGGL((k_scan_fast<T, 32>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
+        default: hipLaunchKernelGGL((k_scan_fast<T, 64>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
     }
     LAUNCH_CHECK("k_scan_fast");
     return 0;
 }
 
 template <typename Tin, typename Tout>
-static int launch_scan_generic(const codec_params* P, const void* cover, void* stego, uint32_t* hist, hipStream_t st) {
+static int launch_scan_generic(const codec_params* P, const void* cover, void* stego, uint32_t* hist, uint32_t* orv,
+                               hipStream_t st) {
     const long long npx = (long long)P->H * P->W;
     const int target = sizeof(Tin) == 2 ? 256 : 1024;
     long long wgps = (target + P->B - 1) / P->B;
@@ -1258,7 +1274,7 @@ static int launch_scan_generic(const codec_params* P, const void* cover, void* s
     const uint32_t keep = P->nbits >= 32 ? 0xFFFFFFFFu : ((1u << P->nbits) - 1u);
     ProfScope prof(st, CODEC_K_SCAN_GENERIC);
     hipLaunchKernelGGL((k_scan_generic<Tin, Tout>), dim3((unsigned)wgps, P->B), dim3(1024), 0, st,
-                       static_cast<const Tin*>(cover), static_cast<Tout*>(stego), npx, per, keep, hist);
+                       static_cast<const Tin*>(cover), static_cast<Tout*>(stego), npx, per, keep, hist, orv);
     LAUNCH_CHECK("k_scan_generic");
     return 0;
 }
@@ -1280,19 +1296,21 @@ int codec_plan(const codec_params* P, const void* cover, void* stego, const doub
     char* ws = static_cast<char*>(workspace);
     uint32_t* hist = reinterpret_cast<uint32_t*>(ws + L.hist);
     u64* keys = reinterpret_cast<u64*>(ws + L.keys);
+    uint32_t* orv = reinterpret_cast<uint32_t*>(ws + L.orv);
     double* exact = reinterpret_cast<double*>(ws + L.exact);
-    HIP_TRY(hipMemsetAsync(ws, 0, L.exact, st));   // histograms + block keys
+    double* terms = reinterpret_cast<double*>(ws + L.terms);
+    HIP_TRY(hipMemsetAsync(ws, 0, L.exact, st));   // histograms, block keys, OR words
 
     const bool fast = use_fast_scan(P, cover, stego ? stego : cover);
     if (fast) {
-        rc = P->in_bytes == 2 ? launch_scan_fast<uint16_t>(P, cover, stego, hist, keys, st)
-                              : launch_scan_fast<uint8_t>(P, cover, stego, hist, keys, st);
+        rc = P->in_bytes == 2 ? launch_scan_fast<uint16_t>(P, cover, stego, hist, keys, orv, st)
+                              : launch_scan_fast<uint8_t>(P, cover, stego, hist, keys, orv, st);
     } else if (P->in_bytes == 2) {
-        rc = P->out_bytes == 2 ? launch_scan_generic<uint16_t, uint16_t>(P, cover, stego, hist, st)
-                               : launch_scan_generic<uint16_t, uint8_t>(P, cover, stego, hist, st);
+        rc = P->out_bytes == 2 ? launch_scan_generic<uint16_t, uint16_t>(P, cover, stego, hist, orv, st)
+                               : launch_scan_generic<uint16_t, uint8_t>(P, cover, stego, hist, orv, st);
     } else {
-        rc = P->out_bytes == 2 ? launch_scan_generic<uint8_t, uint16_t>(P, cover, stego, hist, st)
-                               : launch_scan_generic<uint8_t, uint8_t>(P, cover, stego, hist, st);
+        rc = P->out_bytes == 2 ? launch_scan_generic<uint8_t, uint16_t>(P, cover, stego, hist, orv, st)
+                               : launch_scan_generic<uint8_t, uint8_t>(P, cover, stego, hist, orv, st);
     }
     if (rc) return rc;
 
@@ -1313,10 +1331,10 @@ int codec_plan(const codec_params* P, const void* cover, void* stego, const doub
     const codec_params Pv = *P;
     ProfScope prof(st, CODEC_K_DECIDE);
     if (P->in_bytes == 2)
-        hipLaunchKernelGGL(k_decide<uint16_t>, dim3(P->B), dim3(1024), 0, st, Pv, hist, keys, exact, L.exact_cap,
+        hipLaunchKernelGGL(k_decide<uint16_t>, dim3(P->B), dim3(1024), 0, st, Pv, hist, orv, terms, keys, exact, L.exact_cap,
                            edge_only, fast ? 1 : 0, log2_lut, (long long)lut_len, table, slice_class, meta);
     else
-        hipLaunchKernelGGL(k_decide<uint8_t>, dim3(P->B), dim3(1024), 0, st, Pv, hist, keys, exact, L.exact_cap,
+        hipLaunchKernelGGL(k_decide<uint8_t>, dim3(P->B), dim3(1024), 0, st, Pv, hist, orv, terms, keys, exact, L.exact_cap,
                            edge_only, fast ? 1 : 0, log2_lut, (long long)lut_len, table, slice_class, meta);
     LAUNCH_CHECK("k_decide");
     return 0;

@@ -1,10 +1,41 @@
 #!/bin/bash
+# GPU box check: build, pytest -m gpu, bench, rocprofv3 kernel stats (+ optional PMC passes).
+# usage: bash tools/gpu_check.sh [tests] [bench] [prof] [pmc]   (default: tests bench prof)
 cd "$GRAFT_REPO_ROOT" || exit 9
 mkdir -p gpurun_out
+STAGES="${*:-tests bench prof}"
+has() { [[ " $STAGES " == *" $1 "* ]]; }
 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo build failed; tail gpurun_out/build.log; exit 3; }
-timeout -k 10 900 python -m pytest tests -m gpu -q --maxfail=8 -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?
-echo "pytest rc=$rc"; tail -45 gpurun_out/pytest_gpu.log
-if [ $rc -le 1 ]; then
-  timeout -k 10 600 python bench.py --steps 10 --warmup 2 --cpu-seconds 5 > gpurun_out/bench.json 2> gpurun_out/bench.err; brc=$?
-  echo "bench rc=$brc"; cat gpurun_out/bench.json; tail -20 gpurun_out/bench.err
+if has tests; then
+  timeout -k 10 900 python -m pytest tests -m gpu -q --maxfail=8 -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+  echo "pytest rc=$rc"; tail -25 gpurun_out/pytest_gpu.log
+  [ $rc -le 1 ] || exit $rc
+fi
+if has smoke; then
+  timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1; rc=$?; echo "smoke rc=$rc"; tail -5 gpurun_out/smoke.log
+  [ $rc -eq 0 ] || exit $rc
+fi
+if has bench; then
+  timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?
+  echo "bench rc=$rc"; cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err
+  [ $rc -eq 0 ] || exit $rc
+fi
+if has prof; then
+  R="$GRAFT_REPO_ROOT"
+  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
+      -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --cpu-seconds 0 --no-profile \
+      > "$R/gpurun_out/prof.log" 2>&1 ); rc=$?
+  echo "rocprof rc=$rc"; tail -3 gpurun_out/prof.log
+  find gpurun_out/prof -name "*stats*" | head
+  [ $rc -eq 0 ] || exit $rc
+fi
+if has pmc; then
+  R="$GRAFT_REPO_ROOT"
+  for C in FETCH_SIZE WRITE_SIZE; do
+    ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --pmc $C --kernel-trace --output-format csv \
+        -d "$R/gpurun_out/pmc_$C" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --no-profile \
+        > "$R/gpurun_out/pmc_$C.log" 2>&1 ); rc=$?
+    echo "pmc $C rc=$rc"; tail -2 "gpurun_out/pmc_$C.log"
+    [ $rc -eq 0 ] || exit $rc
+  done
 fi
