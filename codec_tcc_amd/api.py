@@ -210,8 +210,9 @@ def merge_modalities(global_planes, local_planes) -> np.ndarray:
     torch = _torch()
     out = torch.empty((1, n), dtype=torch.uint16 if out_dt == np.uint16 else torch.uint8, device=_dev())
     P = _params(1, 1, n, 1, 2 if out_dt == np.uint16 else 1)
-    _lib.check(_lib.load().codec_merge_planes(C.byref(P), _to_dev(st.reshape(1, total, n)).data_ptr(), total,
-                                              st.dtype.itemsize, out.data_ptr(), _stream()), "codec_merge_planes")
+    planes_t = _to_dev(st.reshape(1, total, n))
+    _lib.check(_lib.load().codec_merge_planes(C.byref(P), planes_t.data_ptr(), total, st.dtype.itemsize,
+                                              out.data_ptr(), _stream()), "codec_merge_planes")
     return out.cpu().numpy()[0].reshape(shape)
 
 
@@ -229,8 +230,9 @@ def extract_local_planes(stego_array, s):
     torch = _torch()
     out = torch.empty((1, s, n), dtype=torch.uint16 if img.dtype == np.uint16 else torch.uint8, device=_dev())
     P = _params(1, 1, n, img.dtype.itemsize, img.dtype.itemsize)
-    _lib.check(_lib.load().codec_unpack_planes(C.byref(P), _to_dev(img.reshape(1, 1, n)).data_ptr(), 0, s,
-                                               out.data_ptr(), img.dtype.itemsize, _stream()), "codec_unpack_planes")
+    src_t = _to_dev(img.reshape(1, 1, n))
+    _lib.check(_lib.load().codec_unpack_planes(C.byref(P), src_t.data_ptr(), 0, s, out.data_ptr(),
+                                               img.dtype.itemsize, _stream()), "codec_unpack_planes")
     host = out.cpu().numpy()[0]
     return [host[i].reshape(img.shape) for i in range(s)]
 
@@ -268,10 +270,14 @@ def decode_message(stego_planes, bitmaps, metadata) -> str:
     bits = torch.zeros((1, cap), dtype=torch.uint8, device=_dev())
     counts = torch.zeros((17,), dtype=torch.int32, device=_dev())
     P = _params(1, 1, n, 1, 1)
-    _lib.check(_lib.load().codec_refdecode_dense(C.byref(P), _to_dev(st.reshape(1, s, n)).data_ptr(), 1,
-                                                 _to_dev(dense.reshape(1, s, n)).data_ptr(), s, meta.data_ptr(),
-                                                 bits.data_ptr(), cap, counts.data_ptr(), _stream()),
-               "codec_refdecode_dense")
+    # keep every device buffer referenced until the launch is enqueued: a temporary freed
+    # mid-call returns its block to the caching allocator, which may hand it to the next
+    # upload on the same stream before the kernel has read it
+    src_t = _to_dev(st.reshape(1, s, n))
+    dense_t = _to_dev(dense.reshape(1, s, n))
+    _lib.check(_lib.load().codec_refdecode_dense(C.byref(P), src_t.data_ptr(), 1, dense_t.data_ptr(), s,
+                                                 meta.data_ptr(), bits.data_ptr(), cap, counts.data_ptr(),
+                                                 _stream()), "codec_refdecode_dense")
     k = int(counts[0].item())
     if k > cap:
         raise RuntimeError("decode_message: output capacity exceeded")

@@ -322,7 +322,23 @@ __device__ void hist_flush<uint8_t>(uint32_t* lds, uint32_t* ghist) {
     }
 }
 
-// 8 pixels of a vector (16 B of uint16 / 8 B of uint8), run-merged histogram adds
+// exact bookkeeping after an LDS add of `cnt` to value v's 16-bit field returned `old`
+// (only called when a field wrapped; see hist16_add)
+__device__ __noinline__ void hist16_fix(uint32_t* ghist, uint32_t v, uint32_t cnt, uint32_t old) {
+    if (v & 1u) {
+        if ((old >> 16) + cnt > 0xFFFFu) atomicAdd(&ghist[v], 0x10000u);
+    } else if ((old & 0xFFFFu) + cnt > 0xFFFFu) {
+        atomicAdd(&ghist[v], 0x10000u);
+        uint32_t adj = 0xFFFFFFFFu;
+        if ((old >> 16) == 0xFFFFu) adj += 0x10000u;
+        atomicAdd(&ghist[v + 1], adj);
+    }
+}
+
+// 8 consecutive pixels of a vector (16 B of uint16 / 8 B of uint8): equal neighbours are
+// merged into one add (constant regions), the 8 LDS atomics are issued back to back and
+// their returned values are checked for 16-bit wraps only afterwards, so the adds
+// pipeline instead of each waiting for its return.
 template <typename T, typename V>
 __device__ __forceinline__ void hist_add8(uint32_t* lds, uint32_t* ghist, const V& vec) {
     uint32_t px[8];
@@ -333,17 +349,39 @@ __device__ __forceinline__ void hist_add8(uint32_t* lds, uint32_t* ghist, const 
 #pragma unroll
         for (int k = 0; k < 4; ++k) { px[k] = (vec.x >> (8 * k)) & 0xFFu; px[4 + k] = (vec.y >> (8 * k)) & 0xFFu; }
     }
+    uint32_t cnt[8];
     uint32_t run = 1;
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
-        if (px[k + 1] == px[k]) {
-            ++run;
-        } else {
-            hist_add<T>(lds, ghist, px[k], run);
-            run = 1;
-        }
+        const bool eq = px[k + 1] == px[k];
+        cnt[k] = eq ? 0u : run;
+        run = eq ? run + 1u : 1u;
     }
-    hist_add<T>(lds, ghist, px[7], run);
+    cnt[7] = run;
+    if constexpr (sizeof(T) == 2) {
+        uint32_t old[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            old[k] = 0;
+            if (cnt[k]) old[k] = atomicAdd(&lds[px[k] >> 1], (px[k] & 1u) ? (cnt[k] << 16) : cnt[k]);
+        }
+        bool wrap = false;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t field = (px[k] & 1u) ? (old[k] >> 16) : (old[k] & 0xFFFFu);
+            wrap |= (field + cnt[k]) > 0xFFFFu;
+        }
+        if (wrap) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (cnt[k]) hist16_fix(ghist, px[k], cnt[k], old[k]);
+        }
+    } else {
+        const uint32_t base = (threadIdx.x >> 6) << 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (cnt[k]) atomicAdd(&lds[base + px[k]], cnt[k]);
+    }
 }
 
 template <typename T> struct Vec8;
@@ -872,8 +910,16 @@ __global__ __launch_bounds__(256) void k_restore(const T* __restrict__ stego, T*
     const long long c1 = min(nchunks, c0 + chunks_per_wg);
     const V* src = reinterpret_cast<const V*>(stego + (size_t)b * npx);
     V* dst = reinterpret_cast<V*>(cover + (size_t)b * npx);
-    for (long long ch = c0 + threadIdx.x; ch < c1; ch += 256) {
-        V v = src[ch];
+    for (long long cb = c0 + threadIdx.x; cb < c1; cb += 4 * 256) {
+      V vv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+          if (cb + u * 256 < c1) vv[u] = src[cb + u * 256];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long long ch = cb + u * 256;
+        if (ch >= c1) break;
+        V v = vv[u];
         const long long q0 = ch * 8;
         for (int k = 0; k < nr; ++k) {
             const Range r = rg[k];
@@ -898,6 +944,7 @@ __global__ __launch_bounds__(256) void k_restore(const T* __restrict__ stego, T*
             }
         }
         dst[ch] = v;
+      }
     }
     // scalar tail (npx % 8) handled by the last workgroup
     if (blockIdx.x == gridDim.x - 1) {
