@@ -5,13 +5,14 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
 template <int U, int NT_LD, int NT_ST>
-__global__ __launch_bounds__(256) void copy_gs(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n) {
+__global__ __launch_bounds__(256) void copy_gs(const v4u* __restrict__ src, v4u* __restrict__ dst, size_t n) {
     const size_t stride = (size_t)gridDim.x * 256 * U;
     for (size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x; base < n; base += stride) {
-        uint4 v[U];
+        v4u v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const size_t i = base + (size_t)u * 256;
@@ -29,11 +30,11 @@ __global__ __launch_bounds__(256) void copy_gs(const uint4* __restrict__ src, ui
 
 // contiguous chunk per block (like k_restore / k_scan_fast: each WG owns a range)
 template <int U>
-__global__ __launch_bounds__(256) void copy_chunk(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n,
+__global__ __launch_bounds__(256) void copy_chunk(const v4u* __restrict__ src, v4u* __restrict__ dst, size_t n,
                                                   size_t per) {
     const size_t c0 = (size_t)blockIdx.x * per, c1 = c0 + per < n ? c0 + per : n;
     for (size_t base = c0 + threadIdx.x; base < c1; base += 256 * U) {
-        uint4 v[U];
+        v4u v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) if (base + u * 256 < c1) v[u] = src[base + u * 256];
 #pragma unroll
@@ -58,14 +59,14 @@ static float timeit(F f, int reps) {
 int main() {
     const size_t bytes = (size_t)256 * 2048 * 2048 * 2;   // the benchmark's cover batch
     const size_t n = bytes / 16;
-    uint4 *src, *dst;
+    v4u *src, *dst;
     CK(hipMalloc(&src, bytes)); CK(hipMalloc(&dst, bytes));
     CK(hipMemset(src, 1, bytes)); CK(hipMemset(dst, 0, bytes));
     const int reps = 10;
     auto report = [&](const char* name, float ms) {
         printf("%-44s %8.3f ms  %7.1f GB/s (r+w)\n", name, ms, 2.0 * bytes / ms / 1e6);
     };
-    report("hipMemcpyAsync D2D", timeit([&] { hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, 0); }, reps));
+    report("hipMemcpyAsync D2D", timeit([&] { (void)hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, 0); }, reps));
     for (int g : {1024, 2048, 4096, 8192, 16384}) {
         char nm[96];
         snprintf(nm, sizeof nm, "grid-stride U=4 plain grid=%d", g);
