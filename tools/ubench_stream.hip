@@ -42,6 +42,19 @@ __global__ __launch_bounds__(256) void copy_chunk(const v4u* __restrict__ src, v
     }
 }
 
+template <int U>
+__global__ __launch_bounds__(256) void copy_chunk_nt(const v4u* __restrict__ src, v4u* __restrict__ dst, size_t n,
+                                                     size_t per) {
+    const size_t c0 = (size_t)blockIdx.x * per, c1 = c0 + per < n ? c0 + per : n;
+    for (size_t base = c0 + threadIdx.x; base < c1; base += 256 * U) {
+        v4u v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) if (base + u * 256 < c1) v[u] = __builtin_nontemporal_load(src + base + u * 256);
+#pragma unroll
+        for (int u = 0; u < U; ++u) if (base + u * 256 < c1) __builtin_nontemporal_store(v[u], dst + base + u * 256);
+    }
+}
+
 template <class F>
 static float timeit(F f, int reps) {
     hipEvent_t a, b;
@@ -83,6 +96,22 @@ int main() {
         const size_t per = (n + g - 1) / g;
         report(nm, timeit([&] { copy_chunk<4><<<g, 256>>>(src, dst, n, per); }, reps));
     }
+    for (int g : {2048, 8192, 16384, 32768}) {
+        char nm[96];
+        snprintf(nm, sizeof nm, "grid-stride U=4 nt-both grid=%d", g);
+        report(nm, timeit([&] { copy_gs<4, 1, 1><<<g, 256>>>(src, dst, n); }, reps));
+    }
+    report("grid-stride U=2 nt-both grid=8192", timeit([&] { copy_gs<2, 1, 1><<<8192, 256>>>(src, dst, n); }, reps));
+    report("grid-stride U=8 nt-both grid=8192", timeit([&] { copy_gs<8, 1, 1><<<8192, 256>>>(src, dst, n); }, reps));
+    for (int g : {256, 2048, 8192, 32768}) {
+        char nm[96];
+        snprintf(nm, sizeof nm, "chunk-per-WG U=4 nt-both grid=%d", g);
+        const size_t per = (n + g - 1) / g;
+        report(nm, timeit([&] { copy_chunk_nt<4><<<g, 256>>>(src, dst, n, per); }, reps));
+    }
+    // repeat the baseline at the end (DVFS / drift check)
+    report("grid-stride U=4 plain grid=4096 (again)", timeit([&] { copy_gs<4, 0, 0><<<4096, 256>>>(src, dst, n); }, reps));
+    report("grid-stride U=4 nt-both grid=4096 (again)", timeit([&] { copy_gs<4, 1, 1><<<4096, 256>>>(src, dst, n); }, reps));
     CK(hipFree(src)); CK(hipFree(dst));
     return 0;
 }
