@@ -20,6 +20,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "codec_tcc.h"
@@ -388,6 +389,43 @@ template <typename T> struct Vec8;
 template <> struct Vec8<uint16_t> { typedef uint4 type; };
 template <> struct Vec8<uint8_t> { typedef uint2 type; };
 
+// streaming loads/stores; NT = non-temporal (measured: nt on BOTH the load and the store
+// stream is what lifts a 2 GiB read+write pass from ~5.1 to ~5.9 TB/s, tools/ubench_stream.hip)
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+template <bool NT> __device__ __forceinline__ uint4 ldv(const uint4* p) {
+    if constexpr (NT) {
+        const v4u x = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+        return make_uint4(x.x, x.y, x.z, x.w);
+    } else {
+        return *p;
+    }
+}
+template <bool NT> __device__ __forceinline__ uint2 ldv(const uint2* p) {
+    if constexpr (NT) {
+        const v2u x = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(p));
+        return make_uint2(x.x, x.y);
+    } else {
+        return *p;
+    }
+}
+template <bool NT> __device__ __forceinline__ void stv(uint4* p, const uint4& v) {
+    if constexpr (NT) {
+        v4u x = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(x, reinterpret_cast<v4u*>(p));
+    } else {
+        *p = v;
+    }
+}
+template <bool NT> __device__ __forceinline__ void stv(uint2* p, const uint2& v) {
+    if constexpr (NT) {
+        v2u x = {v.x, v.y};
+        __builtin_nontemporal_store(x, reinterpret_cast<v2u*>(p));
+    } else {
+        *p = v;
+    }
+}
+
 __device__ __forceinline__ uint32_t vor_of(const uint4& v) { return v.x | v.y | v.z | v.w; }
 __device__ __forceinline__ uint32_t vor_of(const uint2& v) { return v.x | v.y; }
 
@@ -405,7 +443,7 @@ __device__ __forceinline__ uint32_t lsb_count(const uint2& v) {
 // Work item = (band of SB rows, 8-pixel column chunk); a wave covers 64 consecutive
 // chunks of one band, so every load instruction reads 1 KiB (u16) contiguously; the
 // SB/8 lanes of one block column combine their LSB counts with shuffles.
-template <typename T, int SB>
+template <typename T, int SB, bool NT>
 __global__ __launch_bounds__(1024) void k_scan_fast(const T* __restrict__ cover, T* __restrict__ stego,
                                                     int H, int W, int bands_per_wg,
                                                     uint32_t* __restrict__ ghist_all,
@@ -452,15 +490,15 @@ __global__ __launch_bounds__(1024) void k_scan_fast(const T* __restrict__ cover,
             const int stride = W / 8;   // vectors per row
             int r = 0;
             for (; r + 4 <= rows; r += 4) {
-                V v0 = s[(size_t)(r + 0) * stride];
-                V v1 = s[(size_t)(r + 1) * stride];
-                V v2 = s[(size_t)(r + 2) * stride];
-                V v3 = s[(size_t)(r + 3) * stride];
+                V v0 = ldv<NT>(s + (size_t)(r + 0) * stride);
+                V v1 = ldv<NT>(s + (size_t)(r + 1) * stride);
+                V v2 = ldv<NT>(s + (size_t)(r + 2) * stride);
+                V v3 = ldv<NT>(s + (size_t)(r + 3) * stride);
                 if (d) {
-                    d[(size_t)(r + 0) * stride] = v0;
-                    d[(size_t)(r + 1) * stride] = v1;
-                    d[(size_t)(r + 2) * stride] = v2;
-                    d[(size_t)(r + 3) * stride] = v3;
+                    stv<NT>(d + (size_t)(r + 0) * stride, v0);
+                    stv<NT>(d + (size_t)(r + 1) * stride, v1);
+                    stv<NT>(d + (size_t)(r + 2) * stride, v2);
+                    stv<NT>(d + (size_t)(r + 3) * stride, v3);
                 }
                 ones += lsb_count(v0) + lsb_count(v1) + lsb_count(v2) + lsb_count(v3);
                 vor |= vor_of(v0) | vor_of(v1) | vor_of(v2) | vor_of(v3);
@@ -470,8 +508,8 @@ __global__ __launch_bounds__(1024) void k_scan_fast(const T* __restrict__ cover,
                 hist_add8<T>(lds, ghist, v3);
             }
             for (; r < rows; ++r) {
-                V v0 = s[(size_t)r * stride];
-                if (d) d[(size_t)r * stride] = v0;
+                V v0 = ldv<NT>(s + (size_t)r * stride);
+                if (d) stv<NT>(d + (size_t)r * stride, v0);
                 ones += lsb_count(v0);
                 vor |= vor_of(v0);
                 hist_add8<T>(lds, ghist, v0);
@@ -891,7 +929,7 @@ __device__ __forceinline__ uint32_t map_bit(const u64* maps, long long j) {
 }
 
 // cover = stego with every window bit XOR-ed with its location-map bit (stream copy)
-template <typename T>
+template <typename T, bool NT>
 __global__ __launch_bounds__(256) void k_restore(const T* __restrict__ stego, T* __restrict__ cover, long long npx,
                                                  const codec_slice_meta* __restrict__ meta,
                                                  const u64* __restrict__ maps_all, int mw, long long chunks_per_wg) {
@@ -914,7 +952,7 @@ __global__ __launch_bounds__(256) void k_restore(const T* __restrict__ stego, T*
       V vv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-          if (cb + u * 256 < c1) vv[u] = src[cb + u * 256];
+          if (cb + u * 256 < c1) vv[u] = ldv<NT>(src + cb + u * 256);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const long long ch = cb + u * 256;
@@ -943,7 +981,7 @@ __global__ __launch_bounds__(256) void k_restore(const T* __restrict__ stego, T*
                 v.y = px[4] | (px[5] << 8) | (px[6] << 16) | (px[7] << 24);
             }
         }
-        dst[ch] = v;
+        stv<NT>(dst + ch, v);
       }
     }
     // scalar tail (npx % 8) handled by the last workgroup
@@ -1189,6 +1227,12 @@ __global__ __launch_bounds__(256) void k_merge(const Tp* __restrict__ planes, in
 // ====================================================================== host side
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// launch-shape knobs (defaults from measurements on MI355X; env overrides for tuning runs)
+static long long knob(const char* name, long long dflt) {
+    const char* v = getenv(name);
+    return (v && *v) ? atoll(v) : dflt;
+}
+
 static int check_params(const codec_params* P) {
     if (!P) return set_err(CODEC_EINVAL, "params is NULL");
     if (P->B < 1 || P->H < 1 || P->W < 1) return set_err(CODEC_EINVAL, "bad shape B=%d H=%d W=%d", P->B, P->H, P->W);
@@ -1290,7 +1334,8 @@ static int launch_scan_fast(const codec_params* P, const void* cover, void* steg
                             uint32_t* orv, hipStream_t st) {
     const int sb = P->block;
     const int nb = (P->H + sb - 1) / sb;
-    const int target = sizeof(T) == 2 ? 256 : 1024;
+    const int target = (int)knob("CODEC_SCAN_WGS", sizeof(T) == 2 ? 256 : 1024);
+    const bool nt = knob("CODEC_NT", 1) != 0;
     int wgps = (target + P->B - 1) / P->B;
     wgps = wgps < 1 ? 1 : (wgps > nb ? nb : wgps);
     const int bpw = (nb + wgps - 1) / wgps;
@@ -1300,10 +1345,14 @@ static int launch_scan_fast(const codec_params* P, const void* cover, void* steg
     T* s = static_cast<T*>(stego);
     ProfScope prof(st, CODEC_K_SCAN_FAST);
     switch (sb) {
-        case 8: hipLaunchKernelGGL((k_scan_fast<T, 8>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
-        case 16: hipLaunchKernelGGL((k_scan_fast<T, 16>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
-        case 32: hipLaunchKernelGGL((k_scan_fast<T, 32>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
-        default: hipLaunchKernelGGL((k_scan_fast<T, 64>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
+        case 8: if (nt) hipLaunchKernelGGL((k_scan_fast<T, 8, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv);
+                else hipLaunchKernelGGL((k_scan_fast<T, 8, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
+        case 16: if (nt) hipLaunchKernelGGL((k_scan_fast<T, 16, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv);
+                else hipLaunchKernelGGL((k_scan_fast<T, 16, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
+        case 32: if (nt) hipLaunchKernelGGL((k_scan_fast<T, 32, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv);
+                else hipLaunchKernelGGL((k_scan_fast<T, 32, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
+        default: if (nt) hipLaunchKernelGGL((k_scan_fast<T, 64, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv);
+                 else hipLaunchKernelGGL((k_scan_fast<T, 64, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
     }
     LAUNCH_CHECK("k_scan_fast");
     return 0;
@@ -1436,19 +1485,28 @@ int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps
             LAUNCH_CHECK("k_restore_scalar");
         } else {
         const long long nchunks = npx / 8;
-        long long wgps = (2048 + P->B - 1) / P->B;
+        // many small address-ordered workgroups stream best (tools/ubench_stream.hip)
+        const long long target = knob("CODEC_RESTORE_WGS", 32768);
+        const bool nt = knob("CODEC_NT", 1) != 0;
+        long long wgps = (target + P->B - 1) / P->B;
         long long per = (nchunks + wgps - 1) / wgps;
         if (per < 1024) per = 1024;
         wgps = (nchunks + per - 1) / per;
         if (wgps < 1) wgps = 1;
         dim3 grid((unsigned)wgps, P->B);
         ProfScope prof(st, CODEC_K_RESTORE);
-        if (P->in_bytes == 2)
-            hipLaunchKernelGGL(k_restore<uint16_t>, grid, dim3(256), 0, st, static_cast<const uint16_t*>(stego),
-                               static_cast<uint16_t*>(cover_out), npx, meta, reinterpret_cast<const u64*>(maps), P->map_words, per);
-        else
-            hipLaunchKernelGGL(k_restore<uint8_t>, grid, dim3(256), 0, st, static_cast<const uint8_t*>(stego),
-                               static_cast<uint8_t*>(cover_out), npx, meta, reinterpret_cast<const u64*>(maps), P->map_words, per);
+        const u64* mp = reinterpret_cast<const u64*>(maps);
+        if (P->in_bytes == 2) {
+            const uint16_t* sp = static_cast<const uint16_t*>(stego);
+            uint16_t* cp = static_cast<uint16_t*>(cover_out);
+            if (nt) hipLaunchKernelGGL((k_restore<uint16_t, true>), grid, dim3(256), 0, st, sp, cp, npx, meta, mp, P->map_words, per);
+            else hipLaunchKernelGGL((k_restore<uint16_t, false>), grid, dim3(256), 0, st, sp, cp, npx, meta, mp, P->map_words, per);
+        } else {
+            const uint8_t* sp = static_cast<const uint8_t*>(stego);
+            uint8_t* cp = static_cast<uint8_t*>(cover_out);
+            if (nt) hipLaunchKernelGGL((k_restore<uint8_t, true>), grid, dim3(256), 0, st, sp, cp, npx, meta, mp, P->map_words, per);
+            else hipLaunchKernelGGL((k_restore<uint8_t, false>), grid, dim3(256), 0, st, sp, cp, npx, meta, mp, P->map_words, per);
+        }
         LAUNCH_CHECK("k_restore");
         }
     }

@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Interleaved in-process A/B of launch-shape knobs (env read per launch by the C ABI).
+
+    python tools/tune.py [--kind ct12] [--rounds 3]
+Prints, per configuration, the median per-kernel HIP-event time over rounds."""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+CONFIGS = [
+    {"CODEC_NT": "0", "CODEC_SCAN_WGS": "256", "CODEC_RESTORE_WGS": "2048"},
+    {"CODEC_NT": "1", "CODEC_SCAN_WGS": "256", "CODEC_RESTORE_WGS": "2048"},
+    {"CODEC_NT": "0", "CODEC_SCAN_WGS": "256", "CODEC_RESTORE_WGS": "32768"},
+    {"CODEC_NT": "1", "CODEC_SCAN_WGS": "256", "CODEC_RESTORE_WGS": "32768"},
+    {"CODEC_NT": "1", "CODEC_SCAN_WGS": "512", "CODEC_RESTORE_WGS": "32768"},
+    {"CODEC_NT": "1", "CODEC_SCAN_WGS": "1024", "CODEC_RESTORE_WGS": "32768"},
+    {"CODEC_NT": "1", "CODEC_SCAN_WGS": "2048", "CODEC_RESTORE_WGS": "32768"},
+    {"CODEC_NT": "1", "CODEC_SCAN_WGS": "256", "CODEC_RESTORE_WGS": "8192"},
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kind", default="ct12")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--configs", default="")
+    a = ap.parse_args()
+    import torch
+
+    import bench
+    import codec_tcc_amd as ct
+    from codec_tcc_amd import _lib, synth
+    configs = json.loads(a.configs) if a.configs else CONFIGS
+    dev = torch.device("cuda", 0)
+    B, H, W = a.batch, 2048, 2048
+    covers = bench.make_covers(torch, a.kind, B, H, W, dev, 0)
+    codec = ct.Codec(B, H, W, dtype="uint16", device=dev)
+    pl = ct.make_payloads([synth.payload(1024, 7 + i) for i in range(B)], dev)
+    stego = torch.empty_like(covers)
+    cov2 = torch.empty_like(covers)
+    maps = torch.empty((B, pl.map_words), dtype=torch.int64, device=dev)
+    meta = torch.empty((B, _lib.META_BYTES), dtype=torch.uint8, device=dev)
+    pay = torch.empty((B, pl.payload_words), dtype=torch.int64, device=dev)
+    lib = _lib.load()
+
+    def step():
+        codec.encode(covers, pl, stego=stego, maps=maps, meta=meta)
+        codec.decode(stego, maps, meta, payload_words=pl.payload_words, map_words=pl.map_words, cover=cov2,
+                     payload=pay)
+
+    res = {i: {} for i in range(len(configs))}
+    for _r in range(a.rounds):
+        for i, cfg in enumerate(configs):
+            os.environ.update(cfg)
+            step()
+            torch.cuda.synchronize()
+            cap = 32 * a.steps
+            _lib.check(lib.codec_profile_begin(cap), "profile")
+            for _ in range(a.steps):
+                step()
+            torch.cuda.synchronize()
+            ms = (C.c_float * cap)()
+            tags = (C.c_int32 * cap)()
+            n = lib.codec_profile_end(ms, tags, cap)
+            per = {}
+            for k in range(n):
+                per.setdefault(_lib.KERNEL_TAGS[tags[k]], []).append(ms[k])
+            for k, v in per.items():
+                res[i].setdefault(k, []).append(float(np.mean(v)))
+    assert torch.equal(cov2.view(torch.int16), covers.view(torch.int16))
+    for i, cfg in enumerate(configs):
+        row = {k: round(float(np.median(v)), 4) for k, v in res[i].items()}
+        tot = round(sum(row.values()), 4)
+        print(json.dumps({"cfg": cfg, "kernels_ms": row, "sum_ms": tot}))
+
+
+if __name__ == "__main__":
+    main()
