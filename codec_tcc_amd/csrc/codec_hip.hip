@@ -934,18 +934,36 @@ __global__ __launch_bounds__(256) void k_restore(const T* __restrict__ stego, T*
                                                  const codec_slice_meta* __restrict__ meta,
                                                  const u64* __restrict__ maps_all, int mw, long long chunks_per_wg) {
     typedef typename Vec8<T>::type V;
-    __shared__ SliceWin W;
     __shared__ Range rg[32];
     __shared__ int nrg;
     const int b = blockIdx.y;
-    load_win(meta + b, &W);
-    if (threadIdx.x == 0) nrg = build_ranges(W, rg);
-    __syncthreads();
-    const int nr = nrg;
-    const u64* maps = maps_all + (size_t)b * mw;
     const long long nchunks = npx / 8;
     const long long c0 = (long long)blockIdx.x * chunks_per_wg;
     const long long c1 = min(nchunks, c0 + chunks_per_wg);
+    // prologue, parallel: lane p < s contributes plane p's (<= 2) window ranges, kept only
+    // if they touch this workgroup's pixels (most workgroups keep none)
+    if (threadIdx.x == 0) nrg = 0;
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        const codec_slice_meta* M = meta + b;
+        const int p = threadIdx.x;
+        if (p < M->s) {
+            const int n = M->n[p], off = M->off[p], cat = M->cat[p];
+            const long long lo = c0 * 8, hi = (blockIdx.x == gridDim.x - 1) ? npx : c1 * 8;
+            if (n > 0) {
+                const long long end = (long long)off + n;
+                Range r0{off, (int)min(end, npx), p, cat};
+                if (r0.q0 < hi && r0.q1 > lo) rg[atomicAdd(&nrg, 1)] = r0;
+                if (end > npx) {
+                    Range r1{0, (int)(end - npx), p, cat + (int)(npx - off)};
+                    if (r1.q0 < hi && r1.q1 > lo) rg[atomicAdd(&nrg, 1)] = r1;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const int nr = nrg;
+    const u64* maps = maps_all + (size_t)b * mw;
     const V* src = reinterpret_cast<const V*>(stego + (size_t)b * npx);
     V* dst = reinterpret_cast<V*>(cover + (size_t)b * npx);
     for (long long cb = c0 + threadIdx.x; cb < c1; cb += 4 * 256) {
@@ -1334,7 +1352,7 @@ static int launch_scan_fast(const codec_params* P, const void* cover, void* steg
                             uint32_t* orv, hipStream_t st) {
     const int sb = P->block;
     const int nb = (P->H + sb - 1) / sb;
-    const int target = (int)knob("CODEC_SCAN_WGS", sizeof(T) == 2 ? 256 : 1024);
+    const int target = (int)knob("CODEC_SCAN_WGS", sizeof(T) == 2 ? 1024 : 1024);   // tools/tune.py
     const bool nt = knob("CODEC_NT", 1) != 0;
     int wgps = (target + P->B - 1) / P->B;
     wgps = wgps < 1 ? 1 : (wgps > nb ? nb : wgps);
@@ -1486,7 +1504,7 @@ int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps
         } else {
         const long long nchunks = npx / 8;
         // many small address-ordered workgroups stream best (tools/ubench_stream.hip)
-        const long long target = knob("CODEC_RESTORE_WGS", 32768);
+        const long long target = knob("CODEC_RESTORE_WGS", 32768);   // tools/tune.py
         const bool nt = knob("CODEC_NT", 1) != 0;
         long long wgps = (target + P->B - 1) / P->B;
         long long per = (nchunks + wgps - 1) / wgps;
