@@ -164,24 +164,49 @@ __device__ __forceinline__ int np_node_size(int r, int d, int j, int* start) {
     return n;
 }
 
-// np.sum semantics over m <= 65536 elements, computed by a 1024-thread block:
-// thread t owns chunk t/128 and bottom slot t%128 of that chunk's (depth-7) tree.
-// Leaves reached above depth 7 are carried down the left spine; internal nodes are
-// re-summed bottom-up exactly in numpy's order.  Returns the sum to every thread.
+// np.sum semantics over m <= 65536 elements, computed by a 1024-thread block.
+// Slot t = (chunk t/128, bottom slot t%128 of that chunk's depth-7 tree); leaves reached
+// above depth 7 are carried down the left spine.  Leaves are summed wave-cooperatively:
+// 8 lanes per leaf, lane q holding numpy's accumulator r[q] (so one load instruction
+// touches 8 contiguous 64-byte segments), combined as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)).
+// Internal nodes are then re-added bottom-up in numpy's order.  Returns the sum to all.
 template <class F>
 __device__ double np_sum_block1024(const F& f, int m, double* vals /*[1024]*/) {
     const int t = threadIdx.x;
-    const int c = t >> 7, j = t & 127;
-    const int cstart = c * NP_CHUNK;
-    const int r = min(NP_CHUNK, max(0, m - cstart));
-    double v = 0.0;
-    if (r > 0) {
-        int a;
-        const int n = np_node_size(r, 7, j, &a);
-        if (n > 0) v = np_leaf(f, cstart + a, n);
+    {
+        const int lane = t & 63, wv = t >> 6, q = lane & 7;
+        for (int rnd = 0; rnd < 8; ++rnd) {
+            const int slot = wv * 64 + rnd * 8 + (lane >> 3);
+            const int cs = (slot >> 7) * NP_CHUNK;
+            const int rr = min(NP_CHUNK, max(0, m - cs));
+            int a = 0, n = 0;
+            if (rr > 0) n = np_node_size(rr, 7, slot & 127, &a);
+            a += cs;
+            const int lim = n - (n % 8);
+            double acc = 0.0;
+            if (n >= 8) {
+                acc = f(a + q);
+                for (int i = 8; i < lim; i += 8) acc += f(a + i + q);
+            }
+            const double s2 = acc + __shfl_xor(acc, 1, 64);
+            const double s4 = s2 + __shfl_xor(s2, 2, 64);
+            const double s8 = s4 + __shfl_xor(s4, 4, 64);
+            if (q == 0) {
+                double res;
+                if (n >= 8) {
+                    res = s8;
+                    for (int i = lim; i < n; ++i) res += f(a + i);
+                } else {
+                    res = -0.0;
+                    for (int i = 0; i < n; ++i) res += f(a + i);
+                }
+                vals[slot] = n > 0 ? res : 0.0;
+            }
+        }
     }
-    vals[t] = v;
     __syncthreads();
+    const int c = t >> 7, j = t & 127;
+    const int r = min(NP_CHUNK, max(0, m - c * NP_CHUNK));
     for (int d = 6; d >= 0; --d) {
         const bool act = (r > 0) && (j < (1 << d));
         double nv = 0.0;
