@@ -175,18 +175,25 @@ __device__ double np_sum_block1024(const F& f, int m, double* vals /*[1024]*/) {
     const int t = threadIdx.x;
     {
         const int lane = t & 63, wv = t >> 6, q = lane & 7;
-        for (int rnd = 0; rnd < 8; ++rnd) {
-            const int slot = wv * 64 + rnd * 8 + (lane >> 3);
-            const int cs = (slot >> 7) * NP_CHUNK;
+        const int nchunks_ = (m + NP_CHUNK - 1) / NP_CHUNK;
+        for (int rnd = 0; rnd < nchunks_; ++rnd) {          // one numpy buffer per round
+            const int slot = rnd * 128 + wv * 8 + (lane >> 3);
+            const int cs = rnd * NP_CHUNK;
             const int rr = min(NP_CHUNK, max(0, m - cs));
             int a = 0, n = 0;
             if (rr > 0) n = np_node_size(rr, 7, slot & 127, &a);
             a += cs;
             const int lim = n - (n % 8);
+            // all of this lane's (<= 16) loads are issued before the dependent adds
+            double tv[NP_LEAF / 8];
+#pragma unroll
+            for (int u = 0; u < NP_LEAF / 8; ++u) tv[u] = (8 * u < lim) ? f(a + 8 * u + q) : 0.0;
             double acc = 0.0;
             if (n >= 8) {
-                acc = f(a + q);
-                for (int i = 8; i < lim; i += 8) acc += f(a + i + q);
+                acc = tv[0];
+#pragma unroll
+                for (int u = 1; u < NP_LEAF / 8; ++u)
+                    if (8 * u < lim) acc += tv[u];
             }
             const double s2 = acc + __shfl_xor(acc, 1, 64);
             const double s4 = s2 + __shfl_xor(s2, 2, 64);
@@ -694,6 +701,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     __shared__ double vals[1024];
     __shared__ uint32_t sh[20];
     __shared__ uint32_t pops_sh[16];
+    __shared__ double mis_sh[16];
     __shared__ double best_sc[16];
     __shared__ int best_ix[16];
 
@@ -717,14 +725,20 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     uint32_t pop[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) pop[i] = 0;
-    for (int k = 0; k < bpt; ++k) {
-        const int v = v0 + k;
-        if (v < Rp) {
-            const uint32_t c = hist[v];
-            if (c) {
-                nzmask |= 1ull << k;
+    for (int k0 = 0; k0 < bpt; k0 += 16) {
+        uint32_t cc[16];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) pop[i] += ((v >> i) & 1) ? c : 0u;
+        for (int u = 0; u < 16; ++u) {            // 16 loads in flight, then the adds
+            const int v = v0 + k0 + u;
+            cc[u] = (k0 + u < bpt && v < Rp) ? hist[v] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int v = v0 + k0 + u;
+            if (cc[u]) {
+                nzmask |= 1ull << (k0 + u);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) pop[i] += ((v >> i) & 1) ? cc[u] : 0u;
             }
         }
     }
@@ -742,9 +756,25 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     // terms of the non-zero bins in ascending value order, computed once
     if (lut_ok) {
         uint32_t r = rank0;
-        for (u64 msk = nzmask; msk; msk &= msk - 1, ++r) {
-            const int v = v0 + __ffsll((long long)msk) - 1;
-            terms[r] = plogp(lut, hist[v], Nd);
+        u64 msk = nzmask;
+        while (msk) {
+            int vv[8];
+            uint32_t cc[8];
+            int k = 0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {         // up to 8 independent hist->lut chains
+                vv[u] = -1;
+                if (msk) { vv[u] = v0 + __ffsll((long long)msk) - 1; msk &= msk - 1; ++k; }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) cc[u] = vv[u] >= 0 ? hist[vv[u]] : 1u;
+            double tt[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) tt[u] = plogp(lut, cc[u], Nd);
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (u < k) terms[r + u] = tt[u];
+            r += k;
         }
     }
     __syncthreads();
@@ -758,9 +788,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     int s = 1;
     bool decided = false;
     double cum = 0.0;
-    double mis[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) mis[i] = 0.0;
+    if (t < 16) mis_sh[t] = 0.0;
     const bool need_decision = (P.fixed_s <= 0);
     for (int i = 0; i < P.nbits && i < 16 && lut_ok; ++i) {
         if (!(need_decision && !decided) && !P.all_mi) break;
@@ -773,7 +801,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
             mi = (hx + Hy) - hxy;                                // codec.py:554
             if (!(mi > 0.0)) mi = 0.0;                           // max(0.0, mi)
         }
-        mis[i] = mi;
+        if (t == 0) mis_sh[i] = mi;
         if (need_decision && !decided) {
             cum += mi;
             if (cum >= target) { s = i + 1; decided = true; }
@@ -864,7 +892,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     M->target = target;
     M->cum_info = cum;
     M->reserved_d = 0.0;
-    for (int i = 0; i < 16; ++i) M->mi[i] = mis[i];
+    for (int i = 0; i < 16; ++i) M->mi[i] = mis_sh[i];
 }
 
 // ------------------------------------------------------------------ per-slice window cache
