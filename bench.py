@@ -38,6 +38,7 @@ def parse():
     ap.add_argument("--payload-chars", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event pass")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
     return ap.parse_args()
 
 
@@ -58,6 +59,25 @@ def make_covers(torch, kind, b, h, w, device, seed):
         noise = torch.randn((1, h, w), generator=g, device=device) * 16.0
         out[i] = torch.clamp(torch.round(base + noise), 0, 4095).to(torch.int32).to(torch.uint16)[0]
     return out
+
+
+def pmc_traffic(kernel: str, b: int, h: int, w: int, kind: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, tools/pmc_summary.py: FETCH_SIZE x2 (gfx950 correction)
+    + WRITE_SIZE, KB -> bytes), when it was collected on this exact configuration."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    cfg = d.get("config", {})
+    if (cfg.get("batch"), cfg.get("h"), cfg.get("w"), cfg.get("kind")) != (b, h, w, kind):
+        return None
+    k = d.get("kernels", {}).get(kernel)
+    if not k:
+        return None
+    return {"hbm_bytes_per_launch": k["hbm_bytes_per_launch"], "source": d.get("source", path)}
 
 
 def cpu_baseline(size: int, kind: str, chars: int, budget_s: float):
@@ -95,14 +115,19 @@ def main():
 
     import codec_tcc_amd as ct
     from codec_tcc_amd import _lib, synth
+    from codec_tcc_amd import distributed as D
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else torch.cuda.current_device())
+        torch.cuda.set_device(local % ndev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local % ndev))
+        else:   # rehearsal of the multi-rank path on fewer GPUs (e.g. gloo, 2 ranks on 1 GPU)
+            dist.init_process_group(args.backend)
+    dev = torch.device("cuda", local % ndev if world > 1 else torch.cuda.current_device())
     B, H, W = args.batch, args.size, args.size
 
     covers = make_covers(torch, args.kind, B, H, W, dev, seed=rank * B)
@@ -115,19 +140,18 @@ def main():
     meta = torch.empty((B, _lib.META_BYTES), dtype=torch.uint8, device=dev)
     cover_out = torch.empty((B, H, W), dtype=torch.uint16, device=dev)
     payload_out = torch.empty((B, pl.payload_words), dtype=torch.int64, device=dev)
-    rec_words = (_lib.META_BYTES + 7) // 8 + pl.map_words
+    rec_words = D.record_words(pl.map_words)
     gathered = torch.empty((world * B, rec_words), dtype=torch.int64, device=dev) if world > 1 else None
-    record = torch.empty((B, rec_words), dtype=torch.int64, device=dev) if world > 1 else None
+    record = torch.zeros((B, rec_words), dtype=torch.int64, device=dev) if world > 1 else None
 
     def step():
         codec.encode(covers, pl, stego=stego, maps=maps, meta=meta)
         codec.decode(stego, maps, meta, payload_words=pl.payload_words, map_words=pl.map_words,
                      cover=cover_out, payload=payload_out)
         if world > 1:
-            # per-slice fixed-size records: slice meta + packed location map -> every rank
-            record[:, : (_lib.META_BYTES + 7) // 8].view(torch.uint8)[:, : _lib.META_BYTES].copy_(meta)
-            record[:, (_lib.META_BYTES + 7) // 8:].copy_(maps)
-            dist.all_gather_into_tensor(gathered, record)
+            # per-slice fixed-size records (slice meta + packed location map) -> every rank
+            D.pack_records(meta, maps, out=record)
+            D.gather_records(record, out=gathered)
 
     for _ in range(args.warmup):
         step()
@@ -181,6 +205,10 @@ def main():
         roof = {"bound": "hbm", "kernel": "k_scan_fast", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "algorithmic_bytes_per_launch": bytes_scan, "avg_launch_ms": round(t_scan * 1e3, 4)}
+        tr = pmc_traffic("k_scan_fast", B, H, W, args.kind)
+        if tr is not None:
+            roof["traffic"] = tr["hbm_bytes_per_launch"]
+            roof["traffic_source"] = tr["source"]
     step_bytes = npx_rank * 8                        # cover r + stego w + stego r + cover w
     if rank == 0:
         out = {

@@ -29,6 +29,14 @@ if has prof; then
   find gpurun_out/prof -name "*stats*" | head
   [ $rc -eq 0 ] || exit $rc
 fi
+if has multi; then
+  # 2-rank rehearsal of the N>1 path on this 1-GPU box (gloo: RCCL needs distinct GPUs)
+  timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+      --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 1 --batch 64 --backend gloo --cpu-seconds 0 \
+      > gpurun_out/bench_multi.json 2> gpurun_out/bench_multi.err; rc=$?
+  echo "multi rc=$rc"; cat gpurun_out/bench_multi.json; tail -5 gpurun_out/bench_multi.err
+  [ $rc -eq 0 ] || exit $rc
+fi
 if has pmc; then
   R="$GRAFT_REPO_ROOT"
   for C in FETCH_SIZE WRITE_SIZE; do
