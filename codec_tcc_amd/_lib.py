@@ -82,6 +82,10 @@ def load(path: str = LIB_PATH):
     global _lib, _load_error
     if _lib is not None:
         return _lib
+    # torch must be imported first: it ships its own libamdhip64 (soname libamdhip64.so.7).
+    # Loaded first, it is the one our NEEDED entry binds to; loaded second, the process
+    # would hold two HIP runtimes and device pointers from one are unknown to the other.
+    import torch  # noqa: F401
     if not os.path.exists(path):
         raise RuntimeError(f"libcodec_hip.so not found at {path}: build it with "
                            f"`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback)")
