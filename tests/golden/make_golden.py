@@ -280,6 +280,58 @@ def main():
     with open(os.path.join(HERE, "kat2048.json"), "w") as f:
         json.dump(kat, f, indent=1)
 
+    # --- container (.bin "STGC", codec.py:601-750) bytes made by the reference itself
+    import tempfile
+    import zlib
+    cont = {}
+    with tempfile.TemporaryDirectory() as d:
+        k = 0
+        for name, codec, fake in (("pe_b0.4_main", "jxl", b"<jxl bytes>"), ("torax_b0.4_1k", "png", b"\x00\x01" * 50),
+                                  ("ct12_37x53", "j2k", b""), ("u8_5x5", "weird", b"xyz")):
+            res = out  # cases already computed above
+            s = int(res[f"{name}/s"])
+            perm = [int(x) for x in res[f"{name}/perm"]]
+            sizes = [int(x) for x in res[f"{name}/sizes"]]
+            key = str(res[f"{name}/image_key"])
+            img = images[key]
+            h, w = img.shape
+            bm = np.unpackbits(res[f"{name}/bitmaps_packed"])[: s * h * w].astype(np.uint8)
+            blob = zlib.compress(bm.tobytes())
+            with Quiet():
+                hdr = ref.create_header(codec=codec, s=s, segments_lengths=sizes, segments_indices=perm,
+                                        bitmaps_blob_size=len(blob), width=w, height=h, start_offset=0,
+                                        align_across_planes=False)
+                path = os.path.join(d, f"c{k}.bin")
+                size = ref.create_binary_file(path, hdr, fake, blob)
+                md, bmd, stg = ref.parse_bin_file(path)
+            data = open(path, "rb").read()
+            cont[f"{name}/codec"] = np.array(codec)
+            cont[f"{name}/file"] = np.frombuffer(data, np.uint8)
+            cont[f"{name}/fake_stego"] = np.frombuffer(fake, np.uint8)
+            cont[f"{name}/file_size"] = np.int64(size)
+            cont[f"{name}/parsed_json"] = np.frombuffer(json.dumps(md).encode(), np.uint8)
+            assert bmd == blob and stg == fake
+            k += 1
+        # header overflow the reference raises on (struct.error): 2048^2 offsets / seglens
+        with Quiet():
+            for label, kw in (("big_offset", dict(start_offset=70000, segments_lengths=[1])),
+                              ("neg_seglen", dict(start_offset=0, segments_lengths=[-1]))):
+                try:
+                    ref.create_header(codec="jxl", s=1, segments_indices=[0], bitmaps_blob_size=1, width=4,
+                                      height=4, align_across_planes=False, **kw)
+                    cont[f"err/{label}"] = np.array("none")
+                except Exception as e:  # struct.error
+                    cont[f"err/{label}"] = np.array(type(e).__name__)
+    cont["__names__"] = np.array(["pe_b0.4_main", "torax_b0.4_1k", "ct12_37x53", "u8_5x5"])
+    np.savez_compressed(os.path.join(HERE, "container.npz"), **cont)
+
+    # --- DICOM files: header/trailer bytes around the pixel data (pixels are in images.npz)
+    pe_raw = open(os.path.join(REF, "images", "pe.dcm"), "rb").read()
+    tx_raw = open(os.path.join(REF, "images", "torax.dcm"), "rb").read()
+    np.savez_compressed(os.path.join(HERE, "dicom_headers.npz"),
+                        pe_head=np.frombuffer(pe_raw[:7010], np.uint8), pe_tail=np.frombuffer(pe_raw[7010 + 524288:], np.uint8),
+                        torax_head=np.frombuffer(tx_raw[:888], np.uint8), torax_tail=np.frombuffer(tx_raw[888 + 262144:], np.uint8))
+
 
 if __name__ == "__main__":
     main()
