@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event pass")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
+    ap.add_argument("--pee", type=int, default=1, help="also time the MED-PEE path (north-star algorithm)")
+    ap.add_argument("--pee-T", type=int, default=2)
     return ap.parse_args()
 
 
@@ -106,6 +108,78 @@ def cpu_baseline(size: int, kind: str, chars: int, budget_s: float):
                   f"(decompose+hybrid embed+merge+extract_local_planes+decode_message), 1 process",
         "seconds": round(t_work, 2),
     }
+
+
+def _profile(lib, _lib, fn, steps):
+    import ctypes as C
+    import torch
+    cap = 64 * steps
+    _lib.check(lib.codec_profile_begin(cap), "codec_profile_begin")
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    ms = (C.c_float * cap)()
+    tags = (C.c_int32 * cap)()
+    n = lib.codec_profile_end(ms, tags, cap)
+    out = {}
+    for i in range(max(n, 0)):
+        out.setdefault(_lib.KERNEL_TAGS.get(tags[i], str(tags[i])), []).append(ms[i])
+    return {k: float(np.mean(v)) for k, v in out.items()}
+
+
+def bench_pee(args, torch, dist, world, dev, covers, B, H, W):
+    """MED-PEE embed + extract over the same resident batch (1 KB payload per slice):
+    k_pee_scan (copy + per-tile counts) + locate + prefix embed; copy + prefix recover."""
+    from codec_tcc_amd import _lib, synth
+    from codec_tcc_amd.pee import PeeCodec
+    codec = PeeCodec(B, H, W, dtype="uint16", T=args.pee_T, device=dev)
+    pay = [synth.payload(args.payload_chars, 99 + i) for i in range(B)]
+    packed = codec.pack_payloads(pay)
+    stego = torch.empty_like(covers)
+    cov2 = torch.empty_like(covers)
+    lm = torch.empty((B, codec.lm_words), dtype=torch.int64, device=dev)
+    meta = torch.empty((B, _lib.PEE_META_BYTES), dtype=torch.uint8, device=dev)
+    pw = packed[0].shape[1]
+    outw = torch.empty((B, pw), dtype=torch.int64, device=dev)
+
+    def step():
+        codec.embed(covers, None, stego=stego, lm=lm, meta=meta, packed=packed)
+        codec.extract(stego, meta, lm, payload_words=pw, cover=cov2, payload=outw)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    from codec_tcc_amd.pee import PeeEncoded
+    recs = PeeEncoded(stego, lm, meta, packed[1], pw).records()
+    ok = bool(torch.equal(cov2.view(torch.int16), covers.view(torch.int16))) and all(r.status == 0 for r in recs)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    kern = _profile(_lib.load(), _lib, step, args.steps) if not args.no_profile else {}
+    res = {"value": round(B * H * W * world * args.steps / el / 1e6, 1), "unit": "Mpixels/s",
+           "ms_per_step": round(el / args.steps * 1e3, 4), "T": args.pee_T, "roundtrip_ok": ok,
+           "end_candidates_mean": float(np.mean([r.end + 1 for r in recs])),
+           "kernels_ms": {k: round(v, 4) for k, v in kern.items()}}
+    if "k_pee_scan" in kern:
+        t_scan = kern["k_pee_scan"] / 1e3
+        by = B * H * W * 4
+        res["roofline"] = {"bound": "hbm", "kernel": "k_pee_scan", "achieved": round(by / t_scan / 1e9, 1),
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(by / t_scan / 1e9 / HBM_PEAK_GBS, 4),
+                           "algorithmic_bytes_per_launch": by}
+        t_emb = sum(kern.get(k, 0.0) for k in ("k_pee_scan", "k_pee_locate", "k_pee_embed")) / 1e3
+        res["embed_read_roofline_frac"] = round(B * H * W * 2 / t_emb / 1e9 / HBM_PEAK_GBS, 4)
+    return res
 
 
 def main():
@@ -190,6 +264,10 @@ def main():
         for i in range(max(n, 0)):
             kernels.setdefault(_lib.KERNEL_TAGS.get(tags[i], str(tags[i])), []).append(ms[i])
 
+    pee = None
+    if args.pee:
+        pee = bench_pee(args, torch, dist, world, dev, covers, B, H, W)
+
     npx_rank = B * H * W
     total_px = npx_rank * world
     ms_step = elapsed / args.steps * 1e3
@@ -226,6 +304,8 @@ def main():
             "s_values": s_vals,
             "roundtrip_ok": ok,
         }
+        if pee is not None:
+            out["pee"] = pee
         if args.cpu_seconds > 0 and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.size, args.kind, args.payload_chars, args.cpu_seconds)
         print(json.dumps(out), flush=True)

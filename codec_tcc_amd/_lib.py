@@ -48,7 +48,20 @@ class SliceMeta(C.Structure):
     ]
 
 
+class PeeParams(C.Structure):
+    _fields_ = [("B", C.c_int32), ("H", C.c_int32), ("W", C.c_int32), ("bytes", C.c_int32),
+                ("T", C.c_int32), ("maxval", C.c_int32), ("payload_words", C.c_int32), ("lm_words", C.c_int32)]
+
+
+class PeeMeta(C.Structure):
+    _fields_ = [("T", C.c_int32), ("maxval", C.c_int32), ("L", C.c_int32), ("end", C.c_int32),
+                ("nc", C.c_int32), ("ntiles", C.c_int32), ("tile_end", C.c_int32), ("status", C.c_int32),
+                ("capacity", C.c_int32), ("lm_count", C.c_int32), ("h", C.c_int32), ("w", C.c_int32),
+                ("reserved", C.c_int32 * 4)]
+
+
 META_BYTES = C.sizeof(SliceMeta)
+PEE_META_BYTES = C.sizeof(PeeMeta)
 LAYOUT_BYTES = C.sizeof(Layout)
 
 _VP = C.c_void_p
@@ -66,11 +79,15 @@ _SIGS = {
     "codec_restore_dense": (C.c_int, [C.POINTER(Params), _VP, _VP, C.c_int32, _VP, _VP, _VP]),
     "codec_unpack_planes": (C.c_int, [C.POINTER(Params), _VP, C.c_int32, C.c_int32, _VP, C.c_int32, _VP]),
     "codec_merge_planes": (C.c_int, [C.POINTER(Params), _VP, C.c_int32, C.c_int32, _VP, _VP]),
+    "codec_pee_workspace_bytes": (C.c_size_t, [C.POINTER(PeeParams)]),
+    "codec_pee_embed": (C.c_int, [C.POINTER(PeeParams), _VP, _VP, _VP, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),
+    "codec_pee_extract": (C.c_int, [C.POINTER(PeeParams), _VP, _VP, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),
     "codec_profile_begin": (C.c_int, [C.c_int32]),
     "codec_profile_end": (C.c_int, [_VP, _VP, C.c_int32]),
 }
 KERNEL_TAGS = {1: "k_scan_fast", 2: "k_scan_generic", 3: "k_block_exact", 4: "k_decide",
-               5: "k_embed", 6: "k_restore", 7: "k_gather", 8: "other"}
+               5: "k_embed", 6: "k_restore", 7: "k_gather", 8: "other", 9: "k_pee_scan", 10: "k_pee_locate",
+               11: "k_pee_embed", 12: "k_pee_copy", 13: "k_pee_dcount", 14: "k_pee_recover"}
 EXPORTS = tuple(_SIGS)
 
 _lib = None

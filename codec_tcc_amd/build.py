@@ -15,7 +15,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-SRC = os.path.join(HERE, "csrc", "codec_hip.hip")
+SRCS = [os.path.join(HERE, "csrc", "codec_hip.hip"), os.path.join(HERE, "csrc", "codec_pee.hip")]
+HDRS = [os.path.join(HERE, "csrc", "codec_common.h")]
 OUT = os.path.join(HERE, "libcodec_hip.so")
 INC = os.path.join(REPO, "include")
 ARCH = os.environ.get("CODEC_OFFLOAD_ARCH", "gfx950")
@@ -35,7 +36,7 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = [SRC, os.path.join(INC, "codec_tcc.h"), __file__]
+    deps = SRCS + HDRS + [os.path.join(INC, "codec_tcc.h"), __file__]
     return any(os.path.getmtime(d) > t for d in deps)
 
 
@@ -43,7 +44,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return OUT
     tmp = OUT + ".tmp"
-    cmd = [hipcc(), *FLAGS, f"-I{INC}", SRC, "-o", tmp]
+    cmd = [hipcc(), *FLAGS, f"-I{INC}", *SRCS, "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -16,65 +16,10 @@
 //                                  and the payload bits (ballot-packed).
 // Numerics: this file MUST be compiled with -ffp-contract=off (no FMA contraction) so the
 // float64 sums reproduce numpy's bit for bit.
-#include <hip/hip_runtime.h>
-#include <stdarg.h>
-#include <stdint.h>
-#include <stdio.h>
-#include <stdlib.h>
-#include <string.h>
+#include "codec_common.h"
 
-#include "codec_tcc.h"
-
-typedef unsigned long long u64;
-
-// ------------------------------------------------------------------ error reporting
-static thread_local char g_err[512] = "";
-
-static int set_err(int code, const char* fmt, ...) {
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(g_err, sizeof(g_err), fmt, ap);
-    va_end(ap);
-    return code;
-}
-
-#define CODEC_EINVAL (-1000)
-#define HIP_TRY(expr)                                                                     \
-    do {                                                                                  \
-        hipError_t e_ = (expr);                                                           \
-        if (e_ != hipSuccess)                                                             \
-            return set_err(-(int)e_, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_),      \
-                           __FILE__, __LINE__);                                           \
-    } while (0)
-#define LAUNCH_CHECK(name)                                                                \
-    do {                                                                                  \
-        hipError_t e_ = hipGetLastError();                                                \
-        if (e_ != hipSuccess)                                                             \
-            return set_err(-(int)e_, "launch %s: %s", name, hipGetErrorString(e_));       \
-    } while (0)
-
-// ------------------------------------------------------------------ profiling hooks
-struct ProfWin {
-    hipEvent_t* ev = nullptr;
-    int32_t* tag = nullptr;
-    int cap = 0, n = 0;
-};
-static ProfWin g_prof;
-
-struct ProfScope {   // records a start event now and the end event at scope exit
-    hipStream_t st;
-    int slot = -1;
-    ProfScope(hipStream_t s, int tag) : st(s) {
-        if (g_prof.ev && g_prof.n < g_prof.cap) {
-            slot = g_prof.n++;
-            g_prof.tag[slot] = tag;
-            hipEventRecord(g_prof.ev[2 * slot], st);
-        }
-    }
-    ~ProfScope() {
-        if (slot >= 0) hipEventRecord(g_prof.ev[2 * slot + 1], st);
-    }
-};
+thread_local char g_err[512] = "";
+ProfWin g_prof;
 
 // ------------------------------------------------------------------ numpy float emulation
 // numpy's add.reduce over a contiguous float64 array (np.sum) walks it in buffers of
@@ -235,65 +180,6 @@ __device__ double np_sum_block1024(const F& f, int m, double* vals /*[1024]*/) {
     return res;
 }
 
-// ------------------------------------------------------------------ block primitives
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    return x;
-}
-
-// exclusive scan over the block (NT threads); sh needs NT/64+1 words
-template <int NT>
-__device__ uint32_t block_excl_scan(uint32_t x, uint32_t* sh, uint32_t* total) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t inc = wave_incl_scan(x);
-    if (lane == 63) sh[wv] = inc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (int w = 0; w < NT / 64; ++w) {
-            const uint32_t tmp = sh[w];
-            sh[w] = acc;
-            acc += tmp;
-        }
-        sh[NT / 64] = acc;
-    }
-    __syncthreads();
-    const uint32_t r = sh[wv] + inc - x;
-    *total = sh[NT / 64];
-    __syncthreads();
-    return r;
-}
-
-template <int NT>
-__device__ uint32_t block_sum_u32(uint32_t x, uint32_t* sh) {
-    uint32_t tot;
-    block_excl_scan<NT>(x, sh, &tot);
-    return tot;
-}
-
-template <int NT>
-__device__ int block_max_i32(int x, int* sh) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) x = max(x, __shfl_xor(x, o, 64));
-    if (lane == 0) sh[wv] = x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int m = sh[0];
-        for (int w = 1; w < NT / 64; ++w) m = max(m, sh[w]);
-        sh[NT / 64] = m;
-    }
-    __syncthreads();
-    const int r = sh[NT / 64];
-    __syncthreads();
-    return r;
-}
-
 // ------------------------------------------------------------------ histogram helpers
 // uint16 covers: 65536 bins kept as 16-bit halves of 32768 LDS words (128 KiB).  An add
 // whose returned old value shows a half wrapping is rare; its exact effect on the two
@@ -417,57 +303,6 @@ __device__ __forceinline__ void hist_add8(uint32_t* lds, uint32_t* ghist, const 
     }
 }
 
-template <typename T> struct Vec8;
-template <> struct Vec8<uint16_t> { typedef uint4 type; };
-template <> struct Vec8<uint8_t> { typedef uint2 type; };
-
-// streaming loads/stores; NT = non-temporal (measured: nt on BOTH the load and the store
-// stream is what lifts a 2 GiB read+write pass from ~5.1 to ~5.9 TB/s, tools/ubench_stream.hip)
-typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-template <bool NT> __device__ __forceinline__ uint4 ldv(const uint4* p) {
-    if constexpr (NT) {
-        const v4u x = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
-        return make_uint4(x.x, x.y, x.z, x.w);
-    } else {
-        return *p;
-    }
-}
-template <bool NT> __device__ __forceinline__ uint2 ldv(const uint2* p) {
-    if constexpr (NT) {
-        const v2u x = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(p));
-        return make_uint2(x.x, x.y);
-    } else {
-        return *p;
-    }
-}
-template <bool NT> __device__ __forceinline__ void stv(uint4* p, const uint4& v) {
-    if constexpr (NT) {
-        v4u x = {v.x, v.y, v.z, v.w};
-        __builtin_nontemporal_store(x, reinterpret_cast<v4u*>(p));
-    } else {
-        *p = v;
-    }
-}
-template <bool NT> __device__ __forceinline__ void stv(uint2* p, const uint2& v) {
-    if constexpr (NT) {
-        v2u x = {v.x, v.y};
-        __builtin_nontemporal_store(x, reinterpret_cast<v2u*>(p));
-    } else {
-        *p = v;
-    }
-}
-
-__device__ __forceinline__ uint32_t vor_of(const uint4& v) { return v.x | v.y | v.z | v.w; }
-__device__ __forceinline__ uint32_t vor_of(const uint2& v) { return v.x | v.y; }
-
-__device__ __forceinline__ uint32_t lsb_count(const uint4& v) {
-    return __popc(v.x & 0x00010001u) + __popc(v.y & 0x00010001u) + __popc(v.z & 0x00010001u) +
-           __popc(v.w & 0x00010001u);
-}
-__device__ __forceinline__ uint32_t lsb_count(const uint2& v) {
-    return __popc(v.x & 0x01010101u) + __popc(v.y & 0x01010101u);
-}
 
 // ------------------------------------------------------------------ K1: scan + copy (fast)
 // Requirements (checked on the host): W % 8 == 0, SB in {8,16,32,64}, stego dtype ==
@@ -1296,13 +1131,7 @@ __global__ __launch_bounds__(256) void k_merge(const Tp* __restrict__ planes, in
 }
 
 // ====================================================================== host side
-static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
-// launch-shape knobs (defaults from measurements on MI355X; env overrides for tuning runs)
-static long long knob(const char* name, long long dflt) {
-    const char* v = getenv(name);
-    return (v && *v) ? atoll(v) : dflt;
-}
 
 static int check_params(const codec_params* P) {
     if (!P) return set_err(CODEC_EINVAL, "params is NULL");
@@ -1319,7 +1148,6 @@ static int check_params(const codec_params* P) {
     return 0;
 }
 
-static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 static bool pow2_fast_block(int b) { return b == 8 || b == 16 || b == 32 || b == 64; }
 

@@ -1,0 +1,114 @@
+"""MED-predictor prediction-error expansion (PEE) on the MI355X -- the algorithm the north
+star names.  The reference contains no PEE code; the scheme is specified in
+oracle/pee_cpu.py (parity unpinned) and summarised in include/codec_tcc.h.
+
+    codec = PeeCodec(B, H, W, dtype="uint16", T=2)
+    enc = codec.embed(covers, payloads)          # stego, location map, per-slice meta
+    bits, cover = codec.extract(enc.stego, enc.meta, enc.lm, lengths=enc.lengths)
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+
+from . import _lib, framing
+from .codec import _elem_bytes, _require_gpu, _stream, _torch
+
+
+@dataclass
+class PeeEncoded:
+    stego: object      # torch [B,H,W]
+    lm: object         # torch.int64 [B, lm_words]: overflow location map, bit k = candidate k
+    meta: object       # torch.uint8 [B, sizeof(codec_pee_meta)]
+    lengths: List[int]
+    payload_words: int
+
+    def records(self) -> List[_lib.PeeMeta]:
+        raw = self.meta.detach().cpu().contiguous().numpy().tobytes()
+        n = len(raw) // _lib.PEE_META_BYTES
+        return [_lib.PeeMeta.from_buffer_copy(raw, i * _lib.PEE_META_BYTES) for i in range(n)]
+
+
+class PeeCodec:
+    def __init__(self, batch: int, height: int, width: int, dtype="uint16", *, T: int = 2,
+                 maxval: Optional[int] = None, device=None):
+        _require_gpu()
+        torch = _torch()
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        nbytes = 2 if "16" in str(dtype) else 1
+        if str(dtype) not in ("uint16", "torch.uint16", "uint8", "torch.uint8"):
+            raise ValueError("A imagem deve ser uint8 ou uint16.")
+        vmax = 65535 if nbytes == 2 else 255
+        self.B, self.H, self.W, self.bytes = int(batch), int(height), int(width), nbytes
+        self.T = int(T)
+        self.maxval = vmax if maxval is None else int(maxval)
+        self.nc = (self.H // 2) * (self.W // 2)
+        self.lm_words = max(1, (self.nc + 63) // 64)
+        P = self._params(1)
+        ws = _lib.load().codec_pee_workspace_bytes(C.byref(P))
+        if ws == 0:
+            _lib.check(-1, "codec_pee_workspace_bytes")
+        self.workspace = torch.empty(int(ws), dtype=torch.uint8, device=self.device)
+
+    def _params(self, payload_words: int) -> _lib.PeeParams:
+        return _lib.PeeParams(B=self.B, H=self.H, W=self.W, bytes=self.bytes, T=self.T, maxval=self.maxval,
+                              payload_words=int(payload_words), lm_words=self.lm_words)
+
+    def pack_payloads(self, payloads):
+        torch = _torch()
+        bits = [framing.to_bits(p) for p in payloads]
+        if len(bits) != self.B:
+            raise ValueError("one payload per slice is required")
+        packed, lengths = framing.pack_bits(bits)
+        return (torch.from_numpy(packed).to(self.device), lengths,
+                torch.tensor(lengths, dtype=torch.int32, device=self.device))
+
+    def embed(self, covers, payloads, *, stego=None, lm=None, meta=None, packed=None) -> PeeEncoded:
+        torch = _torch()
+        if tuple(covers.shape) != (self.B, self.H, self.W) or _elem_bytes(covers) != self.bytes:
+            raise ValueError("covers do not match the codec's shape/dtype")
+        words, lengths, lens_t = packed if packed is not None else self.pack_payloads(payloads)
+        if stego is None:
+            stego = torch.empty_like(covers)
+        if lm is None:
+            lm = torch.empty((self.B, self.lm_words), dtype=torch.int64, device=self.device)
+        if meta is None:
+            meta = torch.empty((self.B, _lib.PEE_META_BYTES), dtype=torch.uint8, device=self.device)
+        P = self._params(words.shape[1])
+        _lib.check(_lib.load().codec_pee_embed(C.byref(P), covers.data_ptr(), stego.data_ptr(), words.data_ptr(),
+                                               lens_t.data_ptr(), meta.data_ptr(), lm.data_ptr(),
+                                               self.workspace.data_ptr(), self.workspace.numel(), _stream()),
+                   "codec_pee_embed")
+        return PeeEncoded(stego=stego, lm=lm, meta=meta, lengths=list(lengths), payload_words=int(words.shape[1]))
+
+    def extract(self, stego, meta, lm, *, payload_words: int, cover=None, payload=None):
+        torch = _torch()
+        if cover is None:
+            cover = torch.empty_like(stego)
+        if payload is None:
+            payload = torch.empty((self.B, int(payload_words)), dtype=torch.int64, device=self.device)
+        P = self._params(payload_words)
+        _lib.check(_lib.load().codec_pee_extract(C.byref(P), stego.data_ptr(), meta.data_ptr(), lm.data_ptr(),
+                                                 cover.data_ptr(), payload.data_ptr(), self.workspace.data_ptr(),
+                                                 self.workspace.numel(), _stream()), "codec_pee_extract")
+        return payload, cover
+
+    def decode(self, enc: PeeEncoded):
+        """(list of 0/1 bit vectors, restored cover tensor); raises if a slice overflowed."""
+        recs = enc.records()
+        bad = [i for i, r in enumerate(recs) if r.status != 0]
+        if bad:
+            raise ValueError(f"payload exceeds PEE capacity in slices {bad} (T={self.T})")
+        words, cover = self.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words)
+        host = words.cpu().numpy()
+        return [framing.unpack_bits(host[i], enc.lengths[i]) for i in range(self.B)], cover
+
+
+def lm_bits(enc: PeeEncoded, b: int) -> np.ndarray:
+    """Location map of slice b as a bool vector over candidates 0..end."""
+    r = enc.records()[b]
+    raw = enc.lm[b].cpu().numpy().view(np.uint8)
+    return np.unpackbits(raw, bitorder="little")[: r.end + 1].astype(bool)

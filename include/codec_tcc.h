@@ -158,6 +158,40 @@ int codec_unpack_planes(const codec_params* P, const void* img, int32_t first, i
 int codec_merge_planes(const codec_params* P, const void* planes, int32_t nplanes,
                        int32_t plane_bytes, void* out, void* stream);
 
+/* ---- MED-predictor prediction-error expansion (the north star's PEE).
+ * Not present in the reference: this build's own scheme, specified in
+ * oracle/pee_cpu.py (parity unpinned; checked bit-exact against that spec and by
+ * reversibility).  Candidates are the (odd, odd) sublattice, whose MED neighbours are
+ * never modified; bit j goes to the j-th expandable candidate (-T <= e < T) in raster
+ * order, others up to `end` are shifted by T, overflow-prone ones are skipped and set in
+ * the location map lm (one bit per candidate index). */
+typedef struct codec_pee_params {
+    int32_t B, H, W;
+    int32_t bytes;         /* 1 = uint8, 2 = uint16                                   */
+    int32_t T;             /* expansion threshold (>= 1)                              */
+    int32_t maxval;        /* largest admissible pixel value (overflow bound)         */
+    int32_t payload_words; /* uint64 words per slice in payload buffers               */
+    int32_t lm_words;      /* uint64 words per slice of the location map (>= nc/64)   */
+} codec_pee_params;
+
+typedef struct codec_pee_meta {
+    int32_t T, maxval, L, end; /* end = last processed candidate index, -1 if none */
+    int32_t nc, ntiles, tile_end, status; /* status 1: payload exceeds capacity    */
+    int32_t capacity, lm_count, h, w;
+    int32_t reserved[4];
+} codec_pee_meta;
+
+size_t codec_pee_workspace_bytes(const codec_pee_params* P);
+/* cover -> stego (full copy + expansion/shifting of candidates 0..end), lm, meta.
+ * lengths[B] (device int32) = payload bits per slice. */
+int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, const uint64_t* payload,
+                    const int32_t* lengths, codec_pee_meta* meta, uint64_t* lm, void* workspace,
+                    size_t workspace_bytes, void* stream);
+/* stego -> exact payload bits + restored cover. */
+int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_pee_meta* meta,
+                      const uint64_t* lm, void* cover_out, uint64_t* payload_out, void* workspace,
+                      size_t workspace_bytes, void* stream);
+
 /* ---- measurement hooks (bench.py): while a profile window is open, every launcher
  * records a hipEvent pair around each kernel it launches, tagged with a CODEC_K_* id.
  * Events are created/destroyed here, outside any launch function. */
@@ -169,6 +203,12 @@ int codec_merge_planes(const codec_params* P, const void* planes, int32_t nplane
 #define CODEC_K_RESTORE 6
 #define CODEC_K_GATHER 7
 #define CODEC_K_OTHER 8
+#define CODEC_K_PEE_SCAN 9
+#define CODEC_K_PEE_LOCATE 10
+#define CODEC_K_PEE_EMBED 11
+#define CODEC_K_PEE_COPY 12
+#define CODEC_K_PEE_DCOUNT 13
+#define CODEC_K_PEE_RECOVER 14
 int codec_profile_begin(int32_t capacity);
 /* after the stream has been synchronised: fills ms[i], tag[i] for the recorded pairs and
  * returns their count (closes the window and frees the events). */

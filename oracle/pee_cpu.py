@@ -1,0 +1,115 @@
+"""CPU oracle for MED-predictor prediction-error expansion.
+
+TEST INFRASTRUCTURE ONLY (same rules as ref_cpu.py).
+
+PARITY UNPINNED: the reference repository names PEE (README.md:3) but contains no PEE
+code, so there is nothing to be bit-exact against.  This module is the
+specification of the build's own scheme; the HIP path is checked bit-exact against it,
+and the scheme against itself by reversibility (encode -> decode is the identity on the
+payload and on the cover).
+
+Scheme (integer only):
+  candidates  pixels (y, x) with y = 2i+1, x = 2j+1 (i < H//2, j < W//2), index k = i*(W//2)+j.
+              Their MED neighbours a = W(y, x-1), b = N(y-1, x), c = NW(y-1, x-1) all have an
+              even coordinate, so they are never modified: prediction at decode time uses
+              the same values, and every candidate can be processed independently.
+  predictor   MED / LOCO-I: c >= max(a,b) -> min(a,b); c <= min(a,b) -> max(a,b); else a+b-c
+  error       e = x - pred
+  expansion   -T <= e < T  : x' = pred + 2e + bit         (one payload bit)
+  shifting    e >= T       : x' = x + T ;  e < -T : x' = x - T
+  overflow    a candidate whose transform could leave [0, maxval] is left unchanged and
+              flagged in the location map (LM)
+  cursor      payload bit j goes to the j-th expandable, non-overflow candidate in index
+              order; processing stops at that candidate for j = L-1 ("end"); candidates
+              after `end` are untouched.  Side information: T, L, end, maxval, LM[0..end].
+  decoding    e' = x' - pred; LM -> unchanged; -2T <= e' < 2T -> bit = e' & 1,
+              x = pred + (e' >> 1); e' >= 2T -> x = x' - T; else x = x' + T.
+"""
+from __future__ import annotations
+
+from typing import Dict, Tuple
+
+import numpy as np
+
+
+def _grids(img: np.ndarray):
+    H, W = img.shape
+    hc, wc = H // 2, W // 2
+    x = img[1:2 * hc:2, 1:2 * wc:2].astype(np.int64)
+    a = img[1:2 * hc:2, 0:2 * wc:2].astype(np.int64)
+    b = img[0:2 * hc:2, 1:2 * wc:2].astype(np.int64)
+    c = img[0:2 * hc:2, 0:2 * wc:2].astype(np.int64)
+    return x, a, b, c
+
+
+def med(a: np.ndarray, b: np.ndarray, c: np.ndarray) -> np.ndarray:
+    lo = np.minimum(a, b)
+    hi = np.maximum(a, b)
+    return np.where(c >= hi, lo, np.where(c <= lo, hi, a + b - c))
+
+
+def classify(x, p, T: int, maxval: int):
+    e = x - p
+    expand = (e >= -T) & (e < T)
+    right = e >= T
+    safe = np.where(expand, (p + 2 * e >= 0) & (p + 2 * e + 1 <= maxval),
+                    np.where(right, x + T <= maxval, x - T >= 0))
+    return e, expand, right, safe
+
+
+def pee_embed(cover: np.ndarray, bits: np.ndarray, T: int = 2, maxval: int | None = None) -> Tuple[np.ndarray, Dict]:
+    if cover.dtype not in (np.uint8, np.uint16) or cover.ndim != 2:
+        raise ValueError("cover must be a 2-D uint8/uint16 image")
+    if T < 1:
+        raise ValueError("T must be >= 1")
+    maxval = int(np.iinfo(cover.dtype).max) if maxval is None else int(maxval)
+    bits = np.asarray(bits, dtype=np.uint8).ravel()
+    L = bits.size
+    x, a, b, c = _grids(cover)
+    p = med(a, b, c)
+    e, expand, right, safe = classify(x, p, T, maxval)
+    es = (expand & safe).ravel()
+    capacity = int(es.sum())
+    if capacity < L:
+        raise ValueError(f"payload of {L} bits exceeds the capacity {capacity} at T={T}")
+    end = int(np.flatnonzero(es)[L - 1]) if L else -1
+    k = np.arange(es.size)
+    proc = (k <= end) & safe.ravel()
+    cursor = np.cumsum(es) - 1
+    bit = np.zeros(es.size, np.int64)
+    bit[es & proc] = bits[cursor[es & proc]]
+    xf, pf, ef = x.ravel(), p.ravel(), e.ravel()
+    rf = right.ravel()
+    new = np.where(es, pf + 2 * ef + bit, np.where(rf, xf + T, xf - T))
+    out = np.where(proc, new, xf)
+    stego = cover.copy()
+    hc, wc = x.shape
+    stego[1:2 * hc:2, 1:2 * wc:2] = out.reshape(hc, wc).astype(cover.dtype)
+    lm = ~safe.ravel()[: end + 1]
+    return stego, {"T": T, "L": L, "end": end, "maxval": maxval, "lm": lm, "capacity": capacity}
+
+
+def pee_extract(stego: np.ndarray, side: Dict) -> Tuple[np.ndarray, np.ndarray]:
+    T, end, L = side["T"], side["end"], side["L"]
+    x, a, b, c = _grids(stego)
+    p = med(a, b, c).ravel()
+    xf = x.ravel()
+    e2 = xf - p
+    k = np.arange(xf.size)
+    lm = np.zeros(xf.size, bool)
+    lm[: end + 1] = side["lm"]
+    act = (k <= end) & ~lm
+    inner = act & (e2 >= -2 * T) & (e2 < 2 * T)
+    bits = (e2[inner] & 1).astype(np.uint8)[:L]
+    rec = np.where(inner, p + (e2 >> 1), np.where(act & (e2 >= 2 * T), xf - T, np.where(act, xf + T, xf)))
+    cover = stego.copy()
+    hc, wc = x.shape
+    cover[1:2 * hc:2, 1:2 * wc:2] = rec.reshape(hc, wc).astype(stego.dtype)
+    return bits, cover
+
+
+def capacity(cover: np.ndarray, T: int = 2, maxval: int | None = None) -> int:
+    maxval = int(np.iinfo(cover.dtype).max) if maxval is None else int(maxval)
+    x, a, b, c = _grids(cover)
+    _e, expand, _r, safe = classify(x, med(a, b, c), T, maxval)
+    return int((expand & safe).sum())

@@ -1,0 +1,86 @@
+"""MED-PEE (north-star algorithm).  Parity UNPINNED against the reference
+(it has no PEE code): the oracle is this build's own specification (oracle/pee_cpu.py),
+checked here by reversibility and edge cases on CPU, and the HIP path is checked
+bit-exact against it on the GPU."""
+import numpy as np
+import pytest
+
+from codec_tcc_amd import synth
+from oracle import pee_cpu as P
+
+
+def _bits(n, seed):
+    return np.random.default_rng(seed).integers(0, 2, n).astype(np.uint8)
+
+
+@pytest.mark.parametrize("kind,h,w", [("ct12", 64, 64), ("ct12", 37, 53), ("u8", 40, 24), ("u16", 32, 32),
+                                      ("ct12", 2, 2), ("ct12", 1, 9)])
+@pytest.mark.parametrize("T", [1, 2, 5])
+def test_oracle_reversible(kind, h, w, T):
+    img = synth.GENERATORS[kind](h, w, 11)
+    cap = P.capacity(img, T)
+    for L in sorted({0, min(1, cap), cap // 2, cap}):
+        st, side = P.pee_embed(img, _bits(L, L), T)
+        bits, cov = P.pee_extract(st, side)
+        np.testing.assert_array_equal(bits, _bits(L, L))
+        np.testing.assert_array_equal(cov, img)
+        if L == 0:
+            np.testing.assert_array_equal(st, img)
+
+
+def test_oracle_overflow_and_capacity():
+    img = np.zeros((16, 16), np.uint16)
+    img[::2] = 65535                       # saturated neighbours -> overflow candidates
+    img[1::4, 1::2] = 65535
+    cap = P.capacity(img, 1)
+    st, side = P.pee_embed(img, _bits(cap, 1), 1)
+    assert side["lm"].any()
+    bits, cov = P.pee_extract(st, side)
+    np.testing.assert_array_equal(cov, img)
+    with pytest.raises(ValueError):
+        P.pee_embed(img, _bits(cap + 1, 2), 1)
+
+
+def test_oracle_med_definition():
+    a = np.array([5, 5, 5, 9])
+    b = np.array([9, 9, 9, 5])
+    c = np.array([10, 4, 7, 7])
+    np.testing.assert_array_equal(P.med(a, b, c), [5, 9, 7, 7])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,h,w,bsz,T", [("ct12", 256, 256, 3, 2), ("ct12", 120, 136, 2, 1), ("u8", 96, 64, 2, 4),
+                                            ("ct12", 37, 53, 2, 3), ("ct12", 2048, 2048, 2, 2), ("u16", 64, 64, 1, 8)])
+def test_gpu_matches_oracle(kind, h, w, bsz, T):
+    torch = pytest.importorskip("torch")
+    from codec_tcc_amd.pee import PeeCodec, lm_bits
+    covers = np.stack([synth.GENERATORS[kind](h, w, 40 + i) for i in range(bsz)])
+    caps = [P.capacity(c, T) for c in covers]
+    payloads = [_bits(min(cap, 8192 - 97 * i), i) for i, cap in enumerate(caps)]
+    codec = PeeCodec(bsz, h, w, dtype=str(covers.dtype), T=T)
+    enc = codec.embed(torch.from_numpy(covers).cuda(), payloads)
+    recs = enc.records()
+    stego = enc.stego.cpu().numpy()
+    for i in range(bsz):
+        st, side = P.pee_embed(covers[i], payloads[i], T)
+        assert recs[i].status == 0 and recs[i].end == side["end"] and recs[i].capacity == side["capacity"]
+        np.testing.assert_array_equal(stego[i], st)
+        np.testing.assert_array_equal(lm_bits(enc, i), side["lm"])
+        assert recs[i].lm_count == int(side["lm"].sum())
+    bits, cover = codec.decode(enc)
+    for i in range(bsz):
+        np.testing.assert_array_equal(bits[i], payloads[i])
+    np.testing.assert_array_equal(cover.cpu().numpy(), covers)
+
+
+@pytest.mark.gpu
+def test_gpu_capacity_exceeded_flags():
+    torch = pytest.importorskip("torch")
+    from codec_tcc_amd.pee import PeeCodec
+    img = synth.ct12(64, 64, 3)[None]
+    cap = P.capacity(img[0], 1)
+    codec = PeeCodec(1, 64, 64, T=1)
+    enc = codec.embed(torch.from_numpy(img).cuda(), [_bits(cap + 5, 0)])
+    assert enc.records()[0].status == 1
+    with pytest.raises(ValueError):
+        codec.decode(enc)
