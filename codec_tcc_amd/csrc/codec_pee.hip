@@ -57,6 +57,61 @@ __device__ __forceinline__ uint32_t px16(const uint4& v, int e) {
 __device__ __forceinline__ uint32_t px8(const uint2& v, int e) {
     return ((e < 4 ? v.x : v.y) >> (8 * (e & 3))) & 0xFFu;
 }
+__device__ __forceinline__ void set_px(uint4& v, int e, uint32_t val) {
+    uint32_t& w = e < 2 ? v.x : (e < 4 ? v.y : (e < 6 ? v.z : v.w));
+    w = (e & 1) ? ((w & 0xFFFFu) | (val << 16)) : ((w & 0xFFFF0000u) | (val & 0xFFFFu));
+}
+__device__ __forceinline__ void set_px(uint2& v, int e, uint32_t val) {
+    uint32_t& w = e < 4 ? v.x : v.y;
+    const int sh = 8 * (e & 3);
+    w = (w & ~(0xFFu << sh)) | ((val & 0xFFu) << sh);
+}
+template <typename V> __device__ __forceinline__ uint32_t get_px(const V& v, int e);
+template <> __device__ __forceinline__ uint32_t get_px<uint4>(const uint4& v, int e) { return px16(v, e); }
+template <> __device__ __forceinline__ uint32_t get_px<uint2>(const uint2& v, int e) { return px8(v, e); }
+
+// The 4 candidates of tile slot (t, tid): k = 1024 t + 4 tid + u.  VEC (W % 8 == 0): they
+// are the odd pixels of one aligned 8-pixel chunk of row pair r, loaded as two vectors;
+// otherwise scalar loads per candidate.
+template <typename T, bool VEC>
+struct Quad {
+    typedef typename Vec8<T>::type V;
+    V v0, v1;           // VEC: rows 2r (N/NW) and 2r+1 (candidates, W)
+    size_t o1;          // VEC: element offset of v1
+    int x[4], a[4], b[4], c[4];
+    __device__ __forceinline__ void load(const T* img, int W, int wc, int k0, int kmax) {
+        if constexpr (VEC) {
+            if (k0 > kmax) return;
+            const int item = k0 >> 2, CR = W / 8;
+            const int r = item / CR, cc = item - r * CR;
+            const size_t o0 = (size_t)(2 * r) * W + (size_t)cc * 8;
+            o1 = o0 + W;
+            v0 = *reinterpret_cast<const V*>(img + o0);
+            v1 = *reinterpret_cast<const V*>(img + o1);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                x[u] = (int)get_px(v1, 2 * u + 1); a[u] = (int)get_px(v1, 2 * u);
+                b[u] = (int)get_px(v0, 2 * u + 1); c[u] = (int)get_px(v0, 2 * u);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (k0 + u <= kmax) pee_load(img, W, wc, k0 + u, &x[u], &a[u], &b[u], &c[u]);
+        }
+    }
+    // write candidate u's new value (VEC: into v1; flushed by store())
+    __device__ __forceinline__ void put(T* img, int W, int wc, int k, int u, int val) {
+        if constexpr (VEC) {
+            set_px(v1, 2 * u + 1, (uint32_t)val);
+        } else {
+            const int i = k / wc, j = k - (k / wc) * wc;
+            img[(size_t)(2 * i + 1) * W + 2 * j + 1] = (T)val;
+        }
+    }
+    __device__ __forceinline__ void store(T* img) {
+        if constexpr (VEC) *reinterpret_cast<V*>(img + o1) = v1;
+    }
+};
 
 // ---- scan: stream copy + per-tile count of expandable non-overflow candidates (W % 8 == 0)
 template <typename T, bool NT>
@@ -218,7 +273,7 @@ __global__ __launch_bounds__(256) void k_pee_locate(const T* __restrict__ img, i
 }
 
 // ---- embed: prefix tiles only
-template <typename T>
+template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void k_pee_embed(const T* __restrict__ cover, T* __restrict__ stego, int H, int W,
                                                    const u64* __restrict__ payload_all, int pw,
                                                    const uint32_t* __restrict__ tile_off_all, int ntiles_max,
@@ -238,25 +293,25 @@ __global__ __launch_bounds__(256) void k_pee_embed(const T* __restrict__ cover, 
     const uint32_t* off = tile_off_all + (size_t)b * ntiles_max;
     for (int t = blockIdx.x; t <= tile_end; t += gridDim.x) {
         if (threadIdx.x < PEE_TILE / 32) lm32[threadIdx.x] = 0;
+        const int k0 = t * PEE_TILE + 4 * threadIdx.x;
+        Quad<T, VEC> q;
+        q.load(src, W, wc, k0, end);
         PeeCand pc[4];
         uint32_t local = 0;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int k = t * PEE_TILE + 4 * threadIdx.x + u;
             pc[u].expand = pc[u].safe = pc[u].right = false;
-            if (k <= end) {
-                int x, a, bb, cc;
-                pee_load(src, W, wc, k, &x, &a, &bb, &cc);
-                pc[u] = pee_classify(x, a, bb, cc, Tthr, maxval);
+            if (k0 + u <= end) {
+                pc[u] = pee_classify(q.x[u], q.a[u], q.b[u], q.c[u], Tthr, maxval);
                 local += (pc[u].expand && pc[u].safe) ? 1u : 0u;
             }
         }
         uint32_t tot;
-        uint32_t cur = off[t] + block_excl_scan<256>(local, sh, &tot);   // syncs: lm32 zeroed
+        uint32_t cur = off[t] + block_excl_scan<256>(local, sh, &tot);   // also orders lm32 zeroing
         uint32_t nib = 0, unsafe = 0;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int k = t * PEE_TILE + 4 * threadIdx.x + u;
+            const int k = k0 + u;
             if (k > end) continue;
             if (!pc[u].safe) { nib |= 1u << u; ++unsafe; continue; }
             int nv;
@@ -267,9 +322,9 @@ __global__ __launch_bounds__(256) void k_pee_embed(const T* __restrict__ cover, 
             } else {
                 nv = pc[u].right ? pc[u].x + Tthr : pc[u].x - Tthr;
             }
-            const int i = k / wc, j = k - (k / wc) * wc;
-            dst[(size_t)(2 * i + 1) * W + 2 * j + 1] = (T)nv;
+            q.put(dst, W, wc, k, u, nv);
         }
+        if (k0 <= end) q.store(dst);
         if (nib) atomicOr(&lm32[(4 * threadIdx.x) >> 5], nib << ((4 * threadIdx.x) & 31));
         const uint32_t nun = block_sum_u32<256>(unsafe, sh);
         if (threadIdx.x < PEE_TILE / 64) {
@@ -308,7 +363,7 @@ __device__ __forceinline__ bool lm_bit(const u64* lm, int k, int lmw) {
     return (k >> 6) < lmw && ((lm[k >> 6] >> (k & 63)) & 1ull);
 }
 
-template <typename T>
+template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void k_pee_dcount(const T* __restrict__ stego, int H, int W,
                                                     const codec_pee_meta* __restrict__ meta_all,
                                                     const u64* __restrict__ lm_all, int lmw,
@@ -321,14 +376,15 @@ __global__ __launch_bounds__(256) void k_pee_dcount(const T* __restrict__ stego,
     const T* src = stego + (size_t)b * H * W;
     const u64* lm = lm_all + (size_t)b * lmw;
     for (int t = blockIdx.x; t <= tile_end; t += gridDim.x) {
+        const int k0 = t * PEE_TILE + 4 * threadIdx.x;
+        Quad<T, VEC> q;
+        q.load(src, W, wc, k0, end);
         uint32_t local = 0;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int k = t * PEE_TILE + 4 * threadIdx.x + u;
+            const int k = k0 + u;
             if (k <= end && !lm_bit(lm, k, lmw)) {
-                int x, a, bb, cc;
-                pee_load(src, W, wc, k, &x, &a, &bb, &cc);
-                const int e2 = x - med3(a, bb, cc);
+                const int e2 = q.x[u] - med3(q.a[u], q.b[u], q.c[u]);
                 local += (e2 >= -2 * Tthr && e2 < 2 * Tthr) ? 1u : 0u;
             }
         }
@@ -356,7 +412,7 @@ __global__ __launch_bounds__(256) void k_pee_offsets(const codec_pee_meta* __res
     }
 }
 
-template <typename T>
+template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void k_pee_recover(const T* __restrict__ stego, T* __restrict__ cover, int H, int W,
                                                      const codec_pee_meta* __restrict__ meta_all,
                                                      const u64* __restrict__ lm_all, int lmw,
@@ -374,41 +430,54 @@ __global__ __launch_bounds__(256) void k_pee_recover(const T* __restrict__ stego
     u64* payload = payload_all + (size_t)b * pw;
     const uint32_t* off = tile_off_all + (size_t)b * ntiles_max;
     for (int t = blockIdx.x; t <= tile_end; t += gridDim.x) {
-        int xs[4], ps[4];
+        const int k0 = t * PEE_TILE + 4 * threadIdx.x;
+        Quad<T, VEC> q;
+        q.load(src, W, wc, k0, end);
+        int ps[4];
         bool act[4], inner[4];
         uint32_t local = 0;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int k = t * PEE_TILE + 4 * threadIdx.x + u;
+            const int k = k0 + u;
             act[u] = k <= end && !lm_bit(lm, k, lmw);
             inner[u] = false;
+            ps[u] = 0;
             if (act[u]) {
-                int a, bb, cc;
-                pee_load(src, W, wc, k, &xs[u], &a, &bb, &cc);
-                ps[u] = med3(a, bb, cc);
-                const int e2 = xs[u] - ps[u];
+                ps[u] = med3(q.a[u], q.b[u], q.c[u]);
+                const int e2 = q.x[u] - ps[u];
                 inner[u] = e2 >= -2 * Tthr && e2 < 2 * Tthr;
                 local += inner[u] ? 1u : 0u;
             }
         }
         uint32_t tot;
         uint32_t cur = off[t] + block_excl_scan<256>(local, sh, &tot);
+        u64 word = 0;
+        int wi = -1;
+        bool any = false;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (!act[u]) continue;
-            const int k = t * PEE_TILE + 4 * threadIdx.x + u;
-            const int e2 = xs[u] - ps[u];
+            const int e2 = q.x[u] - ps[u];
             int x;
             if (inner[u]) {
-                if (e2 & 1) atomicOr(&payload[cur >> 6], 1ull << (cur & 63));
+                if (e2 & 1) {      // bits of one thread are consecutive: one atomic per word
+                    if (wi != (int)(cur >> 6)) {
+                        if (wi >= 0 && word) atomicOr(&payload[wi], word);
+                        wi = (int)(cur >> 6);
+                        word = 0;
+                    }
+                    word |= 1ull << (cur & 63);
+                }
                 ++cur;
                 x = ps[u] + (e2 >> 1);
             } else {
-                x = e2 >= 2 * Tthr ? xs[u] - Tthr : xs[u] + Tthr;
+                x = e2 >= 2 * Tthr ? q.x[u] - Tthr : q.x[u] + Tthr;
             }
-            const int i = k / wc, j = k - (k / wc) * wc;
-            dst[(size_t)(2 * i + 1) * W + 2 * j + 1] = (T)x;
+            q.put(dst, W, wc, k0 + u, u, x);
+            any = true;
         }
+        if (wi >= 0 && word) atomicOr(&payload[wi], word);
+        if (any) q.store(dst);
     }
 }
 
@@ -464,8 +533,8 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
     uint32_t* off = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.off);
     HIP_TRY(hipMemsetAsync(lm, 0, (size_t)P->B * P->lm_words * 8, st));
     const long long npx = (long long)P->H * P->W;
-    const bool vec = (P->W % 8) == 0 && ((uintptr_t)cover % 16) == 0 && ((uintptr_t)stego % 16) == 0 &&
-                     ((npx * P->bytes) % 16) == 0;
+    const size_t va = P->bytes == 2 ? 16 : 8;
+    const bool vec = (P->W % 8) == 0 && ((uintptr_t)cover % va) == 0 && ((uintptr_t)stego % va) == 0;
     const bool nt = knob("CODEC_NT", 1) != 0;
     {
         ProfScope prof(st, CODEC_K_PEE_SCAN);
@@ -505,14 +574,12 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
         ProfScope prof(st, CODEC_K_PEE_EMBED);
         const int g = (int)knob("CODEC_PEE_EMBED_WGS", 64);
         dim3 grid(g < L.ntiles_max ? g : L.ntiles_max, P->B);
-        if (P->bytes == 2)
-            hipLaunchKernelGGL(k_pee_embed<uint16_t>, grid, dim3(256), 0, st, static_cast<const uint16_t*>(cover),
-                               static_cast<uint16_t*>(stego), P->H, P->W, reinterpret_cast<const u64*>(payload),
-                               P->payload_words, off, L.ntiles_max, meta, reinterpret_cast<u64*>(lm), P->lm_words);
-        else
-            hipLaunchKernelGGL(k_pee_embed<uint8_t>, grid, dim3(256), 0, st, static_cast<const uint8_t*>(cover),
-                               static_cast<uint8_t*>(stego), P->H, P->W, reinterpret_cast<const u64*>(payload),
-                               P->payload_words, off, L.ntiles_max, meta, reinterpret_cast<u64*>(lm), P->lm_words);
+#define PEMB(TT, VV) hipLaunchKernelGGL((k_pee_embed<TT, VV>), grid, dim3(256), 0, st, static_cast<const TT*>(cover), \
+                               static_cast<TT*>(stego), P->H, P->W, reinterpret_cast<const u64*>(payload), \
+                               P->payload_words, off, L.ntiles_max, meta, reinterpret_cast<u64*>(lm), P->lm_words)
+        if (P->bytes == 2) { if (vec) PEMB(uint16_t, true); else PEMB(uint16_t, false); }
+        else { if (vec) PEMB(uint8_t, true); else PEMB(uint8_t, false); }
+#undef PEMB
         LAUNCH_CHECK("k_pee_embed");
     }
     return 0;
@@ -531,6 +598,8 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
     uint32_t* off = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.off);
     const long long nbytes = (long long)P->H * P->W * P->B * P->bytes;
     const bool nt = knob("CODEC_NT", 1) != 0;
+    const size_t va = P->bytes == 2 ? 16 : 8;
+    const bool vec = (P->W % 8) == 0 && ((uintptr_t)stego % va) == 0 && ((uintptr_t)cover_out % va) == 0;
     HIP_TRY(hipMemsetAsync(payload_out, 0, (size_t)P->B * P->payload_words * 8, st));
     {
         ProfScope prof(st, CODEC_K_PEE_COPY);
@@ -552,26 +621,23 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
     dim3 grid(g < L.ntiles_max ? g : L.ntiles_max, P->B);
     {
         ProfScope prof(st, CODEC_K_PEE_DCOUNT);
-        if (P->bytes == 2)
-            hipLaunchKernelGGL(k_pee_dcount<uint16_t>, grid, dim3(256), 0, st, static_cast<const uint16_t*>(stego), P->H, P->W,
-                               meta, reinterpret_cast<const u64*>(lm), P->lm_words, cnt, L.ntiles_max);
-        else
-            hipLaunchKernelGGL(k_pee_dcount<uint8_t>, grid, dim3(256), 0, st, static_cast<const uint8_t*>(stego), P->H, P->W,
-                               meta, reinterpret_cast<const u64*>(lm), P->lm_words, cnt, L.ntiles_max);
+#define PDC(TT, VV) hipLaunchKernelGGL((k_pee_dcount<TT, VV>), grid, dim3(256), 0, st, static_cast<const TT*>(stego), P->H, P->W, \
+                               meta, reinterpret_cast<const u64*>(lm), P->lm_words, cnt, L.ntiles_max)
+        if (P->bytes == 2) { if (vec) PDC(uint16_t, true); else PDC(uint16_t, false); }
+        else { if (vec) PDC(uint8_t, true); else PDC(uint8_t, false); }
+#undef PDC
         LAUNCH_CHECK("k_pee_dcount");
         hipLaunchKernelGGL(k_pee_offsets, dim3(P->B), dim3(256), 0, st, meta, cnt, off, L.ntiles_max);
         LAUNCH_CHECK("k_pee_offsets");
     }
     {
         ProfScope prof(st, CODEC_K_PEE_RECOVER);
-        if (P->bytes == 2)
-            hipLaunchKernelGGL(k_pee_recover<uint16_t>, grid, dim3(256), 0, st, static_cast<const uint16_t*>(stego),
-                               static_cast<uint16_t*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm),
-                               P->lm_words, off, L.ntiles_max, reinterpret_cast<u64*>(payload_out), P->payload_words);
-        else
-            hipLaunchKernelGGL(k_pee_recover<uint8_t>, grid, dim3(256), 0, st, static_cast<const uint8_t*>(stego),
-                               static_cast<uint8_t*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm),
-                               P->lm_words, off, L.ntiles_max, reinterpret_cast<u64*>(payload_out), P->payload_words);
+#define PREC(TT, VV) hipLaunchKernelGGL((k_pee_recover<TT, VV>), grid, dim3(256), 0, st, static_cast<const TT*>(stego), \
+                               static_cast<TT*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm), \
+                               P->lm_words, off, L.ntiles_max, reinterpret_cast<u64*>(payload_out), P->payload_words)
+        if (P->bytes == 2) { if (vec) PREC(uint16_t, true); else PREC(uint16_t, false); }
+        else { if (vec) PREC(uint8_t, true); else PREC(uint8_t, false); }
+#undef PREC
         LAUNCH_CHECK("k_pee_recover");
     }
     return 0;
