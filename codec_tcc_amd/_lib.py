@@ -44,7 +44,7 @@ class SliceMeta(C.Structure):
         ("status", C.c_int32), ("nonzero_bins", C.c_int32),
         ("perm", I16), ("sizes", I16), ("n", I16), ("src", I16), ("off", I16), ("cat", I16),
         ("entropy", C.c_double), ("target", C.c_double), ("cum_info", C.c_double),
-        ("reserved_d", C.c_double), ("mi", D16),
+        ("span_lo", C.c_int32), ("span_len", C.c_int32), ("mi", D16),
     ]
 
 

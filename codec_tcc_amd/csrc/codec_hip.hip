@@ -726,7 +726,14 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     M->entropy = Hy;
     M->target = target;
     M->cum_info = cum;
-    M->reserved_d = 0.0;
+    {   // circular hull of the windows (lets a streaming pass skip untouched chunks cheaply)
+        int maxn = 0;
+        for (int p = 0; p < s; ++p) maxn = max(maxn, M->n[p]);
+        const bool shared_start = (P.mode == CODEC_MODE_MULTI) || P.align;
+        const long long len = shared_start ? maxn : cat;
+        M->span_lo = (P.mode == CODEC_MODE_HYBRID) ? offset : 0;
+        M->span_len = (int)min(len, npx);
+    }
     for (int i = 0; i < 16; ++i) M->mi[i] = mis_sh[i];
 }
 
@@ -899,6 +906,67 @@ __global__ __launch_bounds__(256) void k_restore(const T* __restrict__ stego, T*
                 if (q >= r.q0 && q < r.q1) px ^= map_bit(maps, r.j0 + (q - r.q0)) << r.p;
             }
             cover[(size_t)b * npx + q] = (T)px;
+        }
+    }
+}
+
+// Grid-stride variant: the whole batch is swept as one address-ordered stream (the
+// fastest pattern measured, tools/ubench_stream.hip); a chunk is tested against its slice's
+// window hull (span_lo/span_len, 2 loads from the L2-resident meta) and only the rare
+// chunks inside it walk the per-plane windows.
+template <typename T, bool NT>
+__global__ __launch_bounds__(256) void k_restore_gs(const T* __restrict__ stego, T* __restrict__ cover,
+                                                    uint32_t npx, uint32_t nchunks, uint32_t total_chunks,
+                                                    const codec_slice_meta* __restrict__ meta,
+                                                    const u64* __restrict__ maps_all, int mw) {
+    typedef typename Vec8<T>::type V;
+    const V* src = reinterpret_cast<const V*>(stego);
+    V* dst = reinterpret_cast<V*>(cover);
+    const uint32_t stride = gridDim.x * 256u * 4u;
+    for (uint32_t cb = blockIdx.x * 1024u + threadIdx.x; cb < total_chunks; cb += stride) {
+        V vv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (cb + u * 256u < total_chunks) vv[u] = ldv<NT>(src + cb + u * 256u);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t g = cb + u * 256u;
+            if (g >= total_chunks) break;
+            const uint32_t b = g / nchunks;
+            const long long q0 = (long long)(g - b * nchunks) * 8;
+            const codec_slice_meta* M = meta + b;
+            const long long lo = M->span_lo, hi = lo + M->span_len;
+            const bool hit = (q0 + 8 > lo && q0 < hi) || (hi > (long long)npx && q0 < hi - (long long)npx);
+            V v = vv[u];
+            if (hit) {
+                uint32_t px[8];
+                if constexpr (sizeof(T) == 2) {
+                    px[0] = v.x & 0xFFFFu; px[1] = v.x >> 16; px[2] = v.y & 0xFFFFu; px[3] = v.y >> 16;
+                    px[4] = v.z & 0xFFFFu; px[5] = v.z >> 16; px[6] = v.w & 0xFFFFu; px[7] = v.w >> 16;
+                } else {
+                    for (int e = 0; e < 4; ++e) { px[e] = (v.x >> (8 * e)) & 0xFFu; px[4 + e] = (v.y >> (8 * e)) & 0xFFu; }
+                }
+                const u64* maps = maps_all + (size_t)b * mw;
+                const int s = M->s;
+                for (int p = 0; p < s; ++p) {
+                    const int n = M->n[p];
+                    if (n <= 0) continue;
+                    const long long off = M->off[p], cat = M->cat[p];
+                    for (int e = 0; e < 8; ++e) {
+                        long long i = q0 + e - off;
+                        if (i < 0) i += npx;
+                        if (i < n) px[e] ^= map_bit(maps, cat + i) << p;
+                    }
+                }
+                if constexpr (sizeof(T) == 2) {
+                    v.x = px[0] | (px[1] << 16); v.y = px[2] | (px[3] << 16);
+                    v.z = px[4] | (px[5] << 16); v.w = px[6] | (px[7] << 16);
+                } else {
+                    v.x = px[0] | (px[1] << 8) | (px[2] << 16) | (px[3] << 24);
+                    v.y = px[4] | (px[5] << 8) | (px[6] << 16) | (px[7] << 24);
+                }
+            }
+            stv<NT>(dst + g, v);
         }
     }
 }
@@ -1384,6 +1452,23 @@ int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps
             LAUNCH_CHECK("k_restore_scalar");
         } else {
         const long long nchunks = npx / 8;
+        const bool gs = knob("CODEC_RESTORE_GS", 1) != 0 && (npx % 8) == 0 && nchunks * P->B < 0xFFFFFFFFLL;
+        if (gs) {
+            const bool ntg = knob("CODEC_NT", 1) != 0;
+            const long long g = knob("CODEC_RESTORE_GS_WGS", 16384);
+            const uint32_t total = (uint32_t)(nchunks * P->B);
+            long long grid = (total + 1023) / 1024;
+            if (grid > g) grid = g;
+            if (grid < 1) grid = 1;
+            ProfScope prof(st, CODEC_K_RESTORE);
+            const u64* mp = reinterpret_cast<const u64*>(maps);
+#define RGS(TT, NTV) hipLaunchKernelGGL((k_restore_gs<TT, NTV>), dim3((unsigned)grid), dim3(256), 0, st, \
+                static_cast<const TT*>(stego), static_cast<TT*>(cover_out), (uint32_t)npx, (uint32_t)nchunks, total, meta, mp, P->map_words)
+            if (P->in_bytes == 2) { if (ntg) RGS(uint16_t, true); else RGS(uint16_t, false); }
+            else { if (ntg) RGS(uint8_t, true); else RGS(uint8_t, false); }
+#undef RGS
+            LAUNCH_CHECK("k_restore_gs");
+        } else {
         // many small address-ordered workgroups stream best (tools/ubench_stream.hip)
         const long long target = knob("CODEC_RESTORE_WGS", 32768);   // tools/tune.py
         const bool nt = knob("CODEC_NT", 1) != 0;
@@ -1405,6 +1490,7 @@ int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps
             uint8_t* cp = static_cast<uint8_t*>(cover_out);
             if (nt) hipLaunchKernelGGL((k_restore<uint8_t, true>), grid, dim3(256), 0, st, sp, cp, npx, meta, mp, P->map_words, per);
             else hipLaunchKernelGGL((k_restore<uint8_t, false>), grid, dim3(256), 0, st, sp, cp, npx, meta, mp, P->map_words, per);
+        }
         }
         LAUNCH_CHECK("k_restore");
         }

@@ -85,7 +85,8 @@ typedef struct codec_slice_meta {
     double entropy;       /* calculate_entropy(cover), bit-exact (codec.py:489-502)  */
     double target;        /* beta * entropy                                          */
     double cum_info;      /* cumulative MI at the decision                           */
-    double reserved_d;
+    int32_t span_lo;      /* every window lies in the circular pixel interval          */
+    int32_t span_len;     /*   [span_lo, span_lo + span_len) mod H*W                   */
     double mi[CODEC_MAX_PLANES]; /* calculate_mutual_information per plane, evaluated ones */
 } codec_slice_meta;
 
