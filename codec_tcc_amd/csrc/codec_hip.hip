@@ -914,6 +914,45 @@ __global__ __launch_bounds__(256) void k_restore(const T* __restrict__ stego, T*
 // fastest pattern measured, tools/ubench_stream.hip); a chunk is tested against its slice's
 // window hull (span_lo/span_len, 2 loads from the L2-resident meta) and only the rare
 // chunks inside it walk the per-plane windows.
+template <typename T>
+__device__ __forceinline__ void restore_chunk(typename Vec8<T>::type& v, long long q0, const codec_slice_meta* M,
+                                              const u64* maps, long long npx) {
+    uint32_t px[8];
+    if constexpr (sizeof(T) == 2) {
+        px[0] = v.x & 0xFFFFu; px[1] = v.x >> 16; px[2] = v.y & 0xFFFFu; px[3] = v.y >> 16;
+        px[4] = v.z & 0xFFFFu; px[5] = v.z >> 16; px[6] = v.w & 0xFFFFu; px[7] = v.w >> 16;
+    } else {
+        for (int e = 0; e < 4; ++e) { px[e] = (v.x >> (8 * e)) & 0xFFu; px[4 + e] = (v.y >> (8 * e)) & 0xFFu; }
+    }
+    const int s = M->s;
+    for (int p = 0; p < s; ++p) {
+        const int n = M->n[p];
+        if (n <= 0) continue;
+        const long long off = M->off[p], cat = M->cat[p];
+        for (int e = 0; e < 8; ++e) {
+            long long i = q0 + e - off;
+            if (i < 0) i += npx;
+            if (i < n) px[e] ^= map_bit(maps, cat + i) << p;
+        }
+    }
+    if constexpr (sizeof(T) == 2) {
+        v.x = px[0] | (px[1] << 16); v.y = px[2] | (px[3] << 16);
+        v.z = px[4] | (px[5] << 16); v.w = px[6] | (px[7] << 16);
+    } else {
+        v.x = px[0] | (px[1] << 8) | (px[2] << 16) | (px[3] << 24);
+        v.y = px[4] | (px[5] << 8) | (px[6] << 16) | (px[7] << 24);
+    }
+}
+
+__device__ __forceinline__ bool span_hit(long long q0, long long lo, long long len, long long npx) {
+    const long long hi = lo + len;
+    return (q0 + 8 > lo && q0 < hi) || (hi > npx && q0 < hi - npx);
+}
+
+// Grid-stride variant: the whole batch is swept as one address-ordered stream.  Each
+// iteration of a workgroup covers 1024 consecutive chunks; their slice (and its window
+// hull span_lo/span_len) is looked up once per iteration, wave-uniformly, and only chunks
+// inside the hull walk the per-plane windows.
 template <typename T, bool NT>
 __global__ __launch_bounds__(256) void k_restore_gs(const T* __restrict__ stego, T* __restrict__ cover,
                                                     uint32_t npx, uint32_t nchunks, uint32_t total_chunks,
@@ -922,51 +961,41 @@ __global__ __launch_bounds__(256) void k_restore_gs(const T* __restrict__ stego,
     typedef typename Vec8<T>::type V;
     const V* src = reinterpret_cast<const V*>(stego);
     V* dst = reinterpret_cast<V*>(cover);
-    const uint32_t stride = gridDim.x * 256u * 4u;
-    for (uint32_t cb = blockIdx.x * 1024u + threadIdx.x; cb < total_chunks; cb += stride) {
+    const uint32_t stride = gridDim.x * 1024u;
+    for (uint32_t base = blockIdx.x * 1024u; base < total_chunks; base += stride) {
+        const uint32_t cb = base + threadIdx.x;
         V vv[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             if (cb + u * 256u < total_chunks) vv[u] = ldv<NT>(src + cb + u * 256u);
+        const uint32_t last = min(base + 1023u, total_chunks - 1);
+        const uint32_t b0 = __builtin_amdgcn_readfirstlane(base / nchunks);
+        const uint32_t b1 = __builtin_amdgcn_readfirstlane(last / nchunks);
+        if (b0 == b1) {
+            const codec_slice_meta* M = meta + b0;
+            const long long lo = M->span_lo, len = M->span_len;
+            const long long qbase = (long long)(base - b0 * nchunks) * 8;
+            const u64* maps = maps_all + (size_t)b0 * mw;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t g = cb + u * 256u;
-            if (g >= total_chunks) break;
-            const uint32_t b = g / nchunks;
-            const long long q0 = (long long)(g - b * nchunks) * 8;
-            const codec_slice_meta* M = meta + b;
-            const long long lo = M->span_lo, hi = lo + M->span_len;
-            const bool hit = (q0 + 8 > lo && q0 < hi) || (hi > (long long)npx && q0 < hi - (long long)npx);
-            V v = vv[u];
-            if (hit) {
-                uint32_t px[8];
-                if constexpr (sizeof(T) == 2) {
-                    px[0] = v.x & 0xFFFFu; px[1] = v.x >> 16; px[2] = v.y & 0xFFFFu; px[3] = v.y >> 16;
-                    px[4] = v.z & 0xFFFFu; px[5] = v.z >> 16; px[6] = v.w & 0xFFFFu; px[7] = v.w >> 16;
-                } else {
-                    for (int e = 0; e < 4; ++e) { px[e] = (v.x >> (8 * e)) & 0xFFu; px[4 + e] = (v.y >> (8 * e)) & 0xFFu; }
-                }
-                const u64* maps = maps_all + (size_t)b * mw;
-                const int s = M->s;
-                for (int p = 0; p < s; ++p) {
-                    const int n = M->n[p];
-                    if (n <= 0) continue;
-                    const long long off = M->off[p], cat = M->cat[p];
-                    for (int e = 0; e < 8; ++e) {
-                        long long i = q0 + e - off;
-                        if (i < 0) i += npx;
-                        if (i < n) px[e] ^= map_bit(maps, cat + i) << p;
-                    }
-                }
-                if constexpr (sizeof(T) == 2) {
-                    v.x = px[0] | (px[1] << 16); v.y = px[2] | (px[3] << 16);
-                    v.z = px[4] | (px[5] << 16); v.w = px[6] | (px[7] << 16);
-                } else {
-                    v.x = px[0] | (px[1] << 8) | (px[2] << 16) | (px[3] << 24);
-                    v.y = px[4] | (px[5] << 8) | (px[6] << 16) | (px[7] << 24);
-                }
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t g = cb + u * 256u;
+                if (g >= total_chunks) break;
+                const long long q0 = qbase + (long long)(threadIdx.x + u * 256u) * 8;
+                if (span_hit(q0, lo, len, npx)) restore_chunk<T>(vv[u], q0, M, maps, npx);
+                stv<NT>(dst + g, vv[u]);
             }
-            stv<NT>(dst + g, v);
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t g = cb + u * 256u;
+                if (g >= total_chunks) break;
+                const uint32_t b = g / nchunks;
+                const codec_slice_meta* M = meta + b;
+                const long long q0 = (long long)(g - b * nchunks) * 8;
+                if (span_hit(q0, M->span_lo, M->span_len, npx))
+                    restore_chunk<T>(vv[u], q0, M, maps_all + (size_t)b * mw, npx);
+                stv<NT>(dst + g, vv[u]);
+            }
         }
     }
 }
