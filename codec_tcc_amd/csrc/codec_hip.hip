@@ -310,7 +310,7 @@ __device__ __forceinline__ void hist_add8(uint32_t* lds, uint32_t* ghist, const 
 // Work item = (band of SB rows, 8-pixel column chunk); a wave covers 64 consecutive
 // chunks of one band, so every load instruction reads 1 KiB (u16) contiguously; the
 // SB/8 lanes of one block column combine their LSB counts with shuffles.
-template <typename T, int SB, bool NT>
+template <typename T, int SB, bool NT, bool HIST = true>
 __global__ __launch_bounds__(1024) void k_scan_fast(const T* __restrict__ cover, T* __restrict__ stego,
                                                     int H, int W, int bands_per_wg,
                                                     uint32_t* __restrict__ ghist_all,
@@ -369,17 +369,19 @@ __global__ __launch_bounds__(1024) void k_scan_fast(const T* __restrict__ cover,
                 }
                 ones += lsb_count(v0) + lsb_count(v1) + lsb_count(v2) + lsb_count(v3);
                 vor |= vor_of(v0) | vor_of(v1) | vor_of(v2) | vor_of(v3);
-                hist_add8<T>(lds, ghist, v0);
-                hist_add8<T>(lds, ghist, v1);
-                hist_add8<T>(lds, ghist, v2);
-                hist_add8<T>(lds, ghist, v3);
+                if constexpr (HIST) {
+                    hist_add8<T>(lds, ghist, v0);
+                    hist_add8<T>(lds, ghist, v1);
+                    hist_add8<T>(lds, ghist, v2);
+                    hist_add8<T>(lds, ghist, v3);
+                }
             }
             for (; r < rows; ++r) {
                 V v0 = ldv<NT>(s + (size_t)r * stride);
                 if (d) stv<NT>(d + (size_t)r * stride, v0);
                 ones += lsb_count(v0);
                 vor |= vor_of(v0);
-                hist_add8<T>(lds, ghist, v0);
+                if constexpr (HIST) hist_add8<T>(lds, ghist, v0);
             }
         }
 #pragma unroll
@@ -1343,7 +1345,8 @@ static int launch_scan_fast(const codec_params* P, const void* cover, void* steg
     switch (sb) {
         case 8: if (nt) hipLaunchKernelGGL((k_scan_fast<T, 8, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv);
                 else hipLaunchKernelGGL((k_scan_fast<T, 8, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
-        case 16: if (nt) hipLaunchKernelGGL((k_scan_fast<T, 16, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv);
+        case 16: if (knob("CODEC_DIAG_NOHIST", 0)) hipLaunchKernelGGL((k_scan_fast<T, 16, true, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv);   // timing diagnostics only: s is wrong
+                else if (nt) hipLaunchKernelGGL((k_scan_fast<T, 16, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv);
                 else hipLaunchKernelGGL((k_scan_fast<T, 16, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
         case 32: if (nt) hipLaunchKernelGGL((k_scan_fast<T, 32, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv);
                 else hipLaunchKernelGGL((k_scan_fast<T, 32, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
@@ -1484,7 +1487,7 @@ int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps
         const bool gs = knob("CODEC_RESTORE_GS", 1) != 0 && (npx % 8) == 0 && nchunks * P->B < 0xFFFFFFFFLL;
         if (gs) {
             const bool ntg = knob("CODEC_NT", 1) != 0;
-            const long long g = knob("CODEC_RESTORE_GS_WGS", 16384);
+            const long long g = knob("CODEC_RESTORE_GS_WGS", 1 << 30);   // default: one 1024-chunk block per WG
             const uint32_t total = (uint32_t)(nchunks * P->B);
             long long grid = (total + 1023) / 1024;
             if (grid > g) grid = g;
