@@ -481,6 +481,107 @@ __global__ __launch_bounds__(256) void k_pee_recover(const T* __restrict__ stego
     }
 }
 
+// Fused extract sweep (W % 8 == 0 and 256 | items per slice): stego -> cover for the whole
+// batch in address order; a workgroup iteration covers 4 whole tiles (u-slot u = tile
+// base/256 + u), and slots whose tile lies in the slice's prefix (<= tile_end) recover
+// bits and pixels in registers with a block scan for the cursor.
+template <typename T, bool NT>
+__global__ __launch_bounds__(256) void k_pee_restore_gs(const T* __restrict__ stego, T* __restrict__ cover, int H, int W,
+                                                        uint32_t items_per_slice, uint32_t total_items,
+                                                        const codec_pee_meta* __restrict__ meta_all,
+                                                        const u64* __restrict__ lm_all, int lmw,
+                                                        const uint32_t* __restrict__ tile_off_all, int ntiles_max,
+                                                        u64* __restrict__ payload_all, int pw) {
+    typedef typename Vec8<T>::type V;
+    __shared__ uint32_t sh[8];
+    const int CR = W / 8;
+    const uint32_t tiles_per_slice = items_per_slice / 256u;
+    const size_t npx = (size_t)H * W;
+    const uint32_t stride = gridDim.x * 1024u;
+    for (uint32_t base = blockIdx.x * 1024u; base < total_items; base += stride) {
+        V a0[4], a1[4];
+        size_t o0[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t g = base + u * 256u + threadIdx.x;
+            if (g < total_items) {
+                const uint32_t b = g / items_per_slice, it = g - b * items_per_slice;
+                const uint32_t r = it / CR, c = it - r * CR;
+                o0[u] = b * npx + (size_t)(2 * r) * W + (size_t)c * 8;
+                a0[u] = ldv<NT>(reinterpret_cast<const V*>(stego + o0[u]));
+                a1[u] = ldv<NT>(reinterpret_cast<const V*>(stego + o0[u] + W));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t gt = base / 256u + u;                        // global tile (uniform)
+            if (gt * 256u >= total_items) break;
+            const uint32_t b = gt / tiles_per_slice, t = gt - b * tiles_per_slice;
+            const codec_pee_meta* M = meta_all + b;
+            if ((int)t <= M->tile_end) {                                 // uniform per slot
+                const int end = M->end, Tthr = M->T;
+                const u64* lm = lm_all + (size_t)b * lmw;
+                const int k0 = (int)t * PEE_TILE + 4 * threadIdx.x;
+                int ps[4], xs[4];
+                bool act[4], inner[4];
+                uint32_t local = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int k = k0 + q;
+                    xs[q] = (int)get_px(a1[u], 2 * q + 1);
+                    act[q] = k <= end && !lm_bit(lm, k, lmw);
+                    inner[q] = false;
+                    ps[q] = 0;
+                    if (act[q]) {
+                        ps[q] = med3((int)get_px(a1[u], 2 * q), (int)get_px(a0[u], 2 * q + 1), (int)get_px(a0[u], 2 * q));
+                        const int e2 = xs[q] - ps[q];
+                        inner[q] = e2 >= -2 * Tthr && e2 < 2 * Tthr;
+                        local += inner[q] ? 1u : 0u;
+                    }
+                }
+                uint32_t tot;
+                uint32_t cur = tile_off_all[(size_t)b * ntiles_max + t] + block_excl_scan<256>(local, sh, &tot);
+                u64* payload = payload_all + (size_t)b * pw;
+                u64 word = 0;
+                int wi = -1;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (!act[q]) continue;
+                    const int e2 = xs[q] - ps[q];
+                    int x;
+                    if (inner[q]) {
+                        if (e2 & 1) {
+                            if (wi != (int)(cur >> 6)) {
+                                if (wi >= 0 && word) atomicOr(&payload[wi], word);
+                                wi = (int)(cur >> 6);
+                                word = 0;
+                            }
+                            word |= 1ull << (cur & 63);
+                        }
+                        ++cur;
+                        x = ps[q] + (e2 >> 1);
+                    } else {
+                        x = e2 >= 2 * Tthr ? xs[q] - Tthr : xs[q] + Tthr;
+                    }
+                    set_px(a1[u], 2 * q + 1, (uint32_t)x);
+                }
+                if (wi >= 0 && word) atomicOr(&payload[wi], word);
+            }
+            const uint32_t g = base + u * 256u + threadIdx.x;
+            if (g < total_items) {
+                stv<NT>(reinterpret_cast<V*>(cover + o0[u]), a0[u]);
+                stv<NT>(reinterpret_cast<V*>(cover + o0[u] + W), a1[u]);
+            }
+        }
+    }
+    // odd H: the unpaired last row of every slice is copied verbatim
+    if ((H & 1) && blockIdx.x == 0) {
+        const uint32_t B = total_items / items_per_slice;
+        for (uint32_t b = 0; b < B; ++b)
+            for (int q = threadIdx.x; q < W; q += 256) cover[b * npx + (size_t)(H - 1) * W + q] = stego[b * npx + (size_t)(H - 1) * W + q];
+    }
+}
+
 // ====================================================================== host side
 struct PeeWs {
     size_t cnt, off, total;
@@ -601,6 +702,36 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
     const size_t va = P->bytes == 2 ? 16 : 8;
     const bool vec = (P->W % 8) == 0 && ((uintptr_t)stego % va) == 0 && ((uintptr_t)cover_out % va) == 0;
     HIP_TRY(hipMemsetAsync(payload_out, 0, (size_t)P->B * P->payload_words * 8, st));
+    const long long items = (long long)(P->H / 2) * (P->W / 8);
+    const bool fused = vec && knob("CODEC_PEE_FUSED", 1) != 0 && (P->W % 8) == 0 && items > 0 && (items % 256) == 0 &&
+                       items * P->B < 0xFFFFFFFFLL;
+    if (fused) {
+        const int g = (int)knob("CODEC_PEE_EMBED_WGS", 64);
+        dim3 grid(g < L.ntiles_max ? g : L.ntiles_max, P->B);
+        {
+            ProfScope prof(st, CODEC_K_PEE_DCOUNT);
+#define PDC2(TT) hipLaunchKernelGGL((k_pee_dcount<TT, true>), grid, dim3(256), 0, st, static_cast<const TT*>(stego), P->H, P->W, \
+                               meta, reinterpret_cast<const u64*>(lm), P->lm_words, cnt, L.ntiles_max)
+            if (P->bytes == 2) PDC2(uint16_t); else PDC2(uint8_t);
+#undef PDC2
+            LAUNCH_CHECK("k_pee_dcount");
+            hipLaunchKernelGGL(k_pee_offsets, dim3(P->B), dim3(256), 0, st, meta, cnt, off, L.ntiles_max);
+            LAUNCH_CHECK("k_pee_offsets");
+        }
+        ProfScope prof(st, CODEC_K_PEE_RECOVER);
+        const uint32_t total = (uint32_t)(items * P->B);
+        long long gg = (total + 1023) / 1024;
+        const long long cap = knob("CODEC_PEE_RESTORE_WGS", 1 << 30);
+        if (gg > cap) gg = cap;
+#define PRG(TT, NTV) hipLaunchKernelGGL((k_pee_restore_gs<TT, NTV>), dim3((unsigned)gg), dim3(256), 0, st, static_cast<const TT*>(stego), \
+                static_cast<TT*>(cover_out), P->H, P->W, (uint32_t)items, total, meta, reinterpret_cast<const u64*>(lm), P->lm_words, \
+                off, L.ntiles_max, reinterpret_cast<u64*>(payload_out), P->payload_words)
+        if (P->bytes == 2) { if (nt) PRG(uint16_t, true); else PRG(uint16_t, false); }
+        else { if (nt) PRG(uint8_t, true); else PRG(uint8_t, false); }
+#undef PRG
+        LAUNCH_CHECK("k_pee_restore_gs");
+        return 0;
+    }
     {
         ProfScope prof(st, CODEC_K_PEE_COPY);
         if (((uintptr_t)stego % 16) == 0 && ((uintptr_t)cover_out % 16) == 0) {
