@@ -69,7 +69,7 @@ def test_global_random_state_untouched():
 def test_struct_layout_matches_header():
     """ctypes mirrors of codec_tcc.h: sizes must match the C compiler's view."""
     hdr = os.path.join(REPO, "include", "codec_tcc.h")
-    src = f'#include "{hdr}"\n#include <stdio.h>\n#include <stddef.h>\nint main(){{printf("%zu %zu %zu %zu %zu\\n", sizeof(codec_params), sizeof(codec_layout), sizeof(codec_slice_meta), offsetof(codec_slice_meta, entropy), offsetof(codec_slice_meta, mi));return 0;}}\n'
+    src = f'#include "{hdr}"\n#include <stdio.h>\n#include <stddef.h>\nint main(){{printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(codec_params), sizeof(codec_layout), sizeof(codec_slice_meta), offsetof(codec_slice_meta, entropy), offsetof(codec_slice_meta, mi), sizeof(codec_pee_params), sizeof(codec_pee_meta), offsetof(codec_slice_meta, span_lo), offsetof(codec_pee_meta, lm_count));return 0;}}\n'
     import subprocess
     import tempfile
     with tempfile.TemporaryDirectory() as d:
@@ -84,6 +84,10 @@ def test_struct_layout_matches_header():
     assert sizes[2] == C.sizeof(_lib.SliceMeta)
     assert sizes[3] == _lib.SliceMeta.entropy.offset
     assert sizes[4] == _lib.SliceMeta.mi.offset
+    assert sizes[5] == C.sizeof(_lib.PeeParams)
+    assert sizes[6] == C.sizeof(_lib.PeeMeta) == _lib.PEE_META_BYTES
+    assert sizes[7] == _lib.SliceMeta.span_lo.offset
+    assert sizes[8] == _lib.PeeMeta.lm_count.offset
 
 
 def test_library_exports_every_header_symbol():
