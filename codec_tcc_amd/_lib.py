@@ -57,9 +57,10 @@ class PeeMeta(C.Structure):
     _fields_ = [("T", C.c_int32), ("maxval", C.c_int32), ("L", C.c_int32), ("end", C.c_int32),
                 ("nc", C.c_int32), ("ntiles", C.c_int32), ("tile_end", C.c_int32), ("status", C.c_int32),
                 ("capacity", C.c_int32), ("lm_count", C.c_int32), ("h", C.c_int32), ("w", C.c_int32),
-                ("reserved", C.c_int32 * 4)]
+                ("flags", C.c_int32), ("reserved", C.c_int32 * 3)]
 
 
+PEE_PARTIAL = 1
 META_BYTES = C.sizeof(SliceMeta)
 PEE_META_BYTES = C.sizeof(PeeMeta)
 LAYOUT_BYTES = C.sizeof(Layout)
@@ -87,7 +88,8 @@ _SIGS = {
 }
 KERNEL_TAGS = {1: "k_scan_fast", 2: "k_scan_generic", 3: "k_block_exact", 4: "k_decide",
                5: "k_embed", 6: "k_restore", 7: "k_gather", 8: "other", 9: "k_pee_scan", 10: "k_pee_locate",
-               11: "k_pee_embed", 12: "k_pee_copy", 13: "k_pee_dcount", 14: "k_pee_recover"}
+               11: "k_pee_embed", 12: "k_pee_copy", 13: "k_pee_dcount", 14: "k_pee_recover",
+               15: "k_pee_embed1", 16: "k_pee_extract1"}
 EXPORTS = tuple(_SIGS)
 
 _lib = None

@@ -95,6 +95,34 @@ __device__ uint32_t block_excl_scan(uint32_t x, uint32_t* sh, uint32_t* total) {
     return r;
 }
 
+// 64-bit variant (several packed 16-bit counters scanned at once); sh needs NT/64+1 words
+template <int NT>
+__device__ u64 block_excl_scan64(u64 x, u64* sh, u64* total) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    u64 inc = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const u64 y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) sh[wv] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u64 acc = 0;
+        for (int w = 0; w < NT / 64; ++w) {
+            const u64 tmp = sh[w];
+            sh[w] = acc;
+            acc += tmp;
+        }
+        sh[NT / 64] = acc;
+    }
+    __syncthreads();
+    const u64 r = sh[wv] + inc - x;
+    *total = sh[NT / 64];
+    __syncthreads();
+    return r;
+}
+
 template <int NT>
 __device__ uint32_t block_sum_u32(uint32_t x, uint32_t* sh) {
     uint32_t tot;

@@ -1048,6 +1048,25 @@ __global__ __launch_bounds__(256) void k_gather(const T* __restrict__ stego, lon
     if ((threadIdx.x & 63) == 0) out[(size_t)b * pw + (j >> 6)] = bal;
 }
 
+// in-place restore: XOR every window bit with its location-map bit (only the <= T window
+// pixels are touched; 32-bit atomics because windows of different planes may share a pixel)
+template <typename T>
+__global__ __launch_bounds__(256) void k_unxor(T* img, long long npx, const codec_slice_meta* __restrict__ meta,
+                                               const u64* __restrict__ maps_all, int mw) {
+    __shared__ SliceWin W;
+    const int b = blockIdx.y;
+    load_win(meta + b, &W);
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= W.tot || !map_bit(maps_all + (size_t)b * mw, j)) return;
+    const int p = plane_of(W, j);
+    const int i = j - W.cat[p];
+    long long q = (long long)W.off[p] + i;
+    if (q >= npx) q -= npx;
+    const size_t byte = ((size_t)b * npx + q) * sizeof(T);
+    uint32_t* word = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(img) + (byte & ~(size_t)3));
+    atomicXor(word, 1u << ((byte & 3) * 8 + p));
+}
+
 // ------------------------------------------------------------------ K6: reference decode
 // python `seq[:k]` length for a sequence of length `count`
 __device__ __forceinline__ int pyslice_take(int count, int k) {
@@ -1396,10 +1415,14 @@ int codec_plan(const codec_params* P, const void* cover, void* stego, const doub
     double* terms = reinterpret_cast<double*>(ws + L.terms);
     HIP_TRY(hipMemsetAsync(ws, 0, L.exact, st));   // histograms, block keys, OR words
 
+    if (stego == cover && P->in_bytes != P->out_bytes)
+        return set_err(CODEC_EINVAL, "codec_plan: in place (stego == cover) needs one pixel dtype");
     const bool fast = use_fast_scan(P, cover, stego ? stego : cover);
     if (fast) {
-        rc = P->in_bytes == 2 ? launch_scan_fast<uint16_t>(P, cover, stego, hist, keys, orv, st)
-                              : launch_scan_fast<uint8_t>(P, cover, stego, hist, keys, orv, st);
+        // in place the stego copy is the cover itself: the scan only reads
+        void* sdst = stego == cover ? nullptr : stego;
+        rc = P->in_bytes == 2 ? launch_scan_fast<uint16_t>(P, cover, sdst, hist, keys, orv, st)
+                              : launch_scan_fast<uint8_t>(P, cover, sdst, hist, keys, orv, st);
     } else if (P->in_bytes == 2) {
         rc = P->out_bytes == 2 ? launch_scan_generic<uint16_t, uint16_t>(P, cover, stego, hist, orv, st)
                                : launch_scan_generic<uint16_t, uint8_t>(P, cover, stego, hist, orv, st);
@@ -1469,7 +1492,8 @@ int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps
     if (P->in_bytes != P->out_bytes) return set_err(CODEC_EINVAL, "codec_extract: stego and cover share a dtype");
     const long long npx = (long long)P->H * P->W;
     hipStream_t st = as_stream(stream);
-    if (cover_out) {
+    const bool inplace = cover_out == stego;   // restore only the window pixels, after the gather
+    if (cover_out && !inplace) {
         const size_t va = P->in_bytes == 2 ? 16 : 8;
         if ((uintptr_t)stego % va || (uintptr_t)cover_out % va || ((npx * P->in_bytes) % va)) {
             long long gx = (npx + 255) / 256;
@@ -1540,6 +1564,17 @@ int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps
             hipLaunchKernelGGL(k_gather<uint8_t>, grid, dim3(256), 0, st, static_cast<const uint8_t*>(stego), npx,
                                meta, reinterpret_cast<u64*>(payload_out), P->payload_words);
         LAUNCH_CHECK("k_gather");
+    }
+    if (inplace) {
+        dim3 grid((unsigned)(((long long)P->map_words * 64 + 255) / 256), P->B);
+        ProfScope prof(st, CODEC_K_RESTORE);
+        if (P->in_bytes == 2)
+            hipLaunchKernelGGL(k_unxor<uint16_t>, grid, dim3(256), 0, st, static_cast<uint16_t*>(cover_out), npx, meta,
+                               reinterpret_cast<const u64*>(maps), P->map_words);
+        else
+            hipLaunchKernelGGL(k_unxor<uint8_t>, grid, dim3(256), 0, st, static_cast<uint8_t*>(cover_out), npx, meta,
+                               reinterpret_cast<const u64*>(maps), P->map_words);
+        LAUNCH_CHECK("k_unxor");
     }
     return 0;
 }

@@ -263,12 +263,13 @@ __global__ __launch_bounds__(256) void k_pee_locate(const T* __restrict__ img, i
         M->w = W;
         if (L == 0) {
             M->end = -1; M->tile_end = -1; M->status = 0;
-        } else if (running < L) {
-            M->end = -1; M->tile_end = -1; M->status = 1;      // payload exceeds capacity
+        } else if (running < L) {   // payload exceeds capacity: embed `running` bits, process all
+            M->end = nc - 1; M->tile_end = ntiles - 1; M->status = 1;
         } else {
             M->end = s_end; M->tile_end = tile; M->status = 0;
         }
         M->lm_count = 0;
+        M->flags = 0;
     }
 }
 
@@ -582,10 +583,432 @@ __global__ __launch_bounds__(256) void k_pee_restore_gs(const T* __restrict__ st
     }
 }
 
+
+// ====================================================================== single pass
+// Decoupled look-back (W % 8 == 0): a chunk = 4 tiles = 1024 items = 4096 candidates,
+// handed out by an atomic ticket so that a chunk only ever waits on chunks that were
+// handed out earlier (forward progress).  Each chunk publishes its count of expandable
+// candidates (aggregate), looks back over its slice's predecessors (one wave reads 64
+// status words per round) for its exclusive bit cursor, publishes the inclusive prefix
+// and then embeds / recovers in registers: the cover is read once and the stego written
+// once, and an in-place call touches only the chunks up to `end`.
+#define PEE_CHUNK 1024                     // items per chunk
+#define LB_AGG (1ull << 62)
+#define LB_INC (2ull << 62)
+
+__device__ __forceinline__ void lb_store(u64* p, u64 v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u64 lb_load(u64* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_agent(uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// wave 0 of the block: exclusive prefix of chunk c (>= 1) from st[0..c-1].  The spin is
+// bounded: a predecessor that never publishes (it would take out-of-order workgroup
+// dispatch) sets *timeout instead of hanging the GPU, and the caller flags the slice.
+// `done` (optional): the slice's finished flag.  It can only be set once every chunk before
+// the one holding `end` has published, so a waiter that sees it set lies past `end` and
+// returns `sat` (>= L) instead of waiting for predecessors that may never publish.
+__device__ uint32_t lb_exclusive(u64* st, int c, bool* timeout, uint32_t* done = nullptr, uint32_t sat = 0) {
+    const int lane = threadIdx.x & 63;
+    uint32_t excl = 0;
+    int p = c - 1;
+    uint32_t spins = 0;
+    for (;;) {
+        const int idx = p - lane;
+        const u64 w = idx >= 0 ? lb_load(st + idx) : LB_INC;
+        const uint32_t fl = (uint32_t)(w >> 62);
+        const u64 inc = __ballot(fl == 2u);
+        const u64 notready = __ballot(fl == 0u);
+        const int first = inc ? (int)__builtin_ctzll(inc) : 64;          // nearest inclusive
+        const u64 need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);  // lanes 0..first
+        if (notready & need) {
+            if (done && ld_agent(done)) return sat;
+            if (++spins > (1u << 22)) {
+                *timeout = true;
+                return excl;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        uint32_t v = lane <= first ? (uint32_t)w : 0u;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        excl += v;
+        if (first < 64) return excl;
+        p -= 64;
+    }
+}
+
+template <typename T, bool NT>
+__device__ __forceinline__ void pee_load_chunk(const T* src, int W, int CR, uint32_t items, int c,
+                                               typename Vec8<T>::type* a0, typename Vec8<T>::type* a1, size_t* o0) {
+    typedef typename Vec8<T>::type V;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint32_t it = (uint32_t)c * PEE_CHUNK + u * 256u + threadIdx.x;
+        if (it < items) {
+            const uint32_t r = it / CR, cc = it - r * CR;
+            o0[u] = (size_t)(2 * r) * W + (size_t)cc * 8;
+            a0[u] = ldv<NT>(reinterpret_cast<const V*>(src + o0[u]));
+            a1[u] = ldv<NT>(reinterpret_cast<const V*>(src + o0[u] + W));
+        }
+    }
+}
+
+// ctl[0] = slices finished (in place); slice b: chunk ticket ctl[32 + 32 b], finished flag
+// ctl[33 + 32 b] (one 128-byte line per slice: tickets of different slices never contend).
+// Out of place: one workgroup per (slice, chunk) slot, slice-major.  In place: persistent
+// workgroups walk the slots chunk-major, so a slice's later chunks are only reached after
+// its earlier ones, and skip (without a ticket) once the slice is finished.
+#define PEE_CTL_WORDS(B) (32 + 32 * (size_t)(B))
+#define PEE_SKIP 0xFFFFFFFFu
+#define PEE_STOP 0xFFFFFFFEu
+template <typename T, bool NT, bool INPLACE>
+__global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover, T* stego, int H, int W, int Tthr,
+                                                    int maxval, const int32_t* __restrict__ lengths,
+                                                    const u64* __restrict__ payload_all, int pw, int nchunks, int B,
+                                                    u64* status_all, uint32_t* ctl, codec_pee_meta* meta_all,
+                                                    u64* __restrict__ lm_all, int lmw) {
+    typedef typename Vec8<T>::type V;
+    __shared__ u64 sh64[8];
+    __shared__ uint32_t sh[8];
+    __shared__ uint32_t s_v, s_excl;
+    __shared__ uint32_t lm32[4 * PEE_TILE / 32];
+    const int CR = W / 8;
+    const uint32_t items = (uint32_t)(H / 2) * (uint32_t)CR;
+    const int nc = (H / 2) * (W / 2);
+    const int ntiles = (nc + PEE_TILE - 1) / PEE_TILE;
+    const uint32_t total = (uint32_t)nchunks * (uint32_t)B;
+    const size_t npx = (size_t)H * W;
+    const int tid = threadIdx.x;
+    for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
+        const int b = INPLACE ? (int)(v % (uint32_t)B) : (int)(v / (uint32_t)nchunks);
+        const int j = INPLACE ? (int)(v / (uint32_t)B) : (int)(v % (uint32_t)nchunks);
+        uint32_t* tick = ctl + 32 + 32 * (size_t)b;
+        u64* st = status_all + (size_t)b * nchunks;
+        const uint32_t L = (uint32_t)max(0, lengths[b]);
+        codec_pee_meta* M = meta_all + b;
+        const T* src = cover + b * npx;
+        T* dst = stego + b * npx;
+        V a0[4], a1[4];
+        size_t o0[4];
+        // out of place: the slot's own chunk j is loaded while the ticket is in flight (the
+        // ticket equals j unless workgroups were dispatched out of order)
+        if (!INPLACE) pee_load_chunk<T, NT>(src, W, CR, items, j, a0, a1, o0);
+        if (tid == 0) {
+            uint32_t cc = PEE_SKIP;
+            if (!INPLACE) {
+                cc = atomicAdd(tick, 1u);
+                if (ld_agent(tick + 1)) {   // `end` already placed: this chunk is a plain copy
+                    lb_store(st + cc, LB_INC | (u64)L);
+                    cc |= 0x80000000u;
+                }
+            } else if (ld_agent(ctl) >= (uint32_t)B) {
+                cc = PEE_STOP;
+            } else if (!ld_agent(tick + 1)) {
+                cc = atomicAdd(tick, 1u);
+                if (cc < (uint32_t)nchunks && ld_agent(tick + 1)) {   // finished meanwhile: "prefix >= L"
+                    lb_store(st + cc, LB_INC | (u64)L);
+                    cc = PEE_SKIP;
+                }
+            }
+            s_v = cc;
+        }
+        if (tid < 4 * PEE_TILE / 32) lm32[tid] = 0;
+        __syncthreads();
+        const uint32_t cv = s_v;
+        if (INPLACE) {
+            if (cv == PEE_STOP) return;
+            if (cv >= (uint32_t)nchunks) { __syncthreads(); continue; }
+        }
+        const bool copy_only = !INPLACE && (cv & 0x80000000u);
+        const int c = (int)(cv & 0x7FFFFFFFu);
+        if (INPLACE || c != j) pee_load_chunk<T, NT>(src, W, CR, items, c, a0, a1, o0);
+        if (copy_only) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t it = (uint32_t)c * PEE_CHUNK + u * 256u + tid;
+                if (it < items) {
+                    stv<NT>(reinterpret_cast<V*>(dst + o0[u]), a0[u]);
+                    stv<NT>(reinterpret_cast<V*>(dst + o0[u] + W), a1[u]);
+                }
+            }
+            if (tid < 64) {
+                const int w = c * (4 * PEE_TILE / 64) + tid;
+                if (w < lmw) lm_all[(size_t)b * lmw + w] = 0;
+            }
+            __syncthreads();
+            continue;
+        }
+        uint32_t esm = 0, safem = 0, rightm = 0;   // bit 4u+q
+        u64 packed = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t it = (uint32_t)c * PEE_CHUNK + u * 256u + tid;
+            if (it < items) {
+                uint32_t n = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const PeeCand pc = pee_classify((int)get_px(a1[u], 2 * q + 1), (int)get_px(a1[u], 2 * q),
+                                                    (int)get_px(a0[u], 2 * q + 1), (int)get_px(a0[u], 2 * q), Tthr, maxval);
+                    const uint32_t bit = 1u << (4 * u + q);
+                    if (pc.safe) safem |= bit;
+                    if (pc.right) rightm |= bit;
+                    if (pc.expand && pc.safe) { esm |= bit; ++n; }
+                }
+                packed |= (u64)n << (16 * u);
+            }
+        }
+        u64 ptot;
+        const u64 pex = block_excl_scan64<256>(packed, sh64, &ptot);
+        const uint32_t agg = (uint32_t)((ptot & 0xFFFFu) + ((ptot >> 16) & 0xFFFFu) + ((ptot >> 32) & 0xFFFFu) + (ptot >> 48));
+        if (c == 0) {
+            if (tid == 0) { lb_store(st, LB_INC | (u64)agg); s_excl = 0; }
+        } else {
+            if (tid == 0) lb_store(st + c, LB_AGG | (u64)agg);
+            if (tid < 64) {
+                bool to = false;
+                const uint32_t ex = lb_exclusive(st, c, &to, tick + 1, L);
+                if (tid == 0) {
+                    lb_store(st + c, LB_INC | (u64)(ex + agg));
+                    s_excl = ex;
+                    if (to) M->status = CODEC_PEE_ELOOKBACK;
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t excl = s_excl;
+        const bool last = c == nchunks - 1;
+        if (tid == 0) {
+            if (c == 0) {
+                M->T = Tthr; M->maxval = maxval; M->L = (int)L; M->nc = nc; M->ntiles = ntiles; M->h = H; M->w = W;
+                if (L == 0) { M->end = -1; M->tile_end = -1; M->status = 0; }
+            }
+            // the chunk holding `end` (or the last one on overflow) reports the capacity seen so
+            // far: exact when it is the last chunk, else a lower bound (later chunks are not counted)
+            const bool fin = (excl < L && excl + agg >= L) || (L == 0 && c == 0) || (last && excl + agg < L);
+            if (fin) {
+                M->capacity = (int)(excl + agg);
+                M->flags = last ? 0 : CODEC_PEE_PARTIAL;
+            }
+            if (last && excl + agg < L) { M->end = nc - 1; M->tile_end = ntiles - 1; M->status = 1; }
+        }
+        __syncthreads();   // lm32 zeroing vs the ORs below
+        if (excl < L) {   // some candidate of this chunk is active
+            uint32_t base = excl;
+            uint32_t unsafe_n = 0;
+            const u64* payload = payload_all + (size_t)b * pw;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t it = (uint32_t)c * PEE_CHUNK + u * 256u + tid;
+                uint32_t r = base + (uint32_t)((pex >> (16 * u)) & 0xFFFFu);
+                base += (uint32_t)((ptot >> (16 * u)) & 0xFFFFu);
+                if (it >= items) continue;
+                bool touched = false;
+                uint32_t nib = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t bit = 1u << (4 * u + q);
+                    if (r >= L) break;                     // past `end` (ranks only grow)
+                    const int x = (int)get_px(a1[u], 2 * q + 1);
+                    const int k = (int)(4 * it) + q;
+                    touched = true;
+                    if (!(safem & bit)) { nib |= 1u << q; ++unsafe_n; continue; }
+                    int nv;
+                    if (esm & bit) {
+                        const int p = med3((int)get_px(a1[u], 2 * q), (int)get_px(a0[u], 2 * q + 1), (int)get_px(a0[u], 2 * q));
+                        const int pb = (int)((payload[r >> 6] >> (r & 63)) & 1ull);
+                        nv = p + 2 * (x - p) + pb;
+                        if (r == L - 1) { M->end = k; M->tile_end = k / PEE_TILE; M->status = 0; }
+                        ++r;
+                    } else {
+                        nv = (rightm & bit) ? x + Tthr : x - Tthr;
+                    }
+                    set_px(a1[u], 2 * q + 1, (uint32_t)nv);
+                }
+                if (nib) atomicOr(&lm32[u * 32 + (tid >> 3)], nib << (4 * (tid & 7)));
+                if (INPLACE && touched) stv<NT>(reinterpret_cast<V*>(dst + o0[u] + W), a1[u]);
+            }
+            const uint32_t nun = block_sum_u32<256>(unsafe_n, sh);   // also orders the lm32 ORs
+            if (tid == 0 && nun) atomicAdd(&M->lm_count, (int)nun);
+        }
+        if (tid == 0) {   // `end` is in this chunk (or there is none): later chunks need no cursor
+            const bool fin = (excl < L && excl + agg >= L) || (L == 0 && c == 0) || (last && excl + agg < L);
+            if (fin) {
+                __hip_atomic_store(tick + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (INPLACE) atomicAdd(ctl, 1u);
+            }
+        }
+        if (!INPLACE) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t it = (uint32_t)c * PEE_CHUNK + u * 256u + tid;
+                if (it < items) {
+                    stv<NT>(reinterpret_cast<V*>(dst + o0[u]), a0[u]);
+                    stv<NT>(reinterpret_cast<V*>(dst + o0[u] + W), a1[u]);
+                }
+            }
+        }
+        // location-map words of this chunk (zeros past `end`); in place only where active
+        if (!INPLACE || excl < L) {
+            if (tid < 64) {
+                const int w = c * (4 * PEE_TILE / 64) + tid;
+                if (w < lmw) lm_all[(size_t)b * lmw + w] = (u64)lm32[2 * tid] | ((u64)lm32[2 * tid + 1] << 32);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// extract: chunks up to the one holding `end` recover bits + pixels (look-back over the
+// inner-candidate counts); later chunks are a plain copy (out of place) or skipped.
+template <typename T, bool NT, bool INPLACE>
+__global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, int H, int W,
+                                                      const codec_pee_meta* __restrict__ meta_all,
+                                                      const u64* __restrict__ lm_all, int lmw, int nchunks, int B,
+                                                      u64* status_all, uint32_t* ctl, u64* __restrict__ payload_all,
+                                                      int pw) {
+    typedef typename Vec8<T>::type V;
+    __shared__ u64 sh64[8];
+    __shared__ uint32_t s_v, s_excl;
+    __shared__ int s_cmax;
+    const int CR = W / 8;
+    const uint32_t items = (uint32_t)(H / 2) * (uint32_t)CR;
+    const size_t npx = (size_t)H * W;
+    const int tid = threadIdx.x;
+    const uint32_t total = (uint32_t)nchunks * (uint32_t)B;
+    int cmax = nchunks - 1;
+    if (INPLACE) {   // chunk-major slots: nothing past the last chunk any slice needs
+        if (tid == 0) s_cmax = -1;
+        __syncthreads();
+        int cm = -1;
+        for (int b = tid; b < B; b += 256) {
+            const int e = meta_all[b].end;
+            cm = max(cm, e >= 0 ? (e >> 2) / PEE_CHUNK : -1);
+        }
+        if (cm >= 0) atomicMax(&s_cmax, cm);
+        __syncthreads();
+        cmax = s_cmax;
+    }
+    for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
+        const int b = INPLACE ? (int)(v % (uint32_t)B) : (int)(v / (uint32_t)nchunks);
+        const int j = INPLACE ? (int)(v / (uint32_t)B) : (int)(v % (uint32_t)nchunks);
+        if (j > cmax) return;                           // in place: slots only grow
+        const codec_pee_meta* M = meta_all + b;
+        const int end = M->end, Tthr = M->T;
+        const int cend = end >= 0 ? (end >> 2) / PEE_CHUNK : -1;
+        if (INPLACE && j > cend) continue;              // uniform: no barrier passed yet
+        const T* src = stego + b * npx;
+        T* dst = cover + b * npx;
+        V a0[4], a1[4];
+        size_t o0[4];
+        pee_load_chunk<T, NT>(src, W, CR, items, j, a0, a1, o0);   // past `end`: plain copy of chunk j
+        int c = j;
+        if (j <= cend) {   // exactly cend+1 slots take tickets 0..cend (almost always c == j)
+            if (tid == 0) s_v = atomicAdd(ctl + 32 + 32 * (size_t)b, 1u);
+            __syncthreads();
+            c = (int)s_v;
+            if (c != j) pee_load_chunk<T, NT>(src, W, CR, items, c, a0, a1, o0);
+        }
+        if (c <= cend) {
+            const u64* lm = lm_all + (size_t)b * lmw;
+            uint32_t actm = 0, innm = 0;
+            u64 packed = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t it = (uint32_t)c * PEE_CHUNK + u * 256u + tid;
+                if (it >= items) continue;
+                const u64 lw = lm[(4 * it) >> 6] >> ((4 * it) & 63);   // 4 bits, same word
+                uint32_t n = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int k = (int)(4 * it) + q;
+                    if (k > end || ((lw >> q) & 1ull)) continue;
+                    actm |= 1u << (4 * u + q);
+                    const int p = med3((int)get_px(a1[u], 2 * q), (int)get_px(a0[u], 2 * q + 1), (int)get_px(a0[u], 2 * q));
+                    const int e2 = (int)get_px(a1[u], 2 * q + 1) - p;
+                    if (e2 >= -2 * Tthr && e2 < 2 * Tthr) { innm |= 1u << (4 * u + q); ++n; }
+                }
+                packed |= (u64)n << (16 * u);
+            }
+            u64 ptot;
+            const u64 pex = block_excl_scan64<256>(packed, sh64, &ptot);
+            const uint32_t agg = (uint32_t)((ptot & 0xFFFFu) + ((ptot >> 16) & 0xFFFFu) + ((ptot >> 32) & 0xFFFFu) + (ptot >> 48));
+            u64* st = status_all + (size_t)b * nchunks;
+            if (c == 0) {
+                if (tid == 0) { if (cend > 0) lb_store(st, LB_INC | (u64)agg); s_excl = 0; }
+            } else {
+                if (tid == 0 && c < cend) lb_store(st + c, LB_AGG | (u64)agg);
+                if (tid < 64) {
+                    bool to = false;
+                    const uint32_t ex = lb_exclusive(st, c, &to);
+                    if (tid == 0) {
+                        if (c < cend) lb_store(st + c, LB_INC | (u64)(ex + agg));
+                        s_excl = ex;
+                        if (to) atomicOr(ctl + 1, 1u);   // reported by codec_pee_extract's status word
+                    }
+                }
+            }
+            __syncthreads();
+            uint32_t base = s_excl;
+            u64* payload = payload_all + (size_t)b * pw;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                uint32_t r = base + (uint32_t)((pex >> (16 * u)) & 0xFFFFu);
+                base += (uint32_t)((ptot >> (16 * u)) & 0xFFFFu);
+                if (!((actm >> (4 * u)) & 0xFu)) continue;
+                u64 word = 0;
+                int wi = -1;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t bit = 1u << (4 * u + q);
+                    if (!(actm & bit)) continue;
+                    const int x = (int)get_px(a1[u], 2 * q + 1);
+                    const int p = med3((int)get_px(a1[u], 2 * q), (int)get_px(a0[u], 2 * q + 1), (int)get_px(a0[u], 2 * q));
+                    const int e2 = x - p;
+                    int nx;
+                    if (innm & bit) {
+                        if (e2 & 1) {
+                            if (wi != (int)(r >> 6)) {
+                                if (wi >= 0) atomicOr(&payload[wi], word);
+                                wi = (int)(r >> 6);
+                                word = 0;
+                            }
+                            word |= 1ull << (r & 63);
+                        }
+                        ++r;
+                        nx = p + (e2 >> 1);
+                    } else {
+                        nx = e2 >= 2 * Tthr ? x - Tthr : x + Tthr;
+                    }
+                    set_px(a1[u], 2 * q + 1, (uint32_t)nx);
+                }
+                if (wi >= 0 && word) atomicOr(&payload[wi], word);
+                if (INPLACE) stv<NT>(reinterpret_cast<V*>(dst + o0[u] + W), a1[u]);
+            }
+        }
+        if (!INPLACE) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t it = (uint32_t)c * PEE_CHUNK + u * 256u + tid;
+                if (it < items) {
+                    stv<NT>(reinterpret_cast<V*>(dst + o0[u]), a0[u]);
+                    stv<NT>(reinterpret_cast<V*>(dst + o0[u] + W), a1[u]);
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // ====================================================================== host side
 struct PeeWs {
-    size_t cnt, off, total;
-    int ntiles_max;
+    size_t cnt, off, st, ctl, total;
+    int ntiles_max, nchunks;
 };
 
 static PeeWs pee_ws(const codec_pee_params* P) {
@@ -593,9 +1016,14 @@ static PeeWs pee_ws(const codec_pee_params* P) {
     const long long nc = (long long)(P->H / 2) * (P->W / 2);
     L.ntiles_max = (int)((nc + PEE_TILE - 1) / PEE_TILE);
     if (L.ntiles_max < 1) L.ntiles_max = 1;
+    const long long items = (long long)(P->H / 2) * (P->W / 8);
+    L.nchunks = (int)((items + PEE_CHUNK - 1) / PEE_CHUNK);
+    if (L.nchunks < 1) L.nchunks = 1;
     L.cnt = 0;
     L.off = align_up((size_t)P->B * L.ntiles_max * 4, 256);
-    L.total = align_up(L.off + (size_t)P->B * L.ntiles_max * 4, 256);
+    L.st = align_up(L.off + (size_t)P->B * L.ntiles_max * 4, 256);
+    L.ctl = L.st + (size_t)P->B * L.nchunks * 8;   // status words and ctl are cleared together
+    L.total = align_up(L.ctl + PEE_CTL_WORDS(P->B) * 4, 256);
     return L;
 }
 
@@ -632,11 +1060,43 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
     hipStream_t st = as_stream(stream);
     uint32_t* cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.cnt);
     uint32_t* off = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.off);
-    HIP_TRY(hipMemsetAsync(lm, 0, (size_t)P->B * P->lm_words * 8, st));
     const long long npx = (long long)P->H * P->W;
     const size_t va = P->bytes == 2 ? 16 : 8;
     const bool vec = (P->W % 8) == 0 && ((uintptr_t)cover % va) == 0 && ((uintptr_t)stego % va) == 0;
     const bool nt = knob("CODEC_NT", 1) != 0;
+    const bool inplace = cover == stego;
+    const long long items = (long long)(P->H / 2) * (P->W / 8);
+    // single pass: always in place (it stops reading after `end`); out of place the two-pass
+    // scan + prefix embed measured faster (tickets + look-back on every chunk cost more than
+    // re-reading the ~12 % prefix).  CODEC_PEE_ONEPASS: -1 auto, 0 never, 1 always.
+    const long long onepass = knob("CODEC_PEE_ONEPASS", -1);
+    if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && (onepass > 0 || (onepass < 0 && inplace))) {
+        u64* stw = reinterpret_cast<u64*>(static_cast<char*>(workspace) + L.st);
+        uint32_t* ctl = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.ctl);
+        HIP_TRY(hipMemsetAsync(stw, 0, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4, st));
+        HIP_TRY(hipMemsetAsync(meta, 0, (size_t)P->B * sizeof(codec_pee_meta), st));
+        if (inplace) HIP_TRY(hipMemsetAsync(lm, 0, (size_t)P->B * P->lm_words * 8, st));
+        ProfScope prof(st, CODEC_K_PEE_EMBED1);
+        const long long total = (long long)L.nchunks * P->B;
+        long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));
+        if (g > total) g = total;
+        if (g < 1) g = 1;
+#define PE1(TT, NTV, IP) hipLaunchKernelGGL((k_pee_embed1<TT, NTV, IP>), dim3((unsigned)g), dim3(256), 0, st, \
+            static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, \
+            reinterpret_cast<const u64*>(payload), P->payload_words, L.nchunks, P->B, stw, ctl, meta, \
+            reinterpret_cast<u64*>(lm), P->lm_words)
+        if (P->bytes == 2) {
+            if (inplace) { if (nt) PE1(uint16_t, true, true); else PE1(uint16_t, false, true); }
+            else { if (nt) PE1(uint16_t, true, false); else PE1(uint16_t, false, false); }
+        } else {
+            if (inplace) { if (nt) PE1(uint8_t, true, true); else PE1(uint8_t, false, true); }
+            else { if (nt) PE1(uint8_t, true, false); else PE1(uint8_t, false, false); }
+        }
+#undef PE1
+        LAUNCH_CHECK("k_pee_embed1");
+        return 0;
+    }
+    HIP_TRY(hipMemsetAsync(lm, 0, (size_t)P->B * P->lm_words * 8, st));
     {
         ProfScope prof(st, CODEC_K_PEE_SCAN);
         const int ntiles = L.ntiles_max;
@@ -651,7 +1111,7 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
 #undef PSCAN
             LAUNCH_CHECK("k_pee_scan");
         } else {
-            HIP_TRY(hipMemcpyAsync(stego, cover, (size_t)npx * P->B * P->bytes, hipMemcpyDeviceToDevice, st));
+            if (!inplace) HIP_TRY(hipMemcpyAsync(stego, cover, (size_t)npx * P->B * P->bytes, hipMemcpyDeviceToDevice, st));
             if (P->bytes == 2)
                 hipLaunchKernelGGL(k_pee_count<uint16_t>, grid, dim3(256), 0, st, static_cast<const uint16_t*>(cover),
                                    P->H, P->W, P->T, P->maxval, per, cnt, L.ntiles_max);
@@ -703,6 +1163,31 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
     const bool vec = (P->W % 8) == 0 && ((uintptr_t)stego % va) == 0 && ((uintptr_t)cover_out % va) == 0;
     HIP_TRY(hipMemsetAsync(payload_out, 0, (size_t)P->B * P->payload_words * 8, st));
     const long long items = (long long)(P->H / 2) * (P->W / 8);
+    const bool inplace = stego == cover_out;
+    const long long onepass = knob("CODEC_PEE_ONEPASS", -1);   // as in codec_pee_embed
+    if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && (onepass > 0 || (onepass < 0 && inplace))) {
+        u64* stw = reinterpret_cast<u64*>(static_cast<char*>(workspace) + L.st);
+        uint32_t* ctl = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.ctl);
+        HIP_TRY(hipMemsetAsync(stw, 0, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4, st));
+        ProfScope prof(st, CODEC_K_PEE_EXTRACT1);
+        const long long total = (long long)L.nchunks * P->B;
+        long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));
+        if (g > total) g = total;
+        if (g < 1) g = 1;
+#define PX1(TT, NTV, IP) hipLaunchKernelGGL((k_pee_extract1<TT, NTV, IP>), dim3((unsigned)g), dim3(256), 0, st, \
+            static_cast<const TT*>(stego), static_cast<TT*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm), \
+            P->lm_words, L.nchunks, P->B, stw, ctl, reinterpret_cast<u64*>(payload_out), P->payload_words)
+        if (P->bytes == 2) {
+            if (inplace) { if (nt) PX1(uint16_t, true, true); else PX1(uint16_t, false, true); }
+            else { if (nt) PX1(uint16_t, true, false); else PX1(uint16_t, false, false); }
+        } else {
+            if (inplace) { if (nt) PX1(uint8_t, true, true); else PX1(uint8_t, false, true); }
+            else { if (nt) PX1(uint8_t, true, false); else PX1(uint8_t, false, false); }
+        }
+#undef PX1
+        LAUNCH_CHECK("k_pee_extract1");
+        return 0;
+    }
     const bool fused = vec && knob("CODEC_PEE_FUSED", 1) != 0 && (P->W % 8) == 0 && items > 0 && (items % 256) == 0 &&
                        items * P->B < 0xFFFFFFFFLL;
     if (fused) {

@@ -103,7 +103,9 @@ size_t codec_workspace_bytes(const codec_params* P);
  *   (merge_modalities, codec.py:215-237).
  * cover[B][H][W] (in_bytes) -> stego[B][H][W] (out_bytes; may be NULL: plan only),
  * meta[B].  log2_lut[c-1] = numpy.log2(c / (H*W)) for c = 1..H*W (lut_len >= H*W);
- * table[n_classes*16 + (s-1)] is the layout for payload class slice_class[b] and s. */
+ * table[n_classes*16 + (s-1)] is the layout for payload class slice_class[b] and s.
+ * stego == cover (same dtype) = in place: the pass only reads, codec_embed then rewrites
+ * the window pixels of the cover buffer itself. */
 int codec_plan(const codec_params* P, const void* cover, void* stego, const double* log2_lut,
                int64_t lut_len, const codec_layout* table, const int32_t* slice_class,
                codec_slice_meta* meta, void* workspace, size_t workspace_bytes, void* stream);
@@ -117,7 +119,8 @@ int codec_embed(const codec_params* P, const void* cover, void* stego, const uin
                 const codec_slice_meta* meta, uint64_t* maps, void* stream);
 
 /* True extraction: payload bits in segment order + cover restore (inverse of the above).
- * cover_out may be NULL (payload only).  payload_out[B][payload_words]. */
+ * cover_out may be NULL (payload only).  payload_out[B][payload_words].
+ * cover_out == stego = in place: only the window pixels are rewritten (after the gather). */
 int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps,
                   const codec_slice_meta* meta, void* cover_out, uint64_t* payload_out,
                   void* stream);
@@ -179,16 +182,30 @@ typedef struct codec_pee_meta {
     int32_t T, maxval, L, end; /* end = last processed candidate index, -1 if none */
     int32_t nc, ntiles, tile_end, status; /* status 1: payload exceeds capacity    */
     int32_t capacity, lm_count, h, w;
-    int32_t reserved[4];
+    int32_t flags;             /* CODEC_PEE_PARTIAL                                 */
+    int32_t reserved[3];
 } codec_pee_meta;
+
+/* meta.flags: the embed stopped reading after the chunk holding `end` (in-place embed),
+ * so `capacity` counts expandable candidates up to that chunk only (a lower bound). */
+#define CODEC_PEE_PARTIAL 1
+/* meta.status values: 0 ok, 1 payload exceeds capacity (truncated, still reversible),
+ * CODEC_PEE_ELOOKBACK: the single-pass cursor look-back gave up waiting for a predecessor
+ * chunk (bounded spin instead of a GPU hang; requires out-of-order workgroup dispatch). */
+#define CODEC_PEE_ELOOKBACK 2
 
 size_t codec_pee_workspace_bytes(const codec_pee_params* P);
 /* cover -> stego (full copy + expansion/shifting of candidates 0..end), lm, meta.
- * lengths[B] (device int32) = payload bits per slice. */
+ * lengths[B] (device int32) = payload bits per slice.
+ * stego == cover is allowed (in place): only the items up to `end` are read and
+ * written, everything after `end` is left untouched.
+ * Payload longer than the capacity: status 1, the first `capacity` bits are embedded,
+ * end = nc - 1 (every candidate processed) and the slice stays exactly reversible. */
 int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, const uint64_t* payload,
                     const int32_t* lengths, codec_pee_meta* meta, uint64_t* lm, void* workspace,
                     size_t workspace_bytes, void* stream);
-/* stego -> exact payload bits + restored cover. */
+/* stego -> exact payload bits + restored cover.  cover_out == stego is allowed (in
+ * place: only the items up to `end` are read and written). */
 int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_pee_meta* meta,
                       const uint64_t* lm, void* cover_out, uint64_t* payload_out, void* workspace,
                       size_t workspace_bytes, void* stream);
@@ -210,6 +227,8 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
 #define CODEC_K_PEE_COPY 12
 #define CODEC_K_PEE_DCOUNT 13
 #define CODEC_K_PEE_RECOVER 14
+#define CODEC_K_PEE_EMBED1 15
+#define CODEC_K_PEE_EXTRACT1 16
 int codec_profile_begin(int32_t capacity);
 /* after the stream has been synchronised: fills ms[i], tag[i] for the recorded pairs and
  * returns their count (closes the window and frees the events). */

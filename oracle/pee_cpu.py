@@ -22,6 +22,11 @@ Scheme (integer only):
   cursor      payload bit j goes to the j-th expandable, non-overflow candidate in index
               order; processing stops at that candidate for j = L-1 ("end"); candidates
               after `end` are untouched.  Side information: T, L, end, maxval, LM[0..end].
+  overflow of the payload (L > capacity): with truncate=True the first `capacity` bits are
+              embedded and end = the last candidate (every candidate is processed), status 1;
+              the slice stays exactly reversible.  A single streaming pass cannot know
+              that no expandable candidate follows, so this -- not "stop at the last
+              expandable one" -- is the definition the GPU kernels implement.
   decoding    e' = x' - pred; LM -> unchanged; -2T <= e' < 2T -> bit = e' & 1,
               x = pred + (e' >> 1); e' >= 2T -> x = x' - T; else x = x' + T.
 """
@@ -57,7 +62,8 @@ def classify(x, p, T: int, maxval: int):
     return e, expand, right, safe
 
 
-def pee_embed(cover: np.ndarray, bits: np.ndarray, T: int = 2, maxval: int | None = None) -> Tuple[np.ndarray, Dict]:
+def pee_embed(cover: np.ndarray, bits: np.ndarray, T: int = 2, maxval: int | None = None,
+              truncate: bool = False) -> Tuple[np.ndarray, Dict]:
     if cover.dtype not in (np.uint8, np.uint16) or cover.ndim != 2:
         raise ValueError("cover must be a 2-D uint8/uint16 image")
     if T < 1:
@@ -70,9 +76,14 @@ def pee_embed(cover: np.ndarray, bits: np.ndarray, T: int = 2, maxval: int | Non
     e, expand, right, safe = classify(x, p, T, maxval)
     es = (expand & safe).ravel()
     capacity = int(es.sum())
+    status = 0
     if capacity < L:
-        raise ValueError(f"payload of {L} bits exceeds the capacity {capacity} at T={T}")
-    end = int(np.flatnonzero(es)[L - 1]) if L else -1
+        if not truncate:
+            raise ValueError(f"payload of {L} bits exceeds the capacity {capacity} at T={T}")
+        bits, L, status = bits[:capacity], capacity, 1
+        end = es.size - 1
+    else:
+        end = int(np.flatnonzero(es)[L - 1]) if L else -1
     k = np.arange(es.size)
     proc = (k <= end) & safe.ravel()
     cursor = np.cumsum(es) - 1
@@ -86,7 +97,7 @@ def pee_embed(cover: np.ndarray, bits: np.ndarray, T: int = 2, maxval: int | Non
     hc, wc = x.shape
     stego[1:2 * hc:2, 1:2 * wc:2] = out.reshape(hc, wc).astype(cover.dtype)
     lm = ~safe.ravel()[: end + 1]
-    return stego, {"T": T, "L": L, "end": end, "maxval": maxval, "lm": lm, "capacity": capacity}
+    return stego, {"T": T, "L": L, "end": end, "maxval": maxval, "lm": lm, "capacity": capacity, "status": status}
 
 
 def pee_extract(stego: np.ndarray, side: Dict) -> Tuple[np.ndarray, np.ndarray]:

@@ -147,3 +147,49 @@ def test_shape_errors():
         codec.encode(torch.zeros((1, 64, 64), dtype=torch.uint16, device="cuda"), ["a"])
     with pytest.raises(TypeError):
         codec.encode(torch.zeros((2, 64, 64), dtype=torch.uint8, device="cuda"), ["a", "b"])
+
+
+INPLACE = [c for c in CASES if int(c["nbits"]) < 0 or int(c["nbits"]) > 8 * c["cover"].dtype.itemsize - 8]
+
+
+@pytest.mark.parametrize("case", INPLACE, ids=[c["name"] for c in INPLACE])
+def test_inplace_matches_out_of_place(case):
+    """stego == cover (codec_plan reads only, codec_embed patches the windows) and
+    cover_out == stego (only the window pixels are XOR-ed back) give the out-of-place
+    results bit for bit."""
+    codec, enc = _run_case(case)
+    cover = case["cover"]
+    bitstr = str(case["bits"])
+    bits = (np.frombuffer(bitstr.encode(), np.uint8) - 48) if bitstr else np.zeros(0, np.uint8)
+    buf = torch.from_numpy(cover[None].copy()).cuda()
+    enc2 = codec.encode(buf, [bits], stego=buf)
+    assert enc2.stego.data_ptr() == buf.data_ptr()
+    np.testing.assert_array_equal(buf.cpu().numpy()[0], golden_io.stego(case))
+    used = (enc.records()[0].total_used + 63) // 64   # words past the embedded bits are unspecified
+    np.testing.assert_array_equal(enc2.maps.cpu().numpy()[:, :used], enc.maps.cpu().numpy()[:, :used])
+    np.testing.assert_array_equal(enc2.meta.cpu().numpy(), enc.meta.cpu().numpy())
+    pw, mw = enc.payloads.payload_words, enc.payloads.map_words
+    words_a, cover_a = codec.decode(enc.stego, enc.maps, enc.meta, payload_words=pw, map_words=mw)
+    words_b, cover_b = codec.decode(buf, enc2.maps, enc2.meta, payload_words=pw, map_words=mw, cover=buf)
+    assert cover_b.data_ptr() == buf.data_ptr()
+    np.testing.assert_array_equal(words_b.cpu().numpy(), words_a.cpu().numpy())
+    np.testing.assert_array_equal(buf.cpu().numpy(), cover_a.cpu().numpy())
+
+
+@pytest.mark.parametrize("kind,h,w,bsz,mode", [("ct12", 512, 512, 4, "hybrid"), ("u16", 256, 320, 3, "hybrid"),
+                                               ("u8", 200, 96, 3, "hybrid"), ("ct12", 128, 128, 3, "multi"),
+                                               ("ct12", 37, 53, 2, "hybrid")])
+def test_inplace_batch_roundtrip(kind, h, w, bsz, mode):
+    gen = synth.GENERATORS[kind]
+    covers = np.stack([gen(h, w, 300 + i) for i in range(bsz)])
+    msgs = [synth.payload(40 + 53 * i, 11 + i) for i in range(bsz)]
+    codec = Codec(bsz, h, w, dtype=str(covers.dtype), beta=0.4, block=16, mode=mode)
+    ref = codec.encode(torch.from_numpy(covers).cuda(), msgs)
+    buf = torch.from_numpy(covers.copy()).cuda()
+    enc = codec.encode(buf, msgs, stego=buf)
+    np.testing.assert_array_equal(buf.cpu().numpy(), ref.stego.cpu().numpy())
+    pw, mw = enc.payloads.payload_words, enc.payloads.map_words
+    words, _ = codec.decode(buf, enc.maps, enc.meta, payload_words=pw, map_words=mw, cover=buf)
+    ref_words, _ = codec.decode(ref.stego, ref.maps, ref.meta, payload_words=pw, map_words=mw)
+    np.testing.assert_array_equal(words.cpu().numpy(), ref_words.cpu().numpy())
+    np.testing.assert_array_equal(buf.cpu().numpy(), covers)

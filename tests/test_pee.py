@@ -48,28 +48,100 @@ def test_oracle_med_definition():
     np.testing.assert_array_equal(P.med(a, b, c), [5, 9, 7, 7])
 
 
+def test_oracle_truncates_on_overflow():
+    img = synth.ct12(48, 64, 5)
+    cap = P.capacity(img, 1)
+    bits = _bits(cap + 40, 9)
+    st, side = P.pee_embed(img, bits, 1, truncate=True)
+    assert side["status"] == 1 and side["L"] == cap and side["end"] == (48 // 2) * (64 // 2) - 1
+    got, cov = P.pee_extract(st, side)
+    np.testing.assert_array_equal(got, bits[:cap])
+    np.testing.assert_array_equal(cov, img)
+
+
+# single pass (decoupled look-back, W % 8 == 0): default for in-place embed and for extract;
+# "1" forces it everywhere, "0" forces the two-pass scan/locate/embed path; small
+# persistent grids exercise the slot loop
+PATHS = {"auto": {}, "onepass": {"CODEC_PEE_ONEPASS": "1"}, "twopass": {"CODEC_PEE_ONEPASS": "0"},
+         "onepass_small_grid": {"CODEC_PEE_ONEPASS": "1", "CODEC_PEE_1P_WGS": "7", "CODEC_PEE_IP_WGS": "3"}}
+
+
+@pytest.fixture(params=sorted(PATHS))
+def pee_path(request, monkeypatch):
+    for k, v in PATHS[request.param].items():
+        monkeypatch.setenv(k, v)
+    return request.param
+
+
+def _lengths(caps, bsz):
+    out = [min(cap, 8192 - 97 * i) for i, cap in enumerate(caps)]
+    if bsz >= 3:
+        out[1] = 0                      # an empty payload in the middle of the batch
+    return out
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("inplace", [False, True])
 @pytest.mark.parametrize("kind,h,w,bsz,T", [("ct12", 256, 256, 3, 2), ("ct12", 120, 136, 2, 1), ("u8", 96, 64, 2, 4),
-                                            ("ct12", 37, 53, 2, 3), ("ct12", 2048, 2048, 2, 2), ("u16", 64, 64, 1, 8)])
-def test_gpu_matches_oracle(kind, h, w, bsz, T):
+                                            ("ct12", 37, 53, 2, 3), ("ct12", 2048, 2048, 2, 2), ("u16", 64, 64, 1, 8),
+                                            ("ct12", 66, 1024, 3, 2)])
+def test_gpu_matches_oracle(kind, h, w, bsz, T, inplace, pee_path):
     torch = pytest.importorskip("torch")
+    from codec_tcc_amd import _lib
     from codec_tcc_amd.pee import PeeCodec, lm_bits
     covers = np.stack([synth.GENERATORS[kind](h, w, 40 + i) for i in range(bsz)])
     caps = [P.capacity(c, T) for c in covers]
-    payloads = [_bits(min(cap, 8192 - 97 * i), i) for i, cap in enumerate(caps)]
+    payloads = [_bits(n, i) for i, n in enumerate(_lengths(caps, bsz))]
     codec = PeeCodec(bsz, h, w, dtype=str(covers.dtype), T=T)
-    enc = codec.embed(torch.from_numpy(covers).cuda(), payloads)
+    dev = torch.from_numpy(covers).cuda()
+    enc = codec.embed(dev, payloads, stego=dev if inplace else None)
     recs = enc.records()
     stego = enc.stego.cpu().numpy()
     for i in range(bsz):
         st, side = P.pee_embed(covers[i], payloads[i], T)
-        assert recs[i].status == 0 and recs[i].end == side["end"] and recs[i].capacity == side["capacity"]
+        assert recs[i].status == 0 and recs[i].end == side["end"]
+        if recs[i].flags & _lib.PEE_PARTIAL:
+            assert pee_path != "twopass" and side["L"] <= recs[i].capacity <= side["capacity"]
+        else:
+            assert recs[i].capacity == side["capacity"]
         np.testing.assert_array_equal(stego[i], st)
         np.testing.assert_array_equal(lm_bits(enc, i), side["lm"])
         assert recs[i].lm_count == int(side["lm"].sum())
-    bits, cover = codec.decode(enc)
+    words, cover = codec.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words,
+                                 cover=enc.stego if inplace else None)
+    host = words.cpu().numpy()
+    from codec_tcc_amd import framing
     for i in range(bsz):
-        np.testing.assert_array_equal(bits[i], payloads[i])
+        np.testing.assert_array_equal(framing.unpack_bits(host[i], len(payloads[i])), payloads[i])
+    np.testing.assert_array_equal(cover.cpu().numpy(), covers)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inplace", [False, True])
+@pytest.mark.parametrize("kind,h,w", [("ct12", 64, 64), ("ct12", 130, 2048), ("u8", 40, 24)])
+def test_gpu_overflow_truncates_and_stays_reversible(kind, h, w, inplace, pee_path):
+    torch = pytest.importorskip("torch")
+    from codec_tcc_amd import framing
+    from codec_tcc_amd.pee import PeeCodec, lm_bits
+    covers = np.stack([synth.GENERATORS[kind](h, w, 70 + i) for i in range(2)])
+    caps = [P.capacity(c, 1) for c in covers]
+    payloads = [_bits(caps[0] + 77, 0), _bits(min(caps[1], 500), 1)]   # slice 0 overflows
+    codec = PeeCodec(2, h, w, dtype=str(covers.dtype), T=1)
+    dev = torch.from_numpy(covers).cuda()
+    enc = codec.embed(dev, payloads, stego=dev if inplace else None)
+    recs = enc.records()
+    st0, side0 = P.pee_embed(covers[0], payloads[0], 1, truncate=True)
+    assert recs[0].status == 1 and recs[0].end == side0["end"] and recs[0].capacity == caps[0]
+    assert recs[1].status == 0
+    np.testing.assert_array_equal(enc.stego[0].cpu().numpy(), st0)
+    np.testing.assert_array_equal(lm_bits(enc, 0), side0["lm"])
+    with pytest.raises(ValueError):
+        codec.decode(enc)
+    words, cover = codec.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words,
+                                 cover=enc.stego if inplace else None)
+    host = words.cpu().numpy()
+    np.testing.assert_array_equal(framing.unpack_bits(host[0], caps[0]), payloads[0][: caps[0]])
+    np.testing.assert_array_equal(framing.unpack_bits(host[1], len(payloads[1])), payloads[1])
     np.testing.assert_array_equal(cover.cpu().numpy(), covers)
 
 
@@ -81,6 +153,6 @@ def test_gpu_capacity_exceeded_flags():
     cap = P.capacity(img[0], 1)
     codec = PeeCodec(1, 64, 64, T=1)
     enc = codec.embed(torch.from_numpy(img).cuda(), [_bits(cap + 5, 0)])
-    assert enc.records()[0].status == 1
+    assert enc.records()[0].status == 1 and enc.records()[0].end == 32 * 32 - 1
     with pytest.raises(ValueError):
         codec.decode(enc)

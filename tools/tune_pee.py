@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of PEE launch knobs (env read per call by the C ABI), out of place and
+in place, on the bench workload.
+
+    python tools/tune_pee.py --configs '[{"CODEC_PEE_IP_WGS": "1024"}, {}]' [--rounds 3]
+Prints, per configuration and mode, the median per-kernel HIP-event times over rounds."""
+import argparse
+import json
+import os
+import sys
+import types
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="[{}]")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--size", type=int, default=2048)
+    ap.add_argument("--kind", default="ct12")
+    a = ap.parse_args()
+    import torch
+
+    import bench
+    configs = json.loads(a.configs)
+    dev = torch.device("cuda", 0)
+    B, H, W = a.batch, a.size, a.size
+    covers = bench.make_covers(torch, a.kind, B, H, W, dev, 0)
+    args = types.SimpleNamespace(payload_chars=1024, pee_T=2, warmup=2, steps=10, no_profile=False)
+    res = {}
+    for _ in range(a.rounds):
+        for i, cfg in enumerate(configs):
+            saved = {k: os.environ.get(k) for k in cfg}
+            os.environ.update(cfg)
+            for mode in (False, True):
+                r = bench.bench_pee(args, torch, None, 1, dev, covers, B, H, W, inplace=mode)
+                assert r["roundtrip_ok"], (cfg, mode)
+                d = res.setdefault((i, mode), {})
+                for k, v in r["kernels_ms"].items():
+                    d.setdefault(k, []).append(v)
+                d.setdefault("step_ms", []).append(r["ms_per_step"])
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+    for (i, mode), d in sorted(res.items()):
+        print(json.dumps({"cfg": configs[i], "inplace": mode,
+                          "ms": {k: round(float(np.median(v)), 4) for k, v in d.items()}}))
+
+
+if __name__ == "__main__":
+    main()
