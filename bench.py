@@ -163,10 +163,10 @@ def bench_lsb_inplace(args, torch, dist, world, dev, covers, codec, pl, B, H, W)
     res = {"value": round(B * H * W * world * args.steps / el / 1e6, 1), "unit": "Mpixels/s",
            "ms_per_step": round(el / args.steps * 1e3, 4), "roundtrip_ok": ok,
            "kernels_ms": {k: round(v, 4) for k, v in kern.items()}}
-    if "k_scan_fast" in kern:
+    if "k_scan_read" in kern:
         by = B * H * W * 2                               # read-only pass over the cover
-        t_k = kern["k_scan_fast"] / 1e3
-        res["roofline"] = {"bound": "hbm", "kernel": "k_scan_fast (read-only)", "achieved": round(by / t_k / 1e9, 1),
+        t_k = kern["k_scan_read"] / 1e3
+        res["roofline"] = {"bound": "hbm", "kernel": "k_scan_read", "achieved": round(by / t_k / 1e9, 1),
                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(by / t_k / 1e9 / HBM_PEAK_GBS, 4),
                            "algorithmic_bytes_per_launch": by}
     return res

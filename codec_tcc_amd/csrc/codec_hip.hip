@@ -310,11 +310,11 @@ __device__ __forceinline__ void hist_add8(uint32_t* lds, uint32_t* ghist, const 
 // Work item = (band of SB rows, 8-pixel column chunk); a wave covers 64 consecutive
 // chunks of one band, so every load instruction reads 1 KiB (u16) contiguously; the
 // SB/8 lanes of one block column combine their LSB counts with shuffles.
-template <typename T, int SB, bool NT, bool HIST = true>
-__global__ __launch_bounds__(1024) void k_scan_fast(const T* __restrict__ cover, T* __restrict__ stego,
-                                                    int H, int W, int bands_per_wg,
-                                                    uint32_t* __restrict__ ghist_all,
-                                                    u64* __restrict__ gkey, uint32_t* __restrict__ gor) {
+template <typename T, int SB, bool NT, bool HIST>
+__device__ __forceinline__ void scan_fast_body(const T* __restrict__ cover, T* __restrict__ stego,
+                                               int H, int W, int bands_per_wg,
+                                               uint32_t* __restrict__ ghist_all,
+                                               u64* __restrict__ gkey, uint32_t* __restrict__ gor) {
     typedef typename Vec8<T>::type V;
     constexpr int G = SB / 8;
     constexpr uint32_t NPB = (uint32_t)SB * SB;
@@ -408,6 +408,23 @@ __global__ __launch_bounds__(1024) void k_scan_fast(const T* __restrict__ cover,
     __syncthreads();
     hist_flush<T>(lds, ghist);
     if (threadIdx.x == 0 && wkey) atomicMax(&gkey[b], wkey);
+}
+
+template <typename T, int SB, bool NT, bool HIST = true>
+__global__ __launch_bounds__(1024) void k_scan_fast(const T* __restrict__ cover, T* __restrict__ stego,
+                                                    int H, int W, int bands_per_wg,
+                                                    uint32_t* __restrict__ ghist_all,
+                                                    u64* __restrict__ gkey, uint32_t* __restrict__ gor) {
+    scan_fast_body<T, SB, NT, HIST>(cover, stego, H, W, bands_per_wg, ghist_all, gkey, gor);
+}
+
+// read-only variant (plan only, or in place where the stego copy is the cover itself); a
+// separate symbol so profiles never average it with the copying pass
+template <typename T, int SB>
+__global__ __launch_bounds__(1024) void k_scan_read(const T* __restrict__ cover, int H, int W, int bands_per_wg,
+                                                    uint32_t* __restrict__ ghist_all,
+                                                    u64* __restrict__ gkey, uint32_t* __restrict__ gor) {
+    scan_fast_body<T, SB, true, true>(cover, nullptr, H, W, bands_per_wg, ghist_all, gkey, gor);
 }
 
 // ------------------------------------------------------------------ K1': scan + copy (generic)
@@ -1360,6 +1377,17 @@ static int launch_scan_fast(const codec_params* P, const void* cover, void* steg
     dim3 grid(wgps, P->B);
     const T* c = static_cast<const T*>(cover);
     T* s = static_cast<T*>(stego);
+    if (!s) {
+        ProfScope prof(st, CODEC_K_SCAN_READ);
+        switch (sb) {
+            case 8: hipLaunchKernelGGL((k_scan_read<T, 8>), grid, dim3(1024), 0, st, c, P->H, P->W, bpw, hist, keys, orv); break;
+            case 16: hipLaunchKernelGGL((k_scan_read<T, 16>), grid, dim3(1024), 0, st, c, P->H, P->W, bpw, hist, keys, orv); break;
+            case 32: hipLaunchKernelGGL((k_scan_read<T, 32>), grid, dim3(1024), 0, st, c, P->H, P->W, bpw, hist, keys, orv); break;
+            default: hipLaunchKernelGGL((k_scan_read<T, 64>), grid, dim3(1024), 0, st, c, P->H, P->W, bpw, hist, keys, orv); break;
+        }
+        LAUNCH_CHECK("k_scan_read");
+        return 0;
+    }
     ProfScope prof(st, CODEC_K_SCAN_FAST);
     switch (sb) {
         case 8: if (nt) hipLaunchKernelGGL((k_scan_fast<T, 8, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv);
@@ -1567,7 +1595,7 @@ int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps
     }
     if (inplace) {
         dim3 grid((unsigned)(((long long)P->map_words * 64 + 255) / 256), P->B);
-        ProfScope prof(st, CODEC_K_RESTORE);
+        ProfScope prof(st, CODEC_K_UNXOR);
         if (P->in_bytes == 2)
             hipLaunchKernelGGL(k_unxor<uint16_t>, grid, dim3(256), 0, st, static_cast<uint16_t*>(cover_out), npx, meta,
                                reinterpret_cast<const u64*>(maps), P->map_words);

@@ -659,6 +659,23 @@ __device__ __forceinline__ void pee_load_chunk(const T* src, int W, int CR, uint
     }
 }
 
+// Slot v -> (slice b, chunk j).  Workgroups are observed to be dealt round-robin over the
+// 8 XCDs (MI355X_MICROARCH.md: blocks b and b+8 share one), so slot lane x = v % 8 owns
+// slices x, x+8, ...: a slice's chunks then start in order on one XCD and their per-slice
+// tickets come back in slot order, which is what lets the speculative load of chunk j be
+// the ticketed chunk (correctness never depends on it: the ticket decides the chunk).
+// Out of place the lane walks its slices slice-major, in place chunk-major.
+__device__ __forceinline__ bool pee_slot(uint32_t v, int B, int nchunks, bool chunk_major, int* b, int* j) {
+    const int B8 = (B + 7) / 8;
+    const int x = (int)(v & 7u);
+    const uint32_t k = v >> 3;
+    int bi;
+    if (chunk_major) { *j = (int)(k / (uint32_t)B8); bi = (int)(k - (uint32_t)*j * B8); }
+    else { bi = (int)(k / (uint32_t)nchunks); *j = (int)(k - (uint32_t)bi * nchunks); }
+    *b = x + 8 * bi;
+    return *b < B;
+}
+
 // ctl[0] = slices finished (in place); slice b: chunk ticket ctl[32 + 32 b], finished flag
 // ctl[33 + 32 b] (one 128-byte line per slice: tickets of different slices never contend).
 // Out of place: one workgroup per (slice, chunk) slot, slice-major.  In place: persistent
@@ -682,12 +699,12 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
     const uint32_t items = (uint32_t)(H / 2) * (uint32_t)CR;
     const int nc = (H / 2) * (W / 2);
     const int ntiles = (nc + PEE_TILE - 1) / PEE_TILE;
-    const uint32_t total = (uint32_t)nchunks * (uint32_t)B;
+    const uint32_t total = 8u * (uint32_t)((B + 7) / 8) * (uint32_t)nchunks;
     const size_t npx = (size_t)H * W;
     const int tid = threadIdx.x;
     for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
-        const int b = INPLACE ? (int)(v % (uint32_t)B) : (int)(v / (uint32_t)nchunks);
-        const int j = INPLACE ? (int)(v / (uint32_t)B) : (int)(v % (uint32_t)nchunks);
+        int b, j;
+        if (!pee_slot(v, B, nchunks, INPLACE, &b, &j)) continue;   // uniform; no barrier passed
         uint32_t* tick = ctl + 32 + 32 * (size_t)b;
         u64* st = status_all + (size_t)b * nchunks;
         const uint32_t L = (uint32_t)max(0, lengths[b]);
@@ -880,7 +897,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
     const uint32_t items = (uint32_t)(H / 2) * (uint32_t)CR;
     const size_t npx = (size_t)H * W;
     const int tid = threadIdx.x;
-    const uint32_t total = (uint32_t)nchunks * (uint32_t)B;
+    const uint32_t total = 8u * (uint32_t)((B + 7) / 8) * (uint32_t)nchunks;
     int cmax = nchunks - 1;
     if (INPLACE) {   // chunk-major slots: nothing past the last chunk any slice needs
         if (tid == 0) s_cmax = -1;
@@ -895,9 +912,10 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
         cmax = s_cmax;
     }
     for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
-        const int b = INPLACE ? (int)(v % (uint32_t)B) : (int)(v / (uint32_t)nchunks);
-        const int j = INPLACE ? (int)(v / (uint32_t)B) : (int)(v % (uint32_t)nchunks);
-        if (j > cmax) return;                           // in place: slots only grow
+        int b, j;
+        const bool valid = pee_slot(v, B, nchunks, INPLACE, &b, &j);
+        if (j > cmax) return;                           // in place: a lane's chunks only grow
+        if (!valid) continue;
         const codec_pee_meta* M = meta_all + b;
         const int end = M->end, Tthr = M->T;
         const int cend = end >= 0 ? (end >> 2) / PEE_CHUNK : -1;
@@ -1077,10 +1095,10 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
         HIP_TRY(hipMemsetAsync(meta, 0, (size_t)P->B * sizeof(codec_pee_meta), st));
         if (inplace) HIP_TRY(hipMemsetAsync(lm, 0, (size_t)P->B * P->lm_words * 8, st));
         ProfScope prof(st, CODEC_K_PEE_EMBED1);
-        const long long total = (long long)L.nchunks * P->B;
+        const long long total = 8LL * ((P->B + 7) / 8) * L.nchunks;
         long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));
         if (g > total) g = total;
-        if (g < 1) g = 1;
+        g = (g + 7) / 8 * 8;   // keep every workgroup on one slot lane (pee_slot)
 #define PE1(TT, NTV, IP) hipLaunchKernelGGL((k_pee_embed1<TT, NTV, IP>), dim3((unsigned)g), dim3(256), 0, st, \
             static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, \
             reinterpret_cast<const u64*>(payload), P->payload_words, L.nchunks, P->B, stw, ctl, meta, \
@@ -1170,10 +1188,10 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
         uint32_t* ctl = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.ctl);
         HIP_TRY(hipMemsetAsync(stw, 0, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4, st));
         ProfScope prof(st, CODEC_K_PEE_EXTRACT1);
-        const long long total = (long long)L.nchunks * P->B;
+        const long long total = 8LL * ((P->B + 7) / 8) * L.nchunks;
         long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));
         if (g > total) g = total;
-        if (g < 1) g = 1;
+        g = (g + 7) / 8 * 8;
 #define PX1(TT, NTV, IP) hipLaunchKernelGGL((k_pee_extract1<TT, NTV, IP>), dim3((unsigned)g), dim3(256), 0, st, \
             static_cast<const TT*>(stego), static_cast<TT*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm), \
             P->lm_words, L.nchunks, P->B, stw, ctl, reinterpret_cast<u64*>(payload_out), P->payload_words)
