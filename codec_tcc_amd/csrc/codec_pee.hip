@@ -724,13 +724,15 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                     lb_store(st + cc, LB_INC | (u64)L);
                     cc |= 0x80000000u;
                 }
-            } else if (ld_agent(ctl) >= (uint32_t)B) {
-                cc = PEE_STOP;
-            } else if (!ld_agent(tick + 1)) {
+            } else {
+                // the two flag loads and the ticket go out together (one round trip); a ticket
+                // taken for a finished slice is published as "prefix >= L" and skipped
+                const uint32_t nd = ld_agent(ctl);
+                const uint32_t dn = ld_agent(tick + 1);
                 cc = atomicAdd(tick, 1u);
-                if (cc < (uint32_t)nchunks && ld_agent(tick + 1)) {   // finished meanwhile: "prefix >= L"
-                    lb_store(st + cc, LB_INC | (u64)L);
-                    cc = PEE_SKIP;
+                if (nd >= (uint32_t)B || dn) {
+                    if (cc < (uint32_t)nchunks) lb_store(st + cc, LB_INC | (u64)L);
+                    cc = nd >= (uint32_t)B ? PEE_STOP : PEE_SKIP;
                 }
             }
             s_v = cc;
@@ -924,13 +926,15 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
         T* dst = cover + b * npx;
         V a0[4], a1[4];
         size_t o0[4];
-        pee_load_chunk<T, NT>(src, W, CR, items, j, a0, a1, o0);   // past `end`: plain copy of chunk j
+        // out of place chunk j is loaded while the ticket is in flight (a plain copy when past
+        // `end`); in place only the ticketed chunk is read
+        if (!INPLACE) pee_load_chunk<T, NT>(src, W, CR, items, j, a0, a1, o0);
         int c = j;
-        if (j <= cend) {   // exactly cend+1 slots take tickets 0..cend (almost always c == j)
+        if (j <= cend) {   // exactly cend+1 slots take tickets 0..cend
             if (tid == 0) s_v = atomicAdd(ctl + 32 + 32 * (size_t)b, 1u);
             __syncthreads();
             c = (int)s_v;
-            if (c != j) pee_load_chunk<T, NT>(src, W, CR, items, c, a0, a1, o0);
+            if (INPLACE || c != j) pee_load_chunk<T, NT>(src, W, CR, items, c, a0, a1, o0);
         }
         if (c <= cend) {
             const u64* lm = lm_all + (size_t)b * lmw;
