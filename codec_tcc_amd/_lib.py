@@ -89,7 +89,8 @@ _SIGS = {
 KERNEL_TAGS = {1: "k_scan_fast", 2: "k_scan_generic", 3: "k_block_exact", 4: "k_decide",
                5: "k_embed", 6: "k_restore", 7: "k_gather", 8: "other", 9: "k_pee_scan", 10: "k_pee_locate",
                11: "k_pee_embed", 12: "k_pee_copy", 13: "k_pee_dcount", 14: "k_pee_recover",
-               15: "k_pee_embed1", 16: "k_pee_extract1", 17: "k_scan_read", 18: "k_unxor"}
+               15: "k_pee_embed1", 16: "k_pee_extract1", 17: "k_scan_read", 18: "k_unxor",
+               19: "k_scan_rows", 20: "k_scan_rows_read"}
 EXPORTS = tuple(_SIGS)
 
 _lib = None

@@ -427,6 +427,188 @@ __global__ __launch_bounds__(1024) void k_scan_read(const T* __restrict__ cover,
     scan_fast_body<T, SB, true, true>(cover, nullptr, H, W, bands_per_wg, ghist_all, gkey, gor);
 }
 
+// ------------------------------------------------------------------ K1 (row-major): scan + copy
+// Same outputs as k_scan_fast, different sweep: a workgroup owns whole SB-row bands of one
+// slice (one contiguous region) and streams it in flat order, 4096 16-B vectors (64 KiB of
+// uint16) per iteration, vector u*1024+t of the iteration to thread t.  Measured on the
+// MI355X (tools/ubench_stagger.hip): this flat per-region order copies at 6.2 TB/s where
+// the column-band order of k_scan_fast tops out at 5.8 TB/s.  Block LSB counts no longer
+// stay in one thread's registers, so they go to packed 16-bit LDS counters (one per full
+// block of the region, pre-combined across the SB/8 lanes of a block row when W % SB == 0)
+// and are turned into argmax keys once the region is done.
+#define SCAN_ROWS_CNT_WORDS 7168   // 28 KiB of LDS = 14 336 block counters per workgroup
+// DIAG (timing diagnostics only, decisions are wrong): 1 = no histogram adds, 4 = copy with
+// the sweep's bookkeeping only, 5 = bare region copy (tools/ubench_stagger.hip's loop)
+template <typename T, int SB, bool NT, bool STORE, int DIAG = 0, bool PIPE = true>
+__device__ __forceinline__ void scan_rows_body(const T* __restrict__ cover, T* __restrict__ stego,
+                                               int H, int W, int bands_per_wg,
+                                               uint32_t* __restrict__ ghist_all,
+                                               u64* __restrict__ gkey, uint32_t* __restrict__ gor) {
+    typedef typename Vec8<T>::type V;
+    constexpr int G = SB / 8;                 // lanes (vectors) per block row segment
+    constexpr int LG = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : 3;
+    constexpr int LSB_ = SB == 8 ? 3 : SB == 16 ? 4 : SB == 32 ? 5 : 6;
+    constexpr uint32_t NPB = (uint32_t)SB * SB;
+    constexpr int NT_ = 1024, U = 4;
+    __shared__ uint32_t lds[HistCfg<T>::kLdsWords];
+    __shared__ uint32_t cnt[SCAN_ROWS_CNT_WORDS];
+    __shared__ u64 wkey;
+    const int b = blockIdx.y;
+    const size_t npx = (size_t)H * W;
+    const T* src = cover + (size_t)b * npx;
+    T* dst = STORE ? stego + (size_t)b * npx : nullptr;
+    uint32_t* ghist = ghist_all + (size_t)b * HistCfg<T>::kBins;
+
+    const int CR = W / 8;                                   // vectors per row
+    const int band0 = blockIdx.x * bands_per_wg;
+    const int row0 = band0 * SB;
+    const int row1 = min(H, row0 + bands_per_wg * SB);
+    const int fullbx = W / SB, fullby = H / SB, nbx = (W + SB - 1) / SB;
+    // full blocks of this region: bands [band0, min(band1, fullby)) x [0, fullbx)
+    const int fb1 = min(fullby, band0 + bands_per_wg);
+    const int nfull = max(0, fb1 - band0) * fullbx;        // host guarantees nfull <= 2*CNT_WORDS
+    for (int i = threadIdx.x; i < HistCfg<T>::kLdsWords; i += NT_) lds[i] = 0;
+    for (int i = threadIdx.x; i < (nfull + 1) / 2; i += NT_) cnt[i] = 0;
+    if (threadIdx.x == 0) wkey = 0;
+    __syncthreads();
+
+    const long long nvec = (long long)max(0, row1 - row0) * CR;
+    const V* s = reinterpret_cast<const V*>(src + (size_t)row0 * W);
+    V* d = STORE ? reinterpret_cast<V*>(dst + (size_t)row0 * W) : nullptr;
+    const int lane = threadIdx.x & 63;
+    const bool grouped = (CR % G) == 0;                     // G-lane groups share a block row
+    // (row, column-vector) of this thread's first vector, advanced incrementally
+    const int dq = NT_ / CR, dr = NT_ % CR;                 // one u step = 1024 vectors
+    int r = threadIdx.x / CR, c = threadIdx.x % CR;
+    uint32_t vor = 0;
+    if constexpr (DIAG == 5) {   // the bare region copy of tools/ubench_stagger.hip
+        unsigned acc = 0;
+        for (long long base = threadIdx.x; base + 3 * NT_ < nvec; base += (long long)NT_ * U) {
+            V w[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) w[u] = ldv<NT>(s + base + u * NT_);
+#pragma unroll
+            for (int u = 0; u < U; ++u) { stv<NT>(d + base + u * NT_, w[u]); acc += w[u].x & 1u; }
+        }
+        if (acc == 0xFFFFFFFFu) gor[b] = acc;
+        return;
+    }
+    // one iteration's stores, block counts and histogram adds on 4 loaded vectors
+    auto process = [&](long long base, const V* v, bool whole) {
+        int rr[U], cc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            rr[u] = r; cc[u] = c;
+            c += dr; r += dq;
+            if (c >= CR) { c -= CR; ++r; }
+        }
+        if constexpr (STORE) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const long long i = base + (long long)u * NT_ + threadIdx.x;
+                if (whole || i < nvec) stv<NT>(d + i, v[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long i = base + (long long)u * NT_ + threadIdx.x;
+            const bool ok = whole || i < nvec;
+            uint32_t ones = ok ? lsb_count(v[u]) : 0u;
+            if (ok) vor |= vor_of(v[u]);
+            // block of this vector (row is region-local)
+            const int by = rr[u] >> LSB_, bx = cc[u] >> LG;
+            const bool full = ok && (band0 + by) < fullby && bx < fullbx;
+            if (DIAG == 4) {
+                vor ^= v[u].x;
+                continue;
+            }
+            if (grouped) {
+#pragma unroll
+                for (int o = 1; o < G; o <<= 1) ones += __shfl_xor(ones, o, 64);
+                if (full && (lane & (G - 1)) == 0) {
+                    const int k = by * fullbx + bx;
+                    atomicAdd(&cnt[k >> 1], ones << ((k & 1) * 16));
+                }
+            } else if (full && ones) {
+                const int k = by * fullbx + bx;
+                atomicAdd(&cnt[k >> 1], ones << ((k & 1) * 16));
+            }
+            if (DIAG == 0)
+                if (ok) hist_add8<T>(lds, ghist, v[u]);
+        }
+    };
+    const long long step = (long long)NT_ * U;
+    const long long nwhole = nvec / step * step;   // iterations with every vector in range
+    if constexpr (PIPE) {
+        // software pipelined: the next iteration's loads are issued before this iteration's
+        // stores and histogram adds
+        V v[U], vn[U];
+        if (nwhole > 0) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = ldv<NT>(s + (long long)u * NT_ + threadIdx.x);
+        }
+        for (long long base = 0; base < nwhole; base += step) {
+            if (base + step < nwhole) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) vn[u] = ldv<NT>(s + base + step + (long long)u * NT_ + threadIdx.x);
+            }
+            process(base, v, true);
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = vn[u];
+        }
+    } else {
+        for (long long base = 0; base < nwhole; base += step) {
+            V v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = ldv<NT>(s + base + (long long)u * NT_ + threadIdx.x);
+            process(base, v, true);
+        }
+    }
+    if (nwhole < nvec) {   // ragged last iteration
+        V v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long i = nwhole + (long long)u * NT_ + threadIdx.x;
+            if (i < nvec) v[u] = ldv<NT>(s + i);
+        }
+        process(nwhole, v, false);
+    }
+    if constexpr (sizeof(T) == 2) vor = (vor | (vor >> 16)) & 0xFFFFu;
+    else vor = (vor | (vor >> 8) | (vor >> 16) | (vor >> 24)) & 0xFFu;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) vor |= __shfl_xor(vor, o, 64);
+    if (lane == 0 && vor) atomicOr(&gor[b], vor);
+    __syncthreads();
+    // block keys: score c(n-c) (exact variance numerator of a full pow2 block), first
+    // maximal block in raster order wins (~index in the low word)
+    u64 best = 0;
+    for (int k = threadIdx.x; k < nfull; k += NT_) {
+        const uint32_t ones = (cnt[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+        const uint32_t score = ones * (NPB - ones);
+        const int by = k / fullbx, bx = k - by * fullbx;
+        const uint32_t idx = (uint32_t)(band0 + by) * nbx + (uint32_t)bx;
+        const u64 key = ((u64)score << 32) | (u64)(0xFFFFFFFFu - idx);
+        best = best > key ? best : key;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const u64 other = __shfl_xor(best, o, 64);
+        best = best > other ? best : other;
+    }
+    if (lane == 0 && best) atomicMax(&wkey, best);
+    if (DIAG == 0) hist_flush<T>(lds, ghist);
+    __syncthreads();
+    if (threadIdx.x == 0 && wkey) atomicMax(&gkey[b], wkey);
+}
+
+template <typename T, int SB, bool NT, bool STORE, int DIAG = 0, bool PIPE = true>
+__global__ __launch_bounds__(1024) void k_scan_rows(const T* __restrict__ cover, T* __restrict__ stego,
+                                                    int H, int W, int bands_per_wg,
+                                                    uint32_t* __restrict__ ghist_all,
+                                                    u64* __restrict__ gkey, uint32_t* __restrict__ gor) {
+    scan_rows_body<T, SB, NT, STORE, DIAG, PIPE>(cover, stego, H, W, bands_per_wg, ghist_all, gkey, gor);
+}
+
 // ------------------------------------------------------------------ K1': scan + copy (generic)
 // Any W, any block size, dtype conversion / plane masking (nbits != dtype bits).
 template <typename Tin, typename Tout>
@@ -707,6 +889,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     int offset = 0;
     if (P.fixed_offset >= 0) offset = P.fixed_offset;
     else if (P.mode == CODEC_MODE_HYBRID) offset = (bix / nbx) * sb * P.W + (bix % nbx) * sb;
+    if (offset < 0 || (long long)offset >= npx) offset = 0;   // no block scored (never for valid stats)
 
     // ---- segment windows (codec.py:455-485 / 288-316)
     const codec_layout& L = table[(size_t)slice_class[b] * 16 + (s - 1)];
@@ -1377,6 +1560,44 @@ static int launch_scan_fast(const codec_params* P, const void* cover, void* steg
     dim3 grid(wgps, P->B);
     const T* c = static_cast<const T*>(cover);
     T* s = static_cast<T*>(stego);
+    // the row sweep needs one band's full blocks to fit its LDS counters; wider images
+    // (e.g. a flattened 1 x N view) take the column-band sweep
+    // Measured (tools/tune.py): the row sweep wins for the copying scan (0.77 vs 0.80-0.83
+    // ms at 256 x 2048^2), the column-band sweep for the read-only scan, which is bound by
+    // LDS atomic throughput (0.54 vs 0.61 ms: concurrent waves of one band hit the same bins)
+    const long long kind = s ? knob("CODEC_SCAN_KIND", 1) : knob("CODEC_SCAN_READ_KIND", 0);
+    if (kind == 1 && P->W / sb <= 2 * SCAN_ROWS_CNT_WORDS) {
+        // row-major sweep: bands per workgroup from CODEC_SCAN_ROWS_WGS, capped by the LDS
+        // block-counter capacity
+        const int fullbx = P->W / sb;
+        const int rtarget = s ? (int)knob("CODEC_SCAN_ROWS_WGS", 1024) : (int)knob("CODEC_SCAN_ROWS_READ_WGS", 1024);
+        int rw = (rtarget + P->B - 1) / P->B;
+        rw = rw < 1 ? 1 : (rw > nb ? nb : rw);
+        int rb = (nb + rw - 1) / rw;
+        const int cap = 2 * SCAN_ROWS_CNT_WORDS;
+        if (fullbx > 0 && rb * fullbx > cap) rb = cap / fullbx;
+        rw = (nb + rb - 1) / rb;
+        dim3 g2(rw, P->B);
+#define ROWS(SBV, ST)                                                                                   \
+        hipLaunchKernelGGL((k_scan_rows<T, SBV, true, ST>), g2, dim3(1024), 0, st, c, s, P->H, P->W, rb, hist, keys, orv)
+        if (!s) {
+            ProfScope prof(st, CODEC_K_SCAN_ROWS_READ);
+            switch (sb) { case 8: ROWS(8, false); break; case 16: ROWS(16, false); break;
+                          case 32: ROWS(32, false); break; default: ROWS(64, false); break; }
+            LAUNCH_CHECK("k_scan_rows(read)");
+        } else {
+            ProfScope prof(st, CODEC_K_SCAN_ROWS);
+            const int diag = (int)knob("CODEC_DIAG_ROWS", 0);   // timing diagnostics only: s is wrong
+            if (sb == 16 && diag == 1) hipLaunchKernelGGL((k_scan_rows<T, 16, true, true, 1>), g2, dim3(1024), 0, st, c, s, P->H, P->W, rb, hist, keys, orv);
+            else if (sb == 16 && diag == 4) hipLaunchKernelGGL((k_scan_rows<T, 16, true, true, 4>), g2, dim3(1024), 0, st, c, s, P->H, P->W, rb, hist, keys, orv);
+            else if (sb == 16 && diag == 5) hipLaunchKernelGGL((k_scan_rows<T, 16, true, true, 5>), g2, dim3(1024), 0, st, c, s, P->H, P->W, rb, hist, keys, orv);
+            else switch (sb) { case 8: ROWS(8, true); break; case 16: ROWS(16, true); break;
+                          case 32: ROWS(32, true); break; default: ROWS(64, true); break; }
+            LAUNCH_CHECK("k_scan_rows");
+        }
+#undef ROWS
+        return 0;
+    }
     if (!s) {
         ProfScope prof(st, CODEC_K_SCAN_READ);
         switch (sb) {

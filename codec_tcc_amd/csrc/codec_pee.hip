@@ -114,51 +114,68 @@ struct Quad {
 };
 
 // ---- scan: stream copy + per-tile count of expandable non-overflow candidates (W % 8 == 0)
+// One wave per tile (256 items = 1024 candidates; 4 items per lane, two 16-B rows each, all
+// 8 loads issued up front), tiles swept grid-stride over the whole batch in address order
+// (global tile g = slice * ntiles + t), so the resident waves read one moving window of
+// HBM; the wave's shuffle reduction writes the tile count directly (no LDS, no barrier).
 template <typename T, bool NT>
 __global__ __launch_bounds__(256) void k_pee_scan(const T* __restrict__ cover, T* __restrict__ stego, int H, int W,
-                                                  int Tthr, int maxval, int tiles_per_wg,
-                                                  uint32_t* __restrict__ tile_cnt_all, int ntiles_max) {
+                                                  int Tthr, int maxval, uint32_t* __restrict__ tile_cnt_all,
+                                                  int ntiles_max, int B) {
     typedef typename Vec8<T>::type V;
-    __shared__ uint32_t sh[8];
-    const int b = blockIdx.y;
     const size_t npx = (size_t)H * W;
-    const T* src = cover + b * npx;
-    T* dst = stego + b * npx;
     const int CR = W / 8, hc = H / 2;
-    const long long items = (long long)hc * CR;
-    const int ntiles = (int)((items + 255) / 256);
-    uint32_t* tile_cnt = tile_cnt_all + (size_t)b * ntiles_max;
-    const int t0 = blockIdx.x * tiles_per_wg;
-    const int t1 = min(ntiles, t0 + tiles_per_wg);
-    for (int t = t0; t < t1; ++t) {
-        const long long it = (long long)t * 256 + threadIdx.x;
-        uint32_t cnt = 0;
-        if (it < items) {
-            const int r = (int)(it / CR), c = (int)(it - (long long)r * CR);
-            const size_t o0 = (size_t)(2 * r) * W + (size_t)c * 8, o1 = o0 + W;
-            const V v0 = ldv<NT>(reinterpret_cast<const V*>(src + o0));
-            const V v1 = ldv<NT>(reinterpret_cast<const V*>(src + o1));
-            stv<NT>(reinterpret_cast<V*>(dst + o0), v0);
-            stv<NT>(reinterpret_cast<V*>(dst + o1), v1);
+    const uint32_t items = (uint32_t)hc * (uint32_t)CR;
+    const uint32_t ntiles = (items + 255u) / 256u;
+    const uint32_t total = ntiles * (uint32_t)B;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wstride = gridDim.x * 4u;
+    for (uint32_t g = blockIdx.x * 4u + (threadIdx.x >> 6); g < total; g += wstride) {
+        const uint32_t b = g / ntiles, t = g - b * ntiles;
+        const T* src = cover + b * npx;
+        T* dst = stego + b * npx;
+        V v0[4], v1[4];
+        size_t o0[4];
+        bool ok[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t it = t * 256u + (uint32_t)(u * 64 + lane);
+            ok[u] = it < items;
+            const uint32_t r = it / (uint32_t)CR, c = it - r * (uint32_t)CR;
+            o0[u] = (size_t)(2 * r) * W + (size_t)c * 8;
+            if (ok[u]) {
+                v0[u] = ldv<NT>(reinterpret_cast<const V*>(src + o0[u]));
+                v1[u] = ldv<NT>(reinterpret_cast<const V*>(src + o0[u] + W));
+            }
+        }
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (!ok[u]) continue;
+            stv<NT>(reinterpret_cast<V*>(dst + o0[u]), v0[u]);
+            stv<NT>(reinterpret_cast<V*>(dst + o0[u] + W), v1[u]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
                 int x, a, bb, cc;
                 if constexpr (sizeof(T) == 2) {
-                    x = (int)px16(v1, 2 * u + 1); a = (int)px16(v1, 2 * u); bb = (int)px16(v0, 2 * u + 1); cc = (int)px16(v0, 2 * u);
+                    x = (int)px16(v1[u], 2 * k + 1); a = (int)px16(v1[u], 2 * k); bb = (int)px16(v0[u], 2 * k + 1); cc = (int)px16(v0[u], 2 * k);
                 } else {
-                    x = (int)px8(v1, 2 * u + 1); a = (int)px8(v1, 2 * u); bb = (int)px8(v0, 2 * u + 1); cc = (int)px8(v0, 2 * u);
+                    x = (int)px8(v1[u], 2 * k + 1); a = (int)px8(v1[u], 2 * k); bb = (int)px8(v0[u], 2 * k + 1); cc = (int)px8(v0[u], 2 * k);
                 }
                 const PeeCand pc = pee_classify(x, a, bb, cc, Tthr, maxval);
                 cnt += (pc.expand && pc.safe) ? 1u : 0u;
             }
         }
-        const uint32_t tot = block_sum_u32<256>(cnt, sh);
-        if (threadIdx.x == 0) tile_cnt[t] = tot;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+        if (lane == 0) tile_cnt_all[(size_t)b * ntiles_max + t] = cnt;
     }
-    // odd H: the last row belongs to no row pair; copy it
-    if ((H & 1) && blockIdx.x == gridDim.x - 1) {
-        const size_t o = (size_t)(H - 1) * W;
-        for (int q = threadIdx.x; q < W; q += 256) dst[o + q] = src[o + q];
+    // odd H: the last row of each slice belongs to no row pair; copy it
+    if (H & 1) {
+        for (int b = blockIdx.x; b < B; b += gridDim.x) {
+            const size_t o = (size_t)b * npx + (size_t)(H - 1) * W;
+            for (int q = threadIdx.x; q < W; q += 256) stego[o + q] = cover[o + q];
+        }
     }
 }
 
@@ -1127,7 +1144,11 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
         if (per < 1) per = 1;
         dim3 grid((ntiles + per - 1) / per, P->B);
         if (vec) {
-#define PSCAN(TT, NTV) hipLaunchKernelGGL((k_pee_scan<TT, NTV>), grid, dim3(256), 0, st, static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, per, cnt, L.ntiles_max)
+            const long long tot = (long long)ntiles * P->B;
+            long long gw = knob("CODEC_PEE_SCAN_GS_WGS", 32768);   // tools/tune_pee.py
+            if (gw > (tot + 3) / 4) gw = (tot + 3) / 4;
+            if (gw < 1) gw = 1;
+#define PSCAN(TT, NTV) hipLaunchKernelGGL((k_pee_scan<TT, NTV>), dim3((unsigned)gw), dim3(256), 0, st, static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, cnt, L.ntiles_max, P->B)
             if (P->bytes == 2) { if (nt) PSCAN(uint16_t, true); else PSCAN(uint16_t, false); }
             else { if (nt) PSCAN(uint8_t, true); else PSCAN(uint8_t, false); }
 #undef PSCAN

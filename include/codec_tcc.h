@@ -231,6 +231,8 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
 #define CODEC_K_PEE_EXTRACT1 16
 #define CODEC_K_SCAN_READ 17
 #define CODEC_K_UNXOR 18
+#define CODEC_K_SCAN_ROWS 19
+#define CODEC_K_SCAN_ROWS_READ 20
 int codec_profile_begin(int32_t capacity);
 /* after the stream has been synchronised: fills ms[i], tag[i] for the recorded pairs and
  * returns their count (closes the window and frees the events). */

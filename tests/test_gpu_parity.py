@@ -193,3 +193,37 @@ def test_inplace_batch_roundtrip(kind, h, w, bsz, mode):
     ref_words, _ = codec.decode(ref.stego, ref.maps, ref.meta, payload_words=pw, map_words=mw)
     np.testing.assert_array_equal(words.cpu().numpy(), ref_words.cpu().numpy())
     np.testing.assert_array_equal(buf.cpu().numpy(), covers)
+
+
+SWEEPS = [("0", None), ("1", None), ("1", "1"), ("1", "7"), ("1", "100000")]
+
+
+@pytest.mark.parametrize("kind,h,w,sb", [("ct12", 512, 512, 16), ("ct12", 200, 136, 16), ("u16", 96, 264, 8),
+                                         ("u8", 130, 72, 32), ("ct12", 256, 192, 64), ("u16", 64, 2048, 16)])
+@pytest.mark.parametrize("sweep,wgs", SWEEPS, ids=[f"kind{a}-wgs{b}" for a, b in SWEEPS])
+def test_scan_sweeps_agree_with_oracle(monkeypatch, kind, h, w, sb, sweep, wgs):
+    """Both scan sweeps (column-band k_scan_fast, row-major k_scan_rows) at several
+    workgroup-region sizes (whole slice per workgroup ... one band per workgroup) give the
+    oracle's s, start offset and stego, including ragged last bands, W % SB != 0 (no lane
+    grouping of block counts) and partial last iterations."""
+    monkeypatch.setenv("CODEC_SCAN_KIND", sweep)
+    monkeypatch.setenv("CODEC_SCAN_READ_KIND", sweep)
+    if wgs is not None:
+        monkeypatch.setenv("CODEC_SCAN_ROWS_WGS", wgs)
+    gen = synth.GENERATORS[kind]
+    bsz = 3
+    covers = np.stack([gen(h, w, 500 + i) for i in range(bsz)])
+    msgs = [synth.payload(90 + 31 * i, 40 + i) for i in range(bsz)]
+    codec = Codec(bsz, h, w, dtype=str(covers.dtype), beta=0.4, block=sb)
+    enc = codec.encode(torch.from_numpy(covers).cuda(), msgs)
+    stego = enc.stego.cpu().numpy()
+    recs = enc.records()
+    for i in range(bsz):
+        exp = R.encode_slice(covers[i], R.message_to_bits(msgs[i]), beta=0.4, sb=sb)
+        assert recs[i].s == exp["s"]
+        assert recs[i].start_offset == exp["start_offset"]
+        np.testing.assert_array_equal(stego[i], exp["stego"])
+    buf = torch.from_numpy(covers.copy()).cuda()          # read-only sweep (in place)
+    enc2 = codec.encode(buf, msgs, stego=buf)
+    np.testing.assert_array_equal(buf.cpu().numpy(), stego)
+    assert [r.start_offset for r in enc2.records()] == [r.start_offset for r in recs]

@@ -7,7 +7,7 @@ STAGES="${*:-tests bench prof}"
 has() { [[ " $STAGES " == *" $1 "* ]]; }
 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo build failed; tail gpurun_out/build.log; exit 3; }
 if has tests; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q --maxfail=8 -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q --maxfail=8 -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
   echo "pytest rc=$rc"; tail -25 gpurun_out/pytest_gpu.log
   [ $rc -le 1 ] || exit $rc
 fi

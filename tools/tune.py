@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--configs", default="")
+    ap.add_argument("--inplace", action="store_true", help="stego is cover, cover_out is stego")
     a = ap.parse_args()
     import torch
 
@@ -56,9 +57,21 @@ def main():
         codec.decode(stego, maps, meta, payload_words=pl.payload_words, map_words=pl.map_words, cover=cov2,
                      payload=pay)
 
+    if a.inplace:
+        work = covers.clone()
+
+        def step():   # noqa: F811
+            codec.encode(work, pl, stego=work, maps=maps, meta=meta)
+            codec.decode(work, maps, meta, payload_words=pl.payload_words, map_words=pl.map_words, cover=work,
+                         payload=pay)
+        cov2 = work
+
     res = {i: {} for i in range(len(configs))}
+    keys = {k for cfg in configs for k in cfg}
     for _r in range(a.rounds):
         for i, cfg in enumerate(configs):
+            for k in keys:          # a key absent from this config falls back to the default
+                os.environ.pop(k, None)
             os.environ.update(cfg)
             step()
             torch.cuda.synchronize()
