@@ -247,6 +247,27 @@ def bench_pee(args, torch, dist, world, dev, covers, B, H, W, inplace=False):
     return res
 
 
+def bench_quality(args, torch, covers, stego, B, H, W):
+    """Stego quality of the LSB leg's output (reference src/mse.py metrics): one read-only
+    pass over cover + stego (k_quality), metrics from exact moments on the host."""
+    from codec_tcc_amd import _lib
+    from codec_tcc_amd import quality as Q
+    q = Q.quality(covers, stego)
+    torch.cuda.synchronize()
+    kern = _profile(_lib.load(), _lib, lambda: Q.moments(covers, stego), 5) if not args.no_profile else {}
+    res = {"psnr_db_mean": round(float(np.mean([r["psnr"] for r in q])), 3),
+           "ssim_min": float(min(r["ssim"] for r in q)),
+           "pixels_changed_mean": float(np.mean([r["pixels_diferentes"] for r in q])),
+           "kernels_ms": {k: round(v, 4) for k, v in kern.items()}}
+    if "k_quality" in kern:
+        by = B * H * W * 4                                # read cover + read stego (uint16)
+        t_k = kern["k_quality"] / 1e3
+        res["roofline"] = {"bound": "hbm", "kernel": "k_quality", "achieved": round(by / t_k / 1e9, 1),
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(by / t_k / 1e9 / HBM_PEAK_GBS, 4),
+                           "algorithmic_bytes_per_launch": by}
+    return res
+
+
 def main():
     args = parse()
     import torch
@@ -329,6 +350,7 @@ def main():
         for i in range(max(n, 0)):
             kernels.setdefault(_lib.KERNEL_TAGS.get(tags[i], str(tags[i])), []).append(ms[i])
 
+    quality = bench_quality(args, torch, covers, stego, B, H, W) if rank == 0 else None
     lsb_inplace = bench_lsb_inplace(args, torch, dist, world, dev, covers, codec, pl, B, H, W)
     pee = None
     if args.pee:
@@ -373,6 +395,7 @@ def main():
             "roundtrip_ok": ok,
         }
         out["inplace"] = lsb_inplace
+        out["quality"] = quality
         if pee is not None:
             out["pee"] = pee
         if args.cpu_seconds > 0 and world == 1:

@@ -15,7 +15,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-SRCS = [os.path.join(HERE, "csrc", "codec_hip.hip"), os.path.join(HERE, "csrc", "codec_pee.hip")]
+SRCS = [os.path.join(HERE, "csrc", "codec_hip.hip"), os.path.join(HERE, "csrc", "codec_pee.hip"),
+        os.path.join(HERE, "csrc", "codec_quality.hip")]
 HDRS = [os.path.join(HERE, "csrc", "codec_common.h")]
 OUT = os.path.join(HERE, "libcodec_hip.so")
 INC = os.path.join(REPO, "include")

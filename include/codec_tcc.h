@@ -210,6 +210,17 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
                       const uint64_t* lm, void* cover_out, uint64_t* payload_out, void* workspace,
                       size_t workspace_bytes, void* stream);
 
+/* ---- stego quality (replaces the metric arithmetic of src/mse.py: AnalisadorMSE.
+ * calcular_mse :74-117, calcular_psnr :119-133, calcular_ssim_simples :135-177 and the
+ * difference statistics of analisar_par_imagens :201-207).  One read-only pass over two
+ * [B][H][W] images of `bytes` (1 or 2) per pixel writes per slice 10 exact uint64
+ * moments out[B][10] = {sum a, sum b, sum a^2, sum b^2, sum a*b, sum |a-b|, max |a-b|,
+ * count(a != b), max a, max b}; the metrics are closed forms of them
+ * (codec_tcc_amd/quality.py evaluates them in exact rational arithmetic). */
+#define CODEC_QUALITY_WORDS 10
+int codec_quality_moments(int32_t B, int32_t H, int32_t W, int32_t bytes, const void* a, const void* b,
+                          uint64_t* out, void* stream);
+
 /* ---- measurement hooks (bench.py): while a profile window is open, every launcher
  * records a hipEvent pair around each kernel it launches, tagged with a CODEC_K_* id.
  * Events are created/destroyed here, outside any launch function. */
@@ -233,6 +244,7 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
 #define CODEC_K_UNXOR 18
 #define CODEC_K_SCAN_ROWS 19
 #define CODEC_K_SCAN_ROWS_READ 20
+#define CODEC_K_QUALITY 21
 int codec_profile_begin(int32_t capacity);
 /* after the stream has been synchronised: fills ms[i], tag[i] for the recorded pairs and
  * returns their count (closes the window and frees the events). */

@@ -61,3 +61,20 @@ def decoded(case):
 
 def message(case):
     return case["msg_utf8"].tobytes().decode("utf-8") if "msg_utf8" in case else None
+
+
+def quality_cases():
+    """Stego-quality golden cases (make_quality_golden.py): dicts with a, b and the
+    reference's array-mode [mse, max_range, psnr, ssim] and file-mode
+    [mse, psnr, ssim, diferenca_media, diferenca_max, percentual_mudanca]."""
+    d = _load("quality.npz")
+    lsb = {c["name"]: c for c in cases() if c["name"] in ("pe_b0.4_1k", "torax_b0.4_1k")}
+    out = []
+    for n in d["names"]:
+        n = str(n)
+        if n in lsb:
+            a, b = lsb[n]["cover"], stego(lsb[n])
+        else:
+            a, b = d[f"{n}__a"], d[f"{n}__b"]
+        out.append({"name": n, "a": a, "b": b, "arr": d[f"{n}__arr"], "file": d[f"{n}__file"]})
+    return out
