@@ -63,7 +63,11 @@ def test_oracle_truncates_on_overflow():
 # "1" forces it everywhere, "0" forces the two-pass scan/locate/embed path; small
 # persistent grids exercise the slot loop
 PATHS = {"auto": {}, "onepass": {"CODEC_PEE_ONEPASS": "1"}, "twopass": {"CODEC_PEE_ONEPASS": "0"},
-         "onepass_small_grid": {"CODEC_PEE_ONEPASS": "1", "CODEC_PEE_1P_WGS": "7", "CODEC_PEE_IP_WGS": "3"}}
+         "onepass_small_grid": {"CODEC_PEE_ONEPASS": "1", "CODEC_PEE_1P_WGS": "7", "CODEC_PEE_IP_WGS": "3"},
+         # decode-side tile counts: workgroup-per-tile (block sums) instead of wave-per-tile,
+         # and wave-per-tile with one workgroup per slice (every wave strides over tiles)
+         "twopass_block_tiles": {"CODEC_PEE_ONEPASS": "0", "CODEC_PEE_WAVE_TILES": "0"},
+         "twopass_wave_tiles_1wg": {"CODEC_PEE_ONEPASS": "0", "CODEC_PEE_DCOUNT_W_WGS": "1"}}
 
 
 @pytest.fixture(params=sorted(PATHS))
@@ -101,7 +105,7 @@ def test_gpu_matches_oracle(kind, h, w, bsz, T, inplace, pee_path):
         st, side = P.pee_embed(covers[i], payloads[i], T)
         assert recs[i].status == 0 and recs[i].end == side["end"]
         if recs[i].flags & _lib.PEE_PARTIAL:
-            assert pee_path != "twopass" and side["L"] <= recs[i].capacity <= side["capacity"]
+            assert not pee_path.startswith("twopass") and side["L"] <= recs[i].capacity <= side["capacity"]
         else:
             assert recs[i].capacity == side["capacity"]
         np.testing.assert_array_equal(stego[i], st)
