@@ -109,6 +109,43 @@ __device__ __forceinline__ int np_node_size(int r, int d, int j, int* start) {
     return n;
 }
 
+// np.sum semantics over any m, computed by ONE wave (no block barrier), so that 16 waves
+// can sum 16 different orders at once.  Per 8192-element buffer: the chunk's depth-7 tree
+// has 128 bottom slots, two per lane (slots lane and lane+64); a slot's leaf (numpy's
+// 8-accumulator loop) is summed serially by its lane, then internal nodes are re-added
+// bottom-up with shuffles (node (d, j) lives in lane j).  Buffer sums are added serially.
+// Result valid in every lane.
+template <class F>
+__device__ __forceinline__ double np_sum_wave(const F& f, int m) {
+    const int lane = threadIdx.x & 63;
+    double res = -0.0;
+    for (int cs = 0; cs < m; cs += NP_CHUNK) {
+        const int r = min(NP_CHUNK, m - cs);
+        int aA, aB;
+        const int nA = np_node_size(r, 7, lane, &aA);
+        const int nB = np_node_size(r, 7, lane + 64, &aB);
+        const double vA = nA > 0 ? np_leaf(f, cs + aA, nA) : 0.0;
+        const double vB = nB > 0 ? np_leaf(f, cs + aB, nB) : 0.0;
+        // level 6: node j (lane j) = slots 2j, 2j+1 (lanes 2j, 2j+1 of vA for j < 32, of vB above)
+        const int s0 = (2 * lane) & 63;
+        const double lA = __shfl(vA, s0, 64), rA = __shfl(vA, s0 + 1, 64);
+        const double lB = __shfl(vB, s0, 64), rB = __shfl(vB, s0 + 1, 64);
+        int a6;
+        const int n6 = np_node_size(r, 6, lane, &a6);
+        const double L6 = lane < 32 ? lA : lB, R6 = lane < 32 ? rA : rB;
+        double v = n6 > NP_LEAF ? L6 + R6 : L6;
+        for (int d = 5; d >= 0; --d) {
+            const double L = __shfl(v, (2 * lane) & 63, 64);
+            const double R = __shfl(v, (2 * lane + 1) & 63, 64);
+            int ad;
+            const int nd = np_node_size(r, d, lane, &ad);
+            v = nd > NP_LEAF ? L + R : L;
+        }
+        res += __shfl(v, 0, 64);
+    }
+    return res;
+}
+
 // np.sum semantics over m <= 65536 elements, computed by a 1024-thread block.
 // Slot t = (chunk t/128, bottom slot t%128 of that chunk's depth-7 tree); leaves reached
 // above depth 7 are carried down the left spine.  Leaves are summed wave-cooperatively:
@@ -698,6 +735,15 @@ struct ListTerm {
     __device__ __forceinline__ double operator()(int k) const { return terms[list[k]]; }
 };
 
+#ifdef DECIDE_TS   // diagnostic build only (tools/decide_phases.py): phase timestamps into the term scratch
+#define DTS(k) do { if (threadIdx.x == 0) reinterpret_cast<long long*>(gterms + (size_t)blockIdx.x * HistCfg<T>::kBins)[HistCfg<T>::kBins - 8 + (k)] = wall_clock64(); } while (0)
+#else
+#define DTS(k) do { } while (0)
+#endif
+// CODEC_DECIDE_WAVES=0 (host env, passed in codec_params.reserved bit 0) forces the
+// block-sequential decision path (A/B and tests)
+__device__ __forceinline__ bool knob_dev_decide_fast(const codec_params& P) { return !(P.reserved & 1); }
+
 __device__ __forceinline__ double plogp(const double* lut, uint32_t c, double N) {
     const double p = (double)c / N;       // counts[counts > 0] / size   (codec.py:498)
     return p * lut[c - 1];                // probabilities * np.log2(probabilities)  (:501)
@@ -733,13 +779,17 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
                                                  const int32_t* __restrict__ slice_class,
                                                  codec_slice_meta* __restrict__ meta_all) {
     constexpr int R = HistCfg<T>::kBins;
-    __shared__ uint16_t list[R];
+    // `list` doubles as the wave-parallel path's arena: terms (8m B), rank -> value (2m B),
+    // one joint-order list per plane in flight (2m B each)
+    __shared__ __align__(16) uint16_t list[R];
     __shared__ double vals[1024];
     __shared__ uint32_t sh[20];
     __shared__ uint32_t pops_sh[16];
     __shared__ double mis_sh[16];
     __shared__ double best_sc[16];
     __shared__ int best_ix[16];
+    __shared__ double hxy_sh[16], hx_sh[16], hy_sh;
+    __shared__ int ctl_sh[4];
 
     const int b = blockIdx.x;
     const int t = threadIdx.x;
@@ -749,6 +799,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     const double Nd = (double)npx;
     codec_slice_meta* M = meta_all + b;
 
+    DTS(0);
     // ---- bins that can be non-zero: [0, Rp), Rp = next power of two above OR(pixels)
     const uint32_t orv = gor[b];
     int Rp = orv ? (1 << (32 - __clz((int)orv))) : 1;
@@ -788,7 +839,23 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
         for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
         if ((t & 63) == 0 && x) atomicAdd(&pops_sh[i], x);
     }
+    DTS(1);
     const bool lut_ok = lut_len >= npx;
+    // wave-parallel path (m small enough that terms + per-plane joint orders fit in LDS):
+    // each wave sums one plane's H(X,Y) with np_sum_wave, no block barriers inside a sum
+    // arena: terms (8m B) | rank -> value (2m B) | per 64-rank group, the 16 bit-plane
+    // ballots of its values (128 B) | one joint-order list per plane in flight (2m B)
+    const size_t arena = sizeof(list);
+    const int ngrp = (int)((m + 63) / 64);
+    const size_t off_pm = (10 * (size_t)m + 15) / 16 * 16;
+    const size_t off_jl = off_pm + (size_t)ngrp * 128;
+    const int wplanes = (m > 1 && off_jl + 2 * (size_t)m <= arena) ? (int)min((size_t)16, (arena - off_jl) / (2 * (size_t)m)) : 0;
+    const bool wfast = lut_ok && wplanes >= 1 && knob_dev_decide_fast(P);
+    double* tl = reinterpret_cast<double*>(list);
+    uint16_t* rv = reinterpret_cast<uint16_t*>(tl + (wfast ? m : 0));
+    u64* pm = reinterpret_cast<u64*>(reinterpret_cast<char*>(list) + off_pm);
+    uint16_t* jl = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(list) + off_jl);
+    if (wfast) terms = tl;
     // terms of the non-zero bins in ascending value order, computed once
     if (lut_ok) {
         uint32_t r = rank0;
@@ -810,23 +877,134 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
 #pragma unroll
             for (int u = 0; u < 8; ++u)
                 if (u < k) terms[r + u] = tt[u];
+            if (wfast) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (u < k) rv[r + u] = (uint16_t)vv[u];
+            }
             r += k;
         }
     }
     __syncthreads();
 
+    DTS(2);
     // ---- calculate_entropy (codec.py:489-502) = H(Y) inside calculate_mutual_information
     double Hy = 0.0;
-    if (lut_ok) Hy = -np_sum_block1024(RankTerm{terms}, (int)m, vals);
-    const double target = P.beta * Hy;
-
-    // ---- the s decision (codec.py:580-593)
     int s = 1;
     bool decided = false;
     double cum = 0.0;
     if (t < 16) mis_sh[t] = 0.0;
     const bool need_decision = (P.fixed_s <= 0);
-    for (int i = 0; i < P.nbits && i < 16 && lut_ok; ++i) {
+    if (wfast) {
+        // H(Y) by wave 0; then rounds of `wplanes` planes, plane i0+w on wave w: its joint
+        // bincount order (bit-i-clear bins ascending, then bit-i-set bins, codec.py:546-551)
+        // is written to its own list and summed with np_sum_wave.  Thread 0 then walks the
+        // round's planes in order exactly like the sequential loop (same early exit).
+        const int wv = t >> 6, lane = t & 63;
+        const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+        for (int g = wv; g < ngrp; g += 16) {             // bit-plane ballots per rank group
+            const int r = g * 64 + lane;
+            const uint32_t v = r < (int)m ? rv[r] : 0u;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const u64 bm = __ballot((v >> i) & 1u);
+                if (lane == i) pm[g * 16 + i] = bm;
+            }
+        }
+        __syncthreads();
+        // planes per round: enough for the usual s (5 on 12-bit data, 7 on uniform 16-bit),
+        // few enough that the round's waves are not sharing SIMDs 4 to 1 (each list build and
+        // sum is VALU-issue bound); H(Y) runs on the last wave meanwhile
+        const int rp = min(wplanes, 8);
+        if (wv == 15) {
+            const double h = -np_sum_wave(RankTerm{tl}, (int)m);
+            if (lane == 0) hy_sh = h;
+        }
+        const int nb = min(P.nbits, 16);
+        if (t == 0) ctl_sh[0] = 0;
+        for (int i0 = 0; i0 < nb; i0 += rp) {
+            const int i = i0 + wv;
+            if (wv < rp && i < nb) {
+                const uint32_t pp = pops_sh[i];
+                double hxy = 0.0;
+                if (pp != 0 && (long long)pp != npx) {
+                    // joint order from the group ballots: lane j holds group (blk + j)'s mask and
+                    // the zeros / ones before it; the group loop then only shuffles and stores
+                    uint16_t* L = jl + (size_t)wv * m;
+                    uint32_t ones = 0;
+                    for (int g = lane; g < ngrp; g += 64) ones += (uint32_t)__popcll(pm[g * 16 + i]);
+#pragma unroll
+                    for (int o = 32; o >= 1; o >>= 1) ones += __shfl_xor(ones, o, 64);
+                    uint32_t zbase = 0, obase = (uint32_t)m - ones;      // ones follow all zeros
+                    for (int blk = 0; blk < ngrp; blk += 64) {
+                        const int g = blk + lane;
+                        const u64 mk = g < ngrp ? pm[g * 16 + i] : 0ull;
+                        const int nr = g < ngrp ? min(64, (int)m - g * 64) : 0;   // ranks in group g
+                        const uint32_t oc = (uint32_t)__popcll(mk), zc = (uint32_t)nr - oc;
+                        uint32_t zi = zc, oi = oc;                         // inclusive scans
+#pragma unroll
+                        for (int o = 1; o < 64; o <<= 1) {
+                            const uint32_t zy = __shfl_up(zi, o, 64), oy = __shfl_up(oi, o, 64);
+                            if (lane >= o) { zi += zy; oi += oy; }
+                        }
+                        const uint32_t zx = zi - zc, ox = oi - oc;
+                        const int gend = min(ngrp - blk, 64);
+                        for (int j = 0; j < gend; ++j) {
+                            const u64 mg = __shfl(mk, j, 64);
+                            const uint32_t zb = zbase + __shfl(zx, j, 64);
+                            const uint32_t ob = obase + __shfl(ox, j, 64);
+                            const int r = (blk + j) * 64 + lane;
+                            if (r < (int)m) {
+                                const bool one = (mg >> lane) & 1ull;
+                                L[one ? ob + __popcll(mg & lt) : zb + __popcll(~mg & lt)] = (uint16_t)r;
+                            }
+                        }
+                        zbase += __shfl(zi, 63, 64);
+                        obase += __shfl(oi, 63, 64);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    if (i0 == 0) DTS(7);
+                    hxy = -np_sum_wave(ListTerm{tl, L}, (int)m);
+                    if (i0 == 0) DTS(6);
+                    if (lane == 0) hx_sh[wv] = -(plogp(lut, (uint32_t)(npx - pp), Nd) + plogp(lut, pp, Nd));
+                }
+                if (lane == 0) hxy_sh[wv] = hxy;
+            }
+            __syncthreads();
+            if (t == 0) {
+                Hy = hy_sh;
+                const double target0 = P.beta * Hy;
+                int stop = 0;
+                for (int k = 0; k < rp && i0 + k < nb; ++k) {
+                    const int ii = i0 + k;
+                    if (!(need_decision && !decided) && !P.all_mi) { stop = 1; break; }
+                    const uint32_t pp = pops_sh[ii];
+                    double mi = 0.0;
+                    if (pp != 0 && (long long)pp != npx) {                // codec.py:520-523
+                        mi = (hx_sh[k] + Hy) - hxy_sh[k];                // codec.py:554
+                        if (!(mi > 0.0)) mi = 0.0;
+                    }
+                    mis_sh[ii] = mi;
+                    if (need_decision && !decided) {
+                        cum += mi;
+                        if (cum >= target0) { s = ii + 1; decided = true; }
+                    }
+                }
+                if (!(need_decision && !decided) && !P.all_mi) stop = 1;
+                ctl_sh[0] = stop;
+            }
+            __syncthreads();
+            if (ctl_sh[0]) break;
+        }
+        Hy = hy_sh;
+    }
+    if (lut_ok && !wfast) Hy = -np_sum_block1024(RankTerm{terms}, (int)m, vals);
+    const double target = P.beta * Hy;
+
+    // ---- the s decision (codec.py:580-593)
+    for (int i = 0; i < P.nbits && i < 16 && lut_ok && !wfast; ++i) {
         if (!(need_decision && !decided) && !P.all_mi) break;
         const uint32_t pp = pops_sh[i];
         double mi = 0.0;
@@ -845,6 +1023,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     }
     if (!need_decision) s = P.fixed_s;
 
+    DTS(3);
     // ---- start offset: first maximal float(np.var) block in raster order (codec.py:441-453)
     const int sb = P.block;
     const int nbx = (P.W + sb - 1) / sb;
@@ -885,6 +1064,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
         }
     }
 
+    DTS(4);
     if (t != 0) return;
     int offset = 0;
     if (P.fixed_offset >= 0) offset = P.fixed_offset;
@@ -937,6 +1117,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
         M->span_len = (int)min(len, npx);
     }
     for (int i = 0; i < 16; ++i) M->mi[i] = mis_sh[i];
+    DTS(5);
 }
 
 // ------------------------------------------------------------------ per-slice window cache
@@ -1695,7 +1876,8 @@ int codec_plan(const codec_params* P, const void* cover, void* stego, const doub
                                P->H, P->W, P->block, edge_only, exact, L.exact_cap);
         LAUNCH_CHECK("k_block_exact");
     }
-    const codec_params Pv = *P;
+    codec_params Pv = *P;
+    Pv.reserved = knob("CODEC_DECIDE_WAVES", 1) ? 0 : 1;   // bit 0: force the block-sequential decision
     ProfScope prof(st, CODEC_K_DECIDE);
     if (P->in_bytes == 2)
         hipLaunchKernelGGL(k_decide<uint16_t>, dim3(P->B), dim3(1024), 0, st, Pv, hist, orv, terms, keys, exact, L.exact_cap,

@@ -31,8 +31,17 @@ def _run_case(case):
     return codec, enc
 
 
+@pytest.fixture(params=["waves", "block"])
+def decide_path(request, monkeypatch):
+    """k_decide's wave-parallel MI path (default when the joint orders fit in LDS) and the
+    block-sequential one (CODEC_DECIDE_WAVES=0; also what large-m slices use)."""
+    if request.param == "block":
+        monkeypatch.setenv("CODEC_DECIDE_WAVES", "0")
+    return request.param
+
+
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
-def test_golden_case(case):
+def test_golden_case(case, decide_path):
     codec, enc = _run_case(case)
     m = enc.records()[0]
     s = int(case["s"])
@@ -78,7 +87,7 @@ def test_golden_case(case):
 
 @pytest.mark.parametrize("kind,h,w,bsz", [("ct12", 512, 512, 5), ("u16", 256, 320, 3), ("u8", 200, 96, 4),
                                           ("ct12", 120, 136, 3)])
-def test_batch_vs_oracle(kind, h, w, bsz):
+def test_batch_vs_oracle(kind, h, w, bsz, decide_path):
     gen = synth.GENERATORS[kind]
     covers = np.stack([gen(h, w, 100 + i) for i in range(bsz)])
     msgs = [synth.payload(64 + 37 * i, i) for i in range(bsz)]
@@ -102,7 +111,7 @@ def test_batch_vs_oracle(kind, h, w, bsz):
 
 
 @pytest.mark.parametrize("kat", golden_io.kat2048(), ids=lambda k: f"{k['kind']}{k['seed']}b{k['beta']}")
-def test_kat_2048(kat):
+def test_kat_2048(kat, decide_path):
     """Full-size (2048^2) known answers from the reference, as sha256 digests."""
     img = synth.GENERATORS[kat["kind"]](kat["h"], kat["w"], kat["seed"])
     assert hashlib.sha256(img.tobytes()).hexdigest() == kat["cover_sha256"]

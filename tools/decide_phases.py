@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Phase timing of k_decide (diagnostic): loads tools/bin/libcodec_hip_dts.so (built with
+-DDECIDE_TS, which makes k_decide's thread 0 stamp wall_clock64() at phase boundaries into
+its term scratch) and prints median per-phase microseconds over the batch.
+    hipcc ... -DDECIDE_TS ... -o tools/bin/libcodec_hip_dts.so && python tools/decide_phases.py"""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    import torch
+
+    from codec_tcc_amd import _lib
+    _lib.load(os.path.join(REPO, "tools", "bin", "libcodec_hip_dts.so"))
+    import bench
+    import codec_tcc_amd as ct
+    from codec_tcc_amd import synth
+    kind = sys.argv[1] if len(sys.argv) > 1 else "ct12"
+    B, H, W = 64, 2048, 2048
+    dev = torch.device("cuda", 0)
+    covers = bench.make_covers(torch, kind, B, H, W, dev, 0)
+    codec = ct.Codec(B, H, W, dtype="uint16", device=dev)
+    pl = ct.make_payloads([synth.payload(1024, 7 + i) for i in range(B)], dev)
+    for _ in range(3):
+        codec.encode(covers, pl)
+    torch.cuda.synchronize()
+    R = 65536
+    keys = (B * R * 4 + 255) // 256 * 256
+    orv = (keys + B * 8 + 255) // 256 * 256
+    exact = (orv + B * 4 + 255) // 256 * 256
+    nby = (H + 15) // 16
+    cap = nby * ((W + 15) // 16)
+    terms = (exact + B * cap * 8 + 255) // 256 * 256
+    ws = codec.workspace.cpu().numpy()
+    raw = ws[terms: terms + B * R * 8].view(np.int64).reshape(B, R)[:, R - 8:]
+    t = raw[:, :6]
+    w0 = raw[:, 6:8]   # wave 0 (plane 0): after its H(X,Y) sum, after its joint-order list
+    print("wave0: masks+list %.2f us, sum %.2f us, then to round end %.2f us" % (
+        np.median(w0[:, 1] - raw[:, 2]) * 0.01, np.median(w0[:, 0] - w0[:, 1]) * 0.01,
+        np.median(raw[:, 3] - w0[:, 0]) * 0.01))
+    d = np.diff(t, axis=1)
+    names = ["pass1+scan", "terms", "H(Y)+MI", "offset argmax", "windows/meta"]
+    med = np.median(d, axis=0)
+    print(kind, "wall_clock64 ticks (100 MHz => 10 ns/tick):")
+    for n, v in zip(names, med):
+        print(f"  {n:16s} {v:8.0f} ticks = {v * 0.01:7.2f} us")
+    print(f"  total            {np.median(t[:, -1] - t[:, 0]) * 0.01:7.2f} us")
+
+
+if __name__ == "__main__":
+    main()
