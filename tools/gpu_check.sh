@@ -23,8 +23,8 @@ fi
 if has prof; then
   R="$GRAFT_REPO_ROOT"
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
-      -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --cpu-seconds 0 --no-profile \
-      > "$R/gpurun_out/prof.log" 2>&1 ); rc=$?
+      -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --cpu-seconds 0 \
+      > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof.log" ); rc=$?
   echo "rocprof rc=$rc"; tail -3 gpurun_out/prof.log
   find gpurun_out/prof -name "*stats*" | head
   [ $rc -eq 0 ] || exit $rc
