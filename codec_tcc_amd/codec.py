@@ -228,7 +228,7 @@ class Codec:
         if not t.is_contiguous():
             raise ValueError("pixel tensor must be contiguous")
 
-    # -- encode: codec_plan + codec_embed
+    # -- encode: codec_encode (= codec_plan + codec_embed, fused when the dtypes allow)
     def encode(self, covers, payloads, *, stego=None, maps=None, meta=None) -> Encoded:
         torch = _torch()
         self._check_pixels(covers, self.in_bytes)
@@ -244,12 +244,10 @@ class Codec:
             meta = torch.empty((self.B, _lib.META_BYTES), dtype=torch.uint8, device=self.device)
         lib = _lib.load()
         st = _stream()
-        _lib.check(lib.codec_plan(C.byref(P), covers.data_ptr(), stego.data_ptr(), self.lut.data_ptr(),
-                                  self.lut.numel(), pl.table.data_ptr(), pl.classes.data_ptr(),
-                                  meta.data_ptr(), self.workspace.data_ptr(), self.workspace.numel(), st),
-                   "codec_plan")
-        _lib.check(lib.codec_embed(C.byref(P), covers.data_ptr(), stego.data_ptr(), pl.words.data_ptr(),
-                                   meta.data_ptr(), maps.data_ptr(), st), "codec_embed")
+        _lib.check(lib.codec_encode(C.byref(P), covers.data_ptr(), stego.data_ptr(), self.lut.data_ptr(),
+                                    self.lut.numel(), pl.table.data_ptr(), pl.classes.data_ptr(),
+                                    meta.data_ptr(), self.workspace.data_ptr(), self.workspace.numel(),
+                                    pl.words.data_ptr(), maps.data_ptr(), st), "codec_encode")
         return Encoded(stego=stego, maps=maps, meta=meta, payloads=pl, config=dict(self.config))
 
     # -- plan only (decomposition + offset, no payload writes)

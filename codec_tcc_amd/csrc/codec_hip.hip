@@ -722,6 +722,33 @@ __global__ __launch_bounds__(256) void k_block_exact(const T* __restrict__ img, 
     scores[(size_t)b * cap + e] = sum / (double)n;
 }
 
+// ------------------------------------------------------------------ per-slice window cache
+struct SliceWin {
+    int s, tot, npix;
+    uint32_t flags;
+    int perm[16], off[16], n[16], cat[16], src[16], sizes[16];
+};
+
+__device__ __forceinline__ void load_win(const codec_slice_meta* M, SliceWin* W) {
+    if (threadIdx.x == 0) {
+        W->s = M->s; W->tot = M->total_used; W->npix = M->npix; W->flags = M->flags;
+        for (int i = 0; i < 16; ++i) {
+            W->perm[i] = M->perm[i]; W->off[i] = M->off[i]; W->n[i] = M->n[i];
+            W->cat[i] = M->cat[i]; W->src[i] = M->src[i]; W->sizes[i] = M->sizes[i];
+        }
+    }
+    __syncthreads();
+}
+
+// plane owning location-map bit j (segments are concatenated in perm order)
+__device__ __forceinline__ int plane_of(const SliceWin& W, int j) {
+    for (int k = 0; k < W.s; ++k) {
+        const int p = W.perm[k];
+        if (j < W.cat[p] + W.n[p]) return p;
+    }
+    return -1;
+}
+
 // ------------------------------------------------------------------ K3: decide
 // identity order: element k is the k-th non-zero bin's term p*log2(p)
 struct RankTerm {
@@ -769,7 +796,18 @@ __device__ void build_joint_order(u64 nzmask, int v0, uint32_t rank0, int plane,
     __syncthreads();
 }
 
-template <typename T>
+// EMBED: codec_encode's fused path -- after thread 0 has written the slice's windows, the
+// workgroup embeds the slice's payload itself (k_embed's work, without its launch)
+struct EmbedArgs {
+    const void* cover;
+    void* stego;
+    const u64* payload;
+    u64* maps;
+    int pw, mw;
+    uint32_t keep;
+};
+
+template <typename T, bool EMBED = false>
 __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t* __restrict__ ghist_all,
                                                  const uint32_t* __restrict__ gor, double* __restrict__ gterms,
                                                  const u64* __restrict__ gkey, const double* __restrict__ exact,
@@ -777,7 +815,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
                                                  const double* __restrict__ lut, long long lut_len,
                                                  const codec_layout* __restrict__ table,
                                                  const int32_t* __restrict__ slice_class,
-                                                 codec_slice_meta* __restrict__ meta_all) {
+                                                 codec_slice_meta* __restrict__ meta_all, EmbedArgs E) {
     constexpr int R = HistCfg<T>::kBins;
     // `list` doubles as the wave-parallel path's arena: terms (8m B), rank -> value (2m B),
     // one joint-order list per plane in flight (2m B each)
@@ -1065,7 +1103,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     }
 
     DTS(4);
-    if (t != 0) return;
+    if (t == 0) {   // ---- windows and the slice record (thread 0)
     int offset = 0;
     if (P.fixed_offset >= 0) offset = P.fixed_offset;
     else if (P.mode == CODEC_MODE_HYBRID) offset = (bix / nbx) * sb * P.W + (bix % nbx) * sb;
@@ -1118,36 +1156,47 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     }
     for (int i = 0; i < 16; ++i) M->mi[i] = mis_sh[i];
     DTS(5);
-}
-
-// ------------------------------------------------------------------ per-slice window cache
-struct SliceWin {
-    int s, tot, npix;
-    uint32_t flags;
-    int perm[16], off[16], n[16], cat[16], src[16], sizes[16];
-};
-
-__device__ __forceinline__ void load_win(const codec_slice_meta* M, SliceWin* W) {
-    if (threadIdx.x == 0) {
-        W->s = M->s; W->tot = M->total_used; W->npix = M->npix; W->flags = M->flags;
-        for (int i = 0; i < 16; ++i) {
-            W->perm[i] = M->perm[i]; W->off[i] = M->off[i]; W->n[i] = M->n[i];
-            W->cat[i] = M->cat[i]; W->src[i] = M->src[i]; W->sizes[i] = M->sizes[i];
+    }
+    if constexpr (EMBED) {
+        __shared__ SliceWin W;
+        load_win(M, &W);                      // thread 0 wrote M; barrier inside
+        const T* cv = static_cast<const T*>(E.cover) + (size_t)b * npx;
+        T* sv = static_cast<T*>(E.stego) + (size_t)b * npx;
+        const u64* pay = E.payload + (size_t)b * E.pw;
+        for (int j0 = 0; j0 < W.tot && j0 < E.mw * 64; j0 += 1024) {
+            const int j = j0 + t;
+            uint32_t mapbit = 0;
+            if (j < W.tot) mapbit = embed_bit<T, T>(cv, sv, npx, E.keep, pay, W, j);
+            const u64 bal = __ballot(mapbit);
+            if ((t & 63) == 0 && (j >> 6) < E.mw) E.maps[(size_t)b * E.mw + (j >> 6)] = bal;
         }
     }
-    __syncthreads();
-}
-
-// plane owning location-map bit j (segments are concatenated in perm order)
-__device__ __forceinline__ int plane_of(const SliceWin& W, int j) {
-    for (int k = 0; k < W.s; ++k) {
-        const int p = W.perm[k];
-        if (j < W.cat[p] + W.n[p]) return p;
-    }
-    return -1;
 }
 
 // ------------------------------------------------------------------ K4: embed (window writes)
+// location-map bit j of one slice: window write of payload bit src[p] + i into plane p of
+// pixel off[p] + i (codec.py:455-485 / 288-316); returns cover_bit ^ message_bit
+template <typename Tin, typename Tout>
+__device__ __forceinline__ uint32_t embed_bit(const Tin* __restrict__ cover, Tout* __restrict__ stego, long long npx,
+                                              uint32_t keep, const u64* __restrict__ payload, const SliceWin& W, int j) {
+    const int p = plane_of(W, j);
+    const int i = j - W.cat[p];
+    long long q = (long long)W.off[p] + i;
+    if (q >= npx) q -= npx;
+    const long long sbit = (long long)W.src[p] + i;
+    const uint32_t mb = (uint32_t)(payload[sbit >> 6] >> (sbit & 63)) & 1u;
+    const uint32_t orig = cover[q];
+    if (!(W.flags & CODEC_FLAG_OVERLAP)) {
+        stego[q] = (Tout)(((orig & keep) & ~(1u << p)) | (mb << p));
+    } else {
+        const size_t byte = (size_t)q * sizeof(Tout);
+        uint32_t* word = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(stego) + (byte & ~(size_t)3));
+        const uint32_t bit = 1u << ((byte & 3) * 8 + p);
+        if (mb) atomicOr(word, bit); else atomicAnd(word, ~bit);
+    }
+    return ((orig >> p) & 1u) ^ mb;
+}
+
 template <typename Tin, typename Tout>
 __global__ __launch_bounds__(256) void k_embed(const Tin* __restrict__ cover, Tout* __restrict__ stego,
                                                long long npx, uint32_t keep, const u64* __restrict__ payload,
@@ -1159,24 +1208,9 @@ __global__ __launch_bounds__(256) void k_embed(const Tin* __restrict__ cover, To
     const int j = blockIdx.x * 256 + threadIdx.x;
     if ((j & ~63) >= W.tot) return;   // whole wave past the end (uniform)
     uint32_t mapbit = 0;
-    if (j < W.tot) {
-        const int p = plane_of(W, j);
-        const int i = j - W.cat[p];
-        long long q = (long long)W.off[p] + i;
-        if (q >= npx) q -= npx;
-        const long long sbit = (long long)W.src[p] + i;
-        const uint32_t mb = (uint32_t)(payload[(size_t)b * pw + (sbit >> 6)] >> (sbit & 63)) & 1u;
-        const uint32_t orig = cover[(size_t)b * npx + q];
-        mapbit = ((orig >> p) & 1u) ^ mb;
-        if (!(W.flags & CODEC_FLAG_OVERLAP)) {
-            stego[(size_t)b * npx + q] = (Tout)(((orig & keep) & ~(1u << p)) | (mb << p));
-        } else {
-            const size_t byte = ((size_t)b * npx + q) * sizeof(Tout);
-            uint32_t* word = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(stego) + (byte & ~(size_t)3));
-            const uint32_t bit = 1u << ((byte & 3) * 8 + p);
-            if (mb) atomicOr(word, bit); else atomicAnd(word, ~bit);
-        }
-    }
+    if (j < W.tot)
+        mapbit = embed_bit<Tin, Tout>(cover + (size_t)b * npx, stego + (size_t)b * npx, npx, keep,
+                                      payload + (size_t)b * pw, W, j);
     const u64 bal = __ballot(mapbit);
     if ((threadIdx.x & 63) == 0) maps[(size_t)b * mw + (j >> 6)] = bal;
 }
@@ -1416,7 +1450,9 @@ __global__ __launch_bounds__(256) void k_gather(const T* __restrict__ stego, lon
     const int b = blockIdx.y;
     load_win(meta + b, &W);
     const int j = blockIdx.x * 256 + threadIdx.x;
-    if ((j & ~63) >= W.tot) return;
+    // every word of the slice's payload row is written (zeros past total_used), so the
+    // caller needs no memset
+    if ((j >> 6) >= pw) return;
     uint32_t bit = 0;
     if (j < W.tot) {
         const int p = plane_of(W, j);
@@ -1823,11 +1859,10 @@ static int launch_scan_generic(const codec_params* P, const void* cover, void* s
     return 0;
 }
 
-extern "C" {
-
-int codec_plan(const codec_params* P, const void* cover, void* stego, const double* log2_lut, int64_t lut_len,
-               const codec_layout* table, const int32_t* slice_class, codec_slice_meta* meta, void* workspace,
-               size_t workspace_bytes, void* stream) {
+// codec_plan's body; E != nullptr: codec_encode's fused path (k_decide embeds the payload)
+static int plan_impl(const codec_params* P, const void* cover, void* stego, const double* log2_lut, int64_t lut_len,
+                     const codec_layout* table, const int32_t* slice_class, codec_slice_meta* meta, void* workspace,
+                     size_t workspace_bytes, void* stream, const EmbedArgs* E) {
     int rc = check_params(P);
     if (rc) return rc;
     if (!cover || !log2_lut || !table || !slice_class || !meta || !workspace)
@@ -1878,15 +1913,44 @@ int codec_plan(const codec_params* P, const void* cover, void* stego, const doub
     }
     codec_params Pv = *P;
     Pv.reserved = knob("CODEC_DECIDE_WAVES", 1) ? 0 : 1;   // bit 0: force the block-sequential decision
-    ProfScope prof(st, CODEC_K_DECIDE);
-    if (P->in_bytes == 2)
-        hipLaunchKernelGGL(k_decide<uint16_t>, dim3(P->B), dim3(1024), 0, st, Pv, hist, orv, terms, keys, exact, L.exact_cap,
-                           edge_only, fast ? 1 : 0, log2_lut, (long long)lut_len, table, slice_class, meta);
-    else
-        hipLaunchKernelGGL(k_decide<uint8_t>, dim3(P->B), dim3(1024), 0, st, Pv, hist, orv, terms, keys, exact, L.exact_cap,
-                           edge_only, fast ? 1 : 0, log2_lut, (long long)lut_len, table, slice_class, meta);
+    ProfScope prof(st, E ? CODEC_K_DECIDE_EMBED : CODEC_K_DECIDE);
+    const EmbedArgs Ev = E ? *E : EmbedArgs{nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
+#define DEC(TT, EM) hipLaunchKernelGGL((k_decide<TT, EM>), dim3(P->B), dim3(1024), 0, st, Pv, hist, orv, terms, keys, exact, \
+                                       L.exact_cap, edge_only, fast ? 1 : 0, log2_lut, (long long)lut_len, table, slice_class, meta, Ev)
+    if (P->in_bytes == 2) { if (E) DEC(uint16_t, true); else DEC(uint16_t, false); }
+    else { if (E) DEC(uint8_t, true); else DEC(uint8_t, false); }
+#undef DEC
     LAUNCH_CHECK("k_decide");
     return 0;
+}
+
+extern "C" {
+
+int codec_plan(const codec_params* P, const void* cover, void* stego, const double* log2_lut, int64_t lut_len,
+               const codec_layout* table, const int32_t* slice_class, codec_slice_meta* meta, void* workspace,
+               size_t workspace_bytes, void* stream) {
+    return plan_impl(P, cover, stego, log2_lut, lut_len, table, slice_class, meta, workspace, workspace_bytes, stream,
+                     nullptr);
+}
+
+int codec_encode(const codec_params* P, const void* cover, void* stego, const double* log2_lut, int64_t lut_len,
+                 const codec_layout* table, const int32_t* slice_class, codec_slice_meta* meta, void* workspace,
+                 size_t workspace_bytes, const uint64_t* payload, uint64_t* maps, void* stream) {
+    int rc = check_params(P);
+    if (rc) return rc;
+    if (!stego || !payload || !maps) return set_err(CODEC_EINVAL, "codec_encode: NULL pointer argument");
+    if (P->payload_words < 1 || P->map_words < 1) return set_err(CODEC_EINVAL, "payload_words/map_words must be >= 1");
+    if ((uintptr_t)stego % 4) return set_err(CODEC_EINVAL, "stego must be 4-byte aligned");
+    // fused when stego and cover share a dtype (the decision kernel is typed on it)
+    if (P->in_bytes == P->out_bytes && knob("CODEC_FUSED_EMBED", 1) != 0) {
+        const EmbedArgs E{cover, stego, reinterpret_cast<const u64*>(payload), reinterpret_cast<u64*>(maps),
+                          P->payload_words, P->map_words, (1u << P->nbits) - 1u};
+        return plan_impl(P, cover, stego, log2_lut, lut_len, table, slice_class, meta, workspace, workspace_bytes,
+                         stream, &E);
+    }
+    rc = plan_impl(P, cover, stego, log2_lut, lut_len, table, slice_class, meta, workspace, workspace_bytes, stream,
+                   nullptr);
+    return rc ? rc : codec_embed(P, cover, stego, payload, meta, maps, stream);
 }
 
 int codec_embed(const codec_params* P, const void* cover, void* stego, const uint64_t* payload,
@@ -1986,7 +2050,6 @@ int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps
         if (P->payload_words < 1) return set_err(CODEC_EINVAL, "payload_words must be >= 1");
         const long long maxbits = (long long)P->payload_words * 64;
         dim3 grid((unsigned)((maxbits + 255) / 256), P->B);
-        HIP_TRY(hipMemsetAsync(payload_out, 0, (size_t)P->B * P->payload_words * 8, st));
         ProfScope prof(st, CODEC_K_GATHER);
         if (P->in_bytes == 2)
             hipLaunchKernelGGL(k_gather<uint16_t>, grid, dim3(256), 0, st, static_cast<const uint16_t*>(stego), npx,

@@ -110,6 +110,15 @@ int codec_plan(const codec_params* P, const void* cover, void* stego, const doub
                int64_t lut_len, const codec_layout* table, const int32_t* slice_class,
                codec_slice_meta* meta, void* workspace, size_t workspace_bytes, void* stream);
 
+/* codec_plan + codec_embed in one call, same results: when stego and cover share a dtype the
+ * decision kernel embeds each slice's payload itself once its windows are known (one launch
+ * fewer, and the embed runs inside the decision's workgroup); otherwise plan then embed.
+ * (Batched API: Codec.encode.) */
+int codec_encode(const codec_params* P, const void* cover, void* stego, const double* log2_lut,
+                 int64_t lut_len, const codec_layout* table, const int32_t* slice_class,
+                 codec_slice_meta* meta, void* workspace, size_t workspace_bytes,
+                 const uint64_t* payload, uint64_t* maps, void* stream);
+
 /* Window writes + location map: the embed loop of lsb_embed_block_then_multiplane
  * (codec.py:455-485) / lsb_embed_multi_plane (codec.py:288-316).  stego must already
  * hold the copy written by codec_plan.  payload[B][payload_words] (bit b of slice =
@@ -245,6 +254,7 @@ int codec_quality_moments(int32_t B, int32_t H, int32_t W, int32_t bytes, const 
 #define CODEC_K_SCAN_ROWS 19
 #define CODEC_K_SCAN_ROWS_READ 20
 #define CODEC_K_QUALITY 21
+#define CODEC_K_DECIDE_EMBED 22
 int codec_profile_begin(int32_t capacity);
 /* after the stream has been synchronised: fills ms[i], tag[i] for the recorded pairs and
  * returns their count (closes the window and frees the events). */

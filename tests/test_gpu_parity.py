@@ -34,9 +34,11 @@ def _run_case(case):
 @pytest.fixture(params=["waves", "block"])
 def decide_path(request, monkeypatch):
     """k_decide's wave-parallel MI path (default when the joint orders fit in LDS) and the
-    block-sequential one (CODEC_DECIDE_WAVES=0; also what large-m slices use)."""
+    block-sequential one (CODEC_DECIDE_WAVES=0; also what large-m slices use).  The block
+    variant also runs codec_encode unfused (codec_plan then the separate k_embed launch)."""
     if request.param == "block":
         monkeypatch.setenv("CODEC_DECIDE_WAVES", "0")
+        monkeypatch.setenv("CODEC_FUSED_EMBED", "0")
     return request.param
 
 
@@ -188,7 +190,7 @@ def test_inplace_matches_out_of_place(case):
 @pytest.mark.parametrize("kind,h,w,bsz,mode", [("ct12", 512, 512, 4, "hybrid"), ("u16", 256, 320, 3, "hybrid"),
                                                ("u8", 200, 96, 3, "hybrid"), ("ct12", 128, 128, 3, "multi"),
                                                ("ct12", 37, 53, 2, "hybrid")])
-def test_inplace_batch_roundtrip(kind, h, w, bsz, mode):
+def test_inplace_batch_roundtrip(kind, h, w, bsz, mode, decide_path):
     gen = synth.GENERATORS[kind]
     covers = np.stack([gen(h, w, 300 + i) for i in range(bsz)])
     msgs = [synth.payload(40 + 53 * i, 11 + i) for i in range(bsz)]
