@@ -408,6 +408,97 @@ __global__ __launch_bounds__(256) void k_pee_dcount_w(const T* __restrict__ steg
     }
 }
 
+// ---- embed, prefix tiles, W % 8 == 0: same work as k_pee_embed with one barrier per tile
+// instead of seven -- the bit cursor is a wave scan plus the (double-buffered) totals of
+// the tile's earlier waves, location-map words are OR-reduced over 16 lanes with shuffles
+// and stored directly, the unsafe count goes out with one atomic per wave at the end.
+template <typename T>
+__global__ __launch_bounds__(256) void k_pee_embed_v(const T* __restrict__ cover, T* __restrict__ stego, int H, int W,
+                                                     const u64* __restrict__ payload_all, int pw,
+                                                     const uint32_t* __restrict__ tile_off_all, int ntiles_max,
+                                                     codec_pee_meta* __restrict__ meta_all,
+                                                     u64* __restrict__ lm_all, int lmw) {
+    typedef typename Vec8<T>::type V;
+    __shared__ uint32_t wtot[2][4];
+    const int b = blockIdx.y;
+    codec_pee_meta* M = meta_all + b;
+    const int tile_end = M->tile_end, end = M->end, Tthr = M->T, maxval = M->maxval;
+    const size_t npx = (size_t)H * W;
+    const T* src = cover + b * npx;
+    T* dst = stego + b * npx;
+    const u64* payload = payload_all + (size_t)b * pw;
+    u64* lm = lm_all + (size_t)b * lmw;
+    const uint32_t* off = tile_off_all + (size_t)b * ntiles_max;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int CR = W / 8;
+    int nun = 0, par = 0;
+    for (int t = blockIdx.x; t <= tile_end; t += gridDim.x, par ^= 1) {
+        const int item = t * 256 + threadIdx.x;
+        const int k0 = 4 * item;
+        const bool ok = k0 <= end;
+        const int r = item / CR, c = item - r * CR;
+        const size_t o0 = (size_t)(2 * r) * W + (size_t)c * 8, o1 = o0 + W;
+        V v0, v1;
+        if (ok) {
+            v0 = *reinterpret_cast<const V*>(src + o0);
+            v1 = *reinterpret_cast<const V*>(src + o1);
+        }
+        const uint32_t tbase = off[t];
+        PeeCand pc[4];
+        uint32_t local = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            pc[u].expand = pc[u].safe = pc[u].right = false;
+            if (ok && k0 + u <= end) {
+                pc[u] = pee_classify((int)get_px(v1, 2 * u + 1), (int)get_px(v1, 2 * u), (int)get_px(v0, 2 * u + 1),
+                                     (int)get_px(v0, 2 * u), Tthr, maxval);
+                local += (pc[u].expand && pc[u].safe) ? 1u : 0u;
+            }
+        }
+        uint32_t inc = local;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        if (lane == 63) wtot[par][wv] = inc;
+        __syncthreads();
+        uint32_t cur = tbase + inc - local;
+        for (int w = 0; w < wv; ++w) cur += wtot[par][w];
+        const uint32_t w0 = cur >> 6;                 // this thread's <= 4 bits: words w0, w0 + 1
+        const u64 p0 = local ? payload[w0] : 0ull;
+        const u64 p1 = (local && (int)w0 + 1 < pw) ? payload[w0 + 1] : 0ull;
+        uint32_t nib = 0;
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (!ok || k0 + u > end) continue;
+            if (!pc[u].safe) { nib |= 1u << u; ++nun; continue; }
+            int nv;
+            if (pc[u].expand) {
+                const u64 wd = (cur >> 6) == w0 ? p0 : p1;
+                const int bit = (int)((wd >> (cur & 63)) & 1ull);
+                ++cur;
+                nv = pc[u].p + 2 * (pc[u].x - pc[u].p) + bit;
+            } else {
+                nv = pc[u].right ? pc[u].x + Tthr : pc[u].x - Tthr;
+            }
+            set_px(v1, 2 * u + 1, (uint32_t)nv);
+            any = true;
+        }
+        if (any) *reinterpret_cast<V*>(dst + o1) = v1;
+        // location-map word (4 * item) / 64 = 16 threads x 4 candidate bits
+        u64 wm = (u64)nib << (4 * (lane & 15));
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) wm |= __shfl_xor(wm, o, 64);
+        const int wi = k0 >> 6;
+        if ((lane & 15) == 0 && wi < lmw) lm[wi] = wm;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) nun += __shfl_xor(nun, o, 64);
+    if (lane == 0 && nun) atomicAdd(&M->lm_count, nun);
+}
+
 // ---- extract
 template <typename T, bool NT>
 __global__ __launch_bounds__(256) void k_pee_copy(const T* __restrict__ src, T* __restrict__ dst, long long nbytes) {
@@ -1232,6 +1323,18 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
         ProfScope prof(st, CODEC_K_PEE_EMBED);
         const int g = (int)knob("CODEC_PEE_EMBED_WGS", 64);
         dim3 grid(g < L.ntiles_max ? g : L.ntiles_max, P->B);
+        if (vec && knob("CODEC_PEE_EMBED_V", 1)) {
+            if (P->bytes == 2)
+                hipLaunchKernelGGL(k_pee_embed_v<uint16_t>, grid, dim3(256), 0, st, static_cast<const uint16_t*>(cover),
+                                   static_cast<uint16_t*>(stego), P->H, P->W, reinterpret_cast<const u64*>(payload),
+                                   P->payload_words, off, L.ntiles_max, meta, reinterpret_cast<u64*>(lm), P->lm_words);
+            else
+                hipLaunchKernelGGL(k_pee_embed_v<uint8_t>, grid, dim3(256), 0, st, static_cast<const uint8_t*>(cover),
+                                   static_cast<uint8_t*>(stego), P->H, P->W, reinterpret_cast<const u64*>(payload),
+                                   P->payload_words, off, L.ntiles_max, meta, reinterpret_cast<u64*>(lm), P->lm_words);
+            LAUNCH_CHECK("k_pee_embed_v");
+            return 0;
+        }
 #define PEMB(TT, VV) hipLaunchKernelGGL((k_pee_embed<TT, VV>), grid, dim3(256), 0, st, static_cast<const TT*>(cover), \
                                static_cast<TT*>(stego), P->H, P->W, reinterpret_cast<const u64*>(payload), \
                                P->payload_words, off, L.ntiles_max, meta, reinterpret_cast<u64*>(lm), P->lm_words)

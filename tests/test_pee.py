@@ -66,7 +66,7 @@ PATHS = {"auto": {}, "onepass": {"CODEC_PEE_ONEPASS": "1"}, "twopass": {"CODEC_P
          "onepass_small_grid": {"CODEC_PEE_ONEPASS": "1", "CODEC_PEE_1P_WGS": "7", "CODEC_PEE_IP_WGS": "3"},
          # decode-side tile counts: workgroup-per-tile (block sums) instead of wave-per-tile,
          # and wave-per-tile with one workgroup per slice (every wave strides over tiles)
-         "twopass_block_tiles": {"CODEC_PEE_ONEPASS": "0", "CODEC_PEE_WAVE_TILES": "0"},
+         "twopass_block_tiles": {"CODEC_PEE_ONEPASS": "0", "CODEC_PEE_WAVE_TILES": "0", "CODEC_PEE_EMBED_V": "0"},
          "twopass_wave_tiles_1wg": {"CODEC_PEE_ONEPASS": "0", "CODEC_PEE_DCOUNT_W_WGS": "1"}}
 
 
