@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
     ap.add_argument("--pee", type=int, default=1, help="also time the MED-PEE path (north-star algorithm)")
     ap.add_argument("--pee-T", type=int, default=2)
+    ap.add_argument("--c3", type=int, default=1, help="also time BASELINE config C3 (256 x 512^2)")
     return ap.parse_args()
 
 
@@ -247,6 +248,51 @@ def bench_pee(args, torch, dist, world, dev, covers, B, H, W, inplace=False):
     return res
 
 
+def bench_c3(args, torch, dist, world, dev, rank):
+    """BASELINE config C3: the same LSB step over 256 x 512^2 ct12 slices (1/16 of the
+    headline bytes: 128 MiB per image tensor, so part of each pass can hit the 256 MiB
+    Infinity Cache -- reported as measured, against the HBM peak)."""
+    import codec_tcc_amd as ct
+    from codec_tcc_amd import _lib, synth
+    B, H, W = 256, 512, 512
+    covers = make_covers(torch, args.kind, B, H, W, dev, seed=1000 + rank * B)
+    codec = ct.Codec(B, H, W, dtype="uint16", beta=0.4, block=16, device=dev)
+    pl = ct.make_payloads([synth.payload(args.payload_chars, 5000 + rank * B + i) for i in range(B)], dev)
+    stego = torch.empty_like(covers)
+    cov2 = torch.empty_like(covers)
+    maps = torch.empty((B, pl.map_words), dtype=torch.int64, device=dev)
+    meta = torch.empty((B, _lib.META_BYTES), dtype=torch.uint8, device=dev)
+    pay = torch.empty((B, pl.payload_words), dtype=torch.int64, device=dev)
+
+    def step():
+        codec.encode(covers, pl, stego=stego, maps=maps, meta=meta)
+        codec.decode(stego, maps, meta, payload_words=pl.payload_words, map_words=pl.map_words, cover=cov2,
+                     payload=pay)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    steps = 4 * args.steps
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    kern = _profile(_lib.load(), _lib, step, steps) if not args.no_profile else {}
+    ok = bool(torch.equal(cov2.view(torch.int16), covers.view(torch.int16)))
+    res = {"workload": f"{args.kind} 512x512 uint16 x 256 slices (C3)", "value": round(B * H * W * steps / el / 1e6, 1),
+           "unit": "Mpixels/s", "ms_per_step": round(el / steps * 1e3, 4), "roundtrip_ok": ok,
+           "kernels_ms": {k: round(v, 4) for k, v in kern.items()}}
+    sk = next((k for k in ("k_scan_rows", "k_scan_fast") if k in kern), None)
+    if sk:
+        by = B * H * W * 4
+        res["roofline"] = {"bound": "hbm", "kernel": sk, "achieved": round(by / (kern[sk] / 1e3) / 1e9, 1),
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(by / (kern[sk] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                           "algorithmic_bytes_per_launch": by}
+    return res
+
+
 def bench_quality(args, torch, covers, stego, B, H, W):
     """Stego quality of the LSB leg's output (reference src/mse.py metrics): one read-only
     pass over cover + stego (k_quality), metrics from exact moments on the host."""
@@ -351,6 +397,7 @@ def main():
             kernels.setdefault(_lib.KERNEL_TAGS.get(tags[i], str(tags[i])), []).append(ms[i])
 
     quality = bench_quality(args, torch, covers, stego, B, H, W) if rank == 0 else None
+    c3 = bench_c3(args, torch, dist, world, dev, rank) if (rank == 0 and args.c3) else None
     lsb_inplace = bench_lsb_inplace(args, torch, dist, world, dev, covers, codec, pl, B, H, W)
     pee = None
     if args.pee:
@@ -396,6 +443,8 @@ def main():
         }
         out["inplace"] = lsb_inplace
         out["quality"] = quality
+        if c3 is not None:
+            out["c3"] = c3
         if pee is not None:
             out["pee"] = pee
         if args.cpu_seconds > 0 and world == 1:

@@ -18,6 +18,8 @@
 // float64 sums reproduce numpy's bit for bit.
 #include "codec_common.h"
 
+#include <algorithm>
+
 thread_local char g_err[512] = "";
 ProfWin g_prof;
 
@@ -1768,7 +1770,13 @@ static int launch_scan_fast(const codec_params* P, const void* cover, void* steg
                             uint32_t* orv, hipStream_t st) {
     const int sb = P->block;
     const int nb = (P->H + sb - 1) / sb;
-    const int target = (int)knob("CODEC_SCAN_WGS", sizeof(T) == 2 ? 1024 : 1024);   // tools/tune.py
+    // workgroups per slice: enough to fill the CUs for small batches, and about one per
+    // 2 MiB of slice otherwise (each workgroup zeroes and flushes a 128 KiB LDS histogram,
+    // so small regions cost more than they stream: measured 256 x 512^2 0.066 ms at one
+    // workgroup per slice vs 0.108 at four; 256 x 2048^2 best at four)
+    const long long slice_bytes = (long long)P->H * P->W * sizeof(T);
+    const int per_slice = (int)std::max<long long>((256 + P->B - 1) / P->B, (slice_bytes + (2 << 20) - 1) / (2 << 20));
+    const int target = (int)knob("CODEC_SCAN_WGS", (long long)per_slice * P->B);   // tools/tune.py
     const bool nt = knob("CODEC_NT", 1) != 0;
     int wgps = (target + P->B - 1) / P->B;
     wgps = wgps < 1 ? 1 : (wgps > nb ? nb : wgps);
@@ -1787,7 +1795,8 @@ static int launch_scan_fast(const codec_params* P, const void* cover, void* steg
         // row-major sweep: bands per workgroup from CODEC_SCAN_ROWS_WGS, capped by the LDS
         // block-counter capacity
         const int fullbx = P->W / sb;
-        const int rtarget = s ? (int)knob("CODEC_SCAN_ROWS_WGS", 1024) : (int)knob("CODEC_SCAN_ROWS_READ_WGS", 1024);
+        const int rtarget = s ? (int)knob("CODEC_SCAN_ROWS_WGS", (long long)per_slice * P->B)
+                              : (int)knob("CODEC_SCAN_ROWS_READ_WGS", (long long)per_slice * P->B);
         int rw = (rtarget + P->B - 1) / P->B;
         rw = rw < 1 ? 1 : (rw > nb ? nb : rw);
         int rb = (nb + rw - 1) / rw;

@@ -160,3 +160,52 @@ def test_gpu_capacity_exceeded_flags():
     assert enc.records()[0].status == 1 and enc.records()[0].end == 32 * 32 - 1
     with pytest.raises(ValueError):
         codec.decode(enc)
+
+
+@pytest.mark.parametrize("name,maxval,T", [("pe", 4095, 2), ("pe", 4095, 1), ("torax", 255, 2), ("torax", 255, 4)])
+def test_oracle_real_dicom_overflow_map(name, maxval, T):
+    """C5: the reference's own 12-bit (pe.dcm, BitsStored=12 -> full scale 4095) and 8-bit
+    (torax.dcm) slices; their saturated / zero regions make the overflow location map non-empty."""
+    import golden_io
+    img = golden_io.images()[name]
+    cap = P.capacity(img, T, maxval)
+    L = min(cap, 8192)
+    st, side = P.pee_embed(img, _bits(L, 3), T, maxval=maxval)
+    assert int(st.max()) <= maxval
+    bits, cov = P.pee_extract(st, side)
+    np.testing.assert_array_equal(bits, _bits(L, 3))
+    np.testing.assert_array_equal(cov, img)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inplace", [False, True])
+@pytest.mark.parametrize("name,maxval,T", [("pe", 4095, 2), ("pe", 4095, 1), ("torax", 255, 2)])
+def test_gpu_real_dicom_matches_oracle(name, maxval, T, inplace, pee_path):
+    """C5 on the GPU: real DICOM pixels with the container's full scale as maxval; stego,
+    location map (overflow candidates), end and the recovered payload/cover vs the oracle."""
+    torch = pytest.importorskip("torch")
+    import golden_io
+    from codec_tcc_amd import framing
+    from codec_tcc_amd.pee import PeeCodec, lm_bits
+    img = golden_io.images()[name]
+    cap = P.capacity(img, T, maxval)
+    payload = _bits(min(cap, 8192), 5)
+    covers = np.stack([img, img[::-1].copy()])
+    payloads = [payload, _bits(min(P.capacity(covers[1], T, maxval), 4000), 6)]
+    codec = PeeCodec(2, img.shape[0], img.shape[1], dtype=str(img.dtype), T=T, maxval=maxval)
+    dev = torch.from_numpy(covers).cuda()
+    enc = codec.embed(dev, payloads, stego=dev if inplace else None)
+    recs = enc.records()
+    for i in range(2):
+        st, side = P.pee_embed(covers[i], payloads[i], T, maxval=maxval)
+        assert recs[i].status == 0 and recs[i].end == side["end"]
+        np.testing.assert_array_equal(enc.stego[i].cpu().numpy(), st)
+        np.testing.assert_array_equal(lm_bits(enc, i), side["lm"])
+        assert recs[i].lm_count == int(side["lm"].sum())
+    assert sum(r.lm_count for r in recs) > 0          # the overflow map is exercised
+    words, cover = codec.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words,
+                                 cover=enc.stego if inplace else None)
+    host = words.cpu().numpy()
+    for i in range(2):
+        np.testing.assert_array_equal(framing.unpack_bits(host[i], len(payloads[i])), payloads[i])
+    np.testing.assert_array_equal(cover.cpu().numpy(), covers)

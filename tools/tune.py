@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--size", type=int, default=2048)
     ap.add_argument("--configs", default="")
     ap.add_argument("--inplace", action="store_true", help="stego is cover, cover_out is stego")
     a = ap.parse_args()
@@ -41,7 +42,7 @@ def main():
     from codec_tcc_amd import _lib, synth
     configs = json.loads(a.configs) if a.configs else CONFIGS
     dev = torch.device("cuda", 0)
-    B, H, W = a.batch, 2048, 2048
+    B, H, W = a.batch, a.size, a.size
     covers = bench.make_covers(torch, a.kind, B, H, W, dev, 0)
     codec = ct.Codec(B, H, W, dtype="uint16", device=dev)
     pl = ct.make_payloads([synth.payload(1024, 7 + i) for i in range(B)], dev)
