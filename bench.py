@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
     ap.add_argument("--pee", type=int, default=1, help="also time the MED-PEE path (north-star algorithm)")
     ap.add_argument("--pee-T", type=int, default=2)
+    ap.add_argument("--cpu-pool", type=int, default=16,
+                    help="workers of the pooled CPU baseline (the box's CPU share per GPU is 16; 0 = skip)")
     ap.add_argument("--c3", type=int, default=1, help="also time BASELINE config C3 (256 x 512^2)")
     return ap.parse_args()
 
@@ -109,6 +111,35 @@ def cpu_baseline(size: int, kind: str, chars: int, budget_s: float):
                   f"(decompose+hybrid embed+merge+extract_local_planes+decode_message), 1 process",
         "seconds": round(t_work, 2),
     }
+
+
+def _cpu_slice(job):
+    """One oracle encode+decode of a distinct slice (pool worker of cpu_baseline_pool)."""
+    size, kind, chars, seed = job
+    from codec_tcc_amd import synth
+    from oracle import ref_cpu as R
+    img = synth.GENERATORS[kind](size, size, seed)
+    bits = R.message_to_bits(synth.payload(chars, 7 + seed))
+    t0 = time.perf_counter()
+    enc = R.encode_slice(img, bits, beta=0.4, sb=16)
+    R.decode_slice(enc["stego"], enc["bitmaps"], enc["s"], enc["segments_lengths"], enc["segment_indices"])
+    return img.size, time.perf_counter() - t0
+
+
+def cpu_baseline_pool(size: int, kind: str, chars: int, workers: int, per_worker: int):
+    """The same oracle work spread over a process pool (one worker per host core
+    of this GPU's share).  Forked BEFORE the GPU is initialised in this process."""
+    import multiprocessing as mp
+    jobs = [(size, kind, chars, 2000 + i) for i in range(workers * per_worker)]
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        res = pool.map(_cpu_slice, jobs, chunksize=1)
+    wall = time.perf_counter() - t0
+    px = sum(r[0] for r in res)
+    return {"value": round(px / wall / 1e6, 3), "unit": "Mpixels/s", "cores": workers, "kind": "port",
+            "sample": f"{len(jobs)} x {size}x{size} {kind} slices over a {workers}-process pool (fork), wall clock",
+            "seconds": round(wall, 2)}
 
 
 def _profile(lib, _lib, fn, steps):
@@ -326,6 +357,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    pool_base = None
+    if args.cpu_seconds > 0 and world == 1 and args.cpu_pool > 0:
+        # before anything touches the GPU: the pool forks this process
+        pool_base = cpu_baseline_pool(args.size, args.kind, args.payload_chars, args.cpu_pool, 2)
     ndev = torch.cuda.device_count()
     if world > 1:
         torch.cuda.set_device(local % ndev)
@@ -449,6 +484,8 @@ def main():
             out["pee"] = pee
         if args.cpu_seconds > 0 and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.size, args.kind, args.payload_chars, args.cpu_seconds)
+            if pool_base is not None:
+                out["cpu_baseline"]["pool"] = pool_base
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
