@@ -1372,22 +1372,22 @@ __device__ __forceinline__ bool span_hit(long long q0, long long lo, long long l
 // iteration of a workgroup covers 1024 consecutive chunks; their slice (and its window
 // hull span_lo/span_len) is looked up once per iteration, wave-uniformly, and only chunks
 // inside the hull walk the per-plane windows.
-template <typename T, bool NT>
-__global__ __launch_bounds__(256) void k_restore_gs(const T* __restrict__ stego, T* __restrict__ cover,
+template <typename T, bool NT, int NTH = 256>
+__global__ __launch_bounds__(NTH) void k_restore_gs(const T* __restrict__ stego, T* __restrict__ cover,
                                                     uint32_t npx, uint32_t nchunks, uint32_t total_chunks,
                                                     const codec_slice_meta* __restrict__ meta,
                                                     const u64* __restrict__ maps_all, int mw) {
     typedef typename Vec8<T>::type V;
     const V* src = reinterpret_cast<const V*>(stego);
     V* dst = reinterpret_cast<V*>(cover);
-    const uint32_t stride = gridDim.x * 1024u;
-    for (uint32_t base = blockIdx.x * 1024u; base < total_chunks; base += stride) {
+    const uint32_t stride = gridDim.x * (4u * NTH);
+    for (uint32_t base = blockIdx.x * (4u * NTH); base < total_chunks; base += stride) {
         const uint32_t cb = base + threadIdx.x;
         V vv[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            if (cb + u * 256u < total_chunks) vv[u] = ldv<NT>(src + cb + u * 256u);
-        const uint32_t last = min(base + 1023u, total_chunks - 1);
+            if (cb + u * (uint32_t)NTH < total_chunks) vv[u] = ldv<NT>(src + cb + u * (uint32_t)NTH);
+        const uint32_t last = min(base + (4u * NTH - 1u), total_chunks - 1);
         const uint32_t b0 = __builtin_amdgcn_readfirstlane(base / nchunks);
         const uint32_t b1 = __builtin_amdgcn_readfirstlane(last / nchunks);
         if (b0 == b1) {
@@ -1397,16 +1397,16 @@ __global__ __launch_bounds__(256) void k_restore_gs(const T* __restrict__ stego,
             const u64* maps = maps_all + (size_t)b0 * mw;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const uint32_t g = cb + u * 256u;
+                const uint32_t g = cb + u * (uint32_t)NTH;
                 if (g >= total_chunks) break;
-                const long long q0 = qbase + (long long)(threadIdx.x + u * 256u) * 8;
+                const long long q0 = qbase + (long long)(threadIdx.x + u * (uint32_t)NTH) * 8;
                 if (span_hit(q0, lo, len, npx)) restore_chunk<T>(vv[u], q0, M, maps, npx);
                 stv<NT>(dst + g, vv[u]);
             }
         } else {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const uint32_t g = cb + u * 256u;
+                const uint32_t g = cb + u * (uint32_t)NTH;
                 if (g >= total_chunks) break;
                 const uint32_t b = g / nchunks;
                 const codec_slice_meta* M = meta + b;
@@ -2017,12 +2017,18 @@ int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps
             const bool ntg = knob("CODEC_NT", 1) != 0;
             const long long g = knob("CODEC_RESTORE_GS_WGS", 1 << 30);   // default: one 1024-chunk block per WG
             const uint32_t total = (uint32_t)(nchunks * P->B);
-            long long grid = (total + 1023) / 1024;
+            // measured: 256-thread workgroups stream a 2 GiB batch best (0.74 vs 0.81 ms at 1024),
+            // 1024-thread ones a 128 MiB batch (256 x 512^2: 0.068 vs 0.093 ms)
+            const long long sweep_bytes = (long long)total * 8 * P->in_bytes;
+            const int nth = (int)knob("CODEC_RESTORE_GS_THREADS", sweep_bytes <= (512LL << 20) ? 1024 : 256);
+            long long grid = (total + 4LL * nth - 1) / (4LL * nth);
             if (grid > g) grid = g;
             if (grid < 1) grid = 1;
             ProfScope prof(st, CODEC_K_RESTORE);
             const u64* mp = reinterpret_cast<const u64*>(maps);
-#define RGS(TT, NTV) hipLaunchKernelGGL((k_restore_gs<TT, NTV>), dim3((unsigned)grid), dim3(256), 0, st, \
+#define RGS(TT, NTV) if (nth == 1024) hipLaunchKernelGGL((k_restore_gs<TT, NTV, 1024>), dim3((unsigned)grid), dim3(1024), 0, st, \
+                static_cast<const TT*>(stego), static_cast<TT*>(cover_out), (uint32_t)npx, (uint32_t)nchunks, total, meta, mp, P->map_words); \
+            else hipLaunchKernelGGL((k_restore_gs<TT, NTV>), dim3((unsigned)grid), dim3(256), 0, st, \
                 static_cast<const TT*>(stego), static_cast<TT*>(cover_out), (uint32_t)npx, (uint32_t)nchunks, total, meta, mp, P->map_words)
             if (P->in_bytes == 2) { if (ntg) RGS(uint16_t, true); else RGS(uint16_t, false); }
             else { if (ntg) RGS(uint8_t, true); else RGS(uint8_t, false); }
