@@ -851,7 +851,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                                                     int maxval, const int32_t* __restrict__ lengths,
                                                     const u64* __restrict__ payload_all, int pw, int nchunks, int B,
                                                     u64* status_all, uint32_t* ctl, codec_pee_meta* meta_all,
-                                                    u64* __restrict__ lm_all, int lmw) {
+                                                    u64* __restrict__ lm_all, int lmw, int cmajor) {
     typedef typename Vec8<T>::type V;
     __shared__ u64 sh64[8];
     __shared__ uint32_t sh[8];
@@ -866,7 +866,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
     const int tid = threadIdx.x;
     for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
         int b, j;
-        if (!pee_slot(v, B, nchunks, INPLACE, &b, &j)) continue;   // uniform; no barrier passed
+        if (!pee_slot(v, B, nchunks, INPLACE || cmajor, &b, &j)) continue;   // uniform; no barrier passed
         uint32_t* tick = ctl + 32 + 32 * (size_t)b;
         u64* st = status_all + (size_t)b * nchunks;
         const uint32_t L = (uint32_t)max(0, lengths[b]);
@@ -1052,7 +1052,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
                                                       const codec_pee_meta* __restrict__ meta_all,
                                                       const u64* __restrict__ lm_all, int lmw, int nchunks, int B,
                                                       u64* status_all, uint32_t* ctl, u64* __restrict__ payload_all,
-                                                      int pw) {
+                                                      int pw, int cmajor) {
     typedef typename Vec8<T>::type V;
     __shared__ u64 sh64[8];
     __shared__ uint32_t s_v, s_excl;
@@ -1077,7 +1077,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
     }
     for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
         int b, j;
-        const bool valid = pee_slot(v, B, nchunks, INPLACE, &b, &j);
+        const bool valid = pee_slot(v, B, nchunks, INPLACE || cmajor, &b, &j);
         if (j > cmax) return;                           // in place: a lane's chunks only grow
         if (!valid) continue;
         const codec_pee_meta* M = meta_all + b;
@@ -1250,11 +1250,15 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
     const bool nt = knob("CODEC_NT", 1) != 0;
     const bool inplace = cover == stego;
     const long long items = (long long)(P->H / 2) * (P->W / 8);
-    // single pass: always in place (it stops reading after `end`); out of place the two-pass
-    // scan + prefix embed measured faster (tickets + look-back on every chunk cost more than
-    // re-reading the ~12 % prefix).  CODEC_PEE_ONEPASS: -1 auto, 0 never, 1 always.
+    // single pass: in place (it stops reading after `end`), and out of place for batches of
+    // >= 32 slices, with chunk-major slot order (all slices' chunk 0 first, then chunk 1 ...:
+    // every slice's look-back chain advances one hop per generation of resident workgroups;
+    // slice-major order left whole generations spinning on one slice's chain, 1.4 ms vs
+    // 0.82 ms at 256 x 2048^2, where the two-pass scan + prefix embed takes 0.85 ms).  Small
+    // batches keep the two-pass path (a lone slice's chain would be the critical path).
+    // CODEC_PEE_ONEPASS: -1 auto, 0 never, 1 always; CODEC_PEE_1P_CHUNK_MAJOR=0: slice-major.
     const long long onepass = knob("CODEC_PEE_ONEPASS", -1);
-    if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && (onepass > 0 || (onepass < 0 && inplace))) {
+    if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && (onepass > 0 || (onepass < 0 && (inplace || P->B >= 32)))) {
         u64* stw = reinterpret_cast<u64*>(static_cast<char*>(workspace) + L.st);
         uint32_t* ctl = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.ctl);
         HIP_TRY(hipMemsetAsync(stw, 0, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4, st));
@@ -1268,7 +1272,8 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
 #define PE1(TT, NTV, IP) hipLaunchKernelGGL((k_pee_embed1<TT, NTV, IP>), dim3((unsigned)g), dim3(256), 0, st, \
             static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, \
             reinterpret_cast<const u64*>(payload), P->payload_words, L.nchunks, P->B, stw, ctl, meta, \
-            reinterpret_cast<u64*>(lm), P->lm_words)
+            reinterpret_cast<u64*>(lm), P->lm_words, cmajor)
+        const int cmajor = (int)knob("CODEC_PEE_1P_CHUNK_MAJOR", 1);
         if (P->bytes == 2) {
             if (inplace) { if (nt) PE1(uint16_t, true, true); else PE1(uint16_t, false, true); }
             else { if (nt) PE1(uint16_t, true, false); else PE1(uint16_t, false, false); }
@@ -1365,7 +1370,7 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
     const long long items = (long long)(P->H / 2) * (P->W / 8);
     const bool inplace = stego == cover_out;
     const long long onepass = knob("CODEC_PEE_ONEPASS", -1);   // as in codec_pee_embed
-    if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && (onepass > 0 || (onepass < 0 && inplace))) {
+    if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && (onepass > 0 || (onepass < 0 && (inplace || P->B >= 32)))) {
         u64* stw = reinterpret_cast<u64*>(static_cast<char*>(workspace) + L.st);
         uint32_t* ctl = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.ctl);
         HIP_TRY(hipMemsetAsync(stw, 0, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4, st));
@@ -1376,7 +1381,8 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
         g = (g + 7) / 8 * 8;
 #define PX1(TT, NTV, IP) hipLaunchKernelGGL((k_pee_extract1<TT, NTV, IP>), dim3((unsigned)g), dim3(256), 0, st, \
             static_cast<const TT*>(stego), static_cast<TT*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm), \
-            P->lm_words, L.nchunks, P->B, stw, ctl, reinterpret_cast<u64*>(payload_out), P->payload_words)
+            P->lm_words, L.nchunks, P->B, stw, ctl, reinterpret_cast<u64*>(payload_out), P->payload_words, cmajor)
+        const int cmajor = (int)knob("CODEC_PEE_1P_CHUNK_MAJOR", 1);
         if (P->bytes == 2) {
             if (inplace) { if (nt) PX1(uint16_t, true, true); else PX1(uint16_t, false, true); }
             else { if (nt) PX1(uint16_t, true, false); else PX1(uint16_t, false, false); }
