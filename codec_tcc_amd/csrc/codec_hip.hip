@@ -1165,12 +1165,50 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
         const T* cv = static_cast<const T*>(E.cover) + (size_t)b * npx;
         T* sv = static_cast<T*>(E.stego) + (size_t)b * npx;
         const u64* pay = E.payload + (size_t)b * E.pw;
-        for (int j0 = 0; j0 < W.tot && j0 < E.mw * 64; j0 += 1024) {
-            const int j = j0 + t;
-            uint32_t mapbit = 0;
-            if (j < W.tot) mapbit = embed_bit<T, T>(cv, sv, npx, E.keep, pay, W, j);
-            const u64 bal = __ballot(mapbit);
-            if ((t & 63) == 0 && (j >> 6) < E.mw) E.maps[(size_t)b * E.mw + (j >> 6)] = bal;
+        // 8 bits per thread per round: all payload-word and cover loads of the round are
+        // issued before any store (the stores may alias the cover, so a per-bit loop would
+        // serialise one HBM round trip per bit)
+        const int lim = min(W.tot, E.mw * 64);
+        for (int j0 = 0; j0 < lim; j0 += 8 * 1024) {
+            int pl[8];
+            long long ql[8];
+            uint32_t mb[8], orig[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int j = j0 + k * 1024 + t;
+                pl[k] = -1;
+                if (j < lim) {
+                    const int p = plane_of(W, j);
+                    const int i = j - W.cat[p];
+                    long long q = (long long)W.off[p] + i;
+                    if (q >= npx) q -= npx;
+                    const long long sbit = (long long)W.src[p] + i;
+                    pl[k] = p;
+                    ql[k] = q;
+                    mb[k] = (uint32_t)(pay[sbit >> 6] >> (sbit & 63)) & 1u;
+                    orig[k] = cv[q];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (j0 + k * 1024 >= lim) break;                 // uniform
+                const int j = j0 + k * 1024 + t;
+                uint32_t mapbit = 0;
+                if (pl[k] >= 0) {
+                    const int p = pl[k];
+                    if (!(W.flags & CODEC_FLAG_OVERLAP)) {
+                        sv[ql[k]] = (T)(((orig[k] & E.keep) & ~(1u << p)) | (mb[k] << p));
+                    } else {
+                        const size_t byte = (size_t)ql[k] * sizeof(T);
+                        uint32_t* word = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(sv) + (byte & ~(size_t)3));
+                        const uint32_t bit = 1u << ((byte & 3) * 8 + p);
+                        if (mb[k]) atomicOr(word, bit); else atomicAnd(word, ~bit);
+                    }
+                    mapbit = ((orig[k] >> p) & 1u) ^ mb[k];
+                }
+                const u64 bal = __ballot(mapbit);
+                if ((t & 63) == 0 && (j >> 6) < E.mw) E.maps[(size_t)b * E.mw + (j >> 6)] = bal;
+            }
         }
     }
 }
@@ -1444,27 +1482,43 @@ __global__ __launch_bounds__(256) void k_restore_scalar(const T* __restrict__ st
 }
 
 // payload bits in segment order: bit j = stego bit p at the j-th window pixel
+// payload bits back out of the windows: one 1024-thread workgroup per slice, 8 bits per
+// thread per round with all loads issued first; every payload word is written (zeros past
+// total_used), so the caller needs no memset
 template <typename T>
-__global__ __launch_bounds__(256) void k_gather(const T* __restrict__ stego, long long npx,
-                                                const codec_slice_meta* __restrict__ meta,
-                                                u64* __restrict__ out, int pw) {
+__global__ __launch_bounds__(1024) void k_gather(const T* __restrict__ stego, long long npx,
+                                                 const codec_slice_meta* __restrict__ meta,
+                                                 u64* __restrict__ out, int pw) {
     __shared__ SliceWin W;
-    const int b = blockIdx.y;
+    const int b = blockIdx.x;
     load_win(meta + b, &W);
-    const int j = blockIdx.x * 256 + threadIdx.x;
-    // every word of the slice's payload row is written (zeros past total_used), so the
-    // caller needs no memset
-    if ((j >> 6) >= pw) return;
-    uint32_t bit = 0;
-    if (j < W.tot) {
-        const int p = plane_of(W, j);
-        const int i = j - W.cat[p];
-        long long q = (long long)W.off[p] + i;
-        if (q >= npx) q -= npx;
-        bit = (stego[(size_t)b * npx + q] >> p) & 1u;
+    const T* sv = stego + (size_t)b * npx;
+    const int t = threadIdx.x;
+    for (int j0 = 0; j0 < pw * 64; j0 += 8 * 1024) {
+        uint32_t v[8];
+        int pl[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int j = j0 + k * 1024 + t;
+            pl[k] = -1;
+            v[k] = 0;
+            if (j < W.tot) {
+                const int p = plane_of(W, j);
+                const int i = j - W.cat[p];
+                long long q = (long long)W.off[p] + i;
+                if (q >= npx) q -= npx;
+                pl[k] = p;
+                v[k] = sv[q];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (j0 + k * 1024 >= pw * 64) break;                 // uniform
+            const int j = j0 + k * 1024 + t;
+            const u64 bal = __ballot(pl[k] >= 0 ? (v[k] >> pl[k]) & 1u : 0u);
+            if ((t & 63) == 0 && (j >> 6) < pw) out[(size_t)b * pw + (j >> 6)] = bal;
+        }
     }
-    const u64 bal = __ballot(bit);
-    if ((threadIdx.x & 63) == 0) out[(size_t)b * pw + (j >> 6)] = bal;
 }
 
 // in-place restore: XOR every window bit with its location-map bit (only the <= T window
@@ -1481,6 +1535,11 @@ __global__ __launch_bounds__(256) void k_unxor(T* img, long long npx, const code
     const int i = j - W.cat[p];
     long long q = (long long)W.off[p] + i;
     if (q >= npx) q -= npx;
+    if (!(W.flags & CODEC_FLAG_OVERLAP)) {   // every window pixel has one owner: plain RMW
+        T* px = img + (size_t)b * npx + q;
+        *px = (T)(*px ^ (1u << p));
+        return;
+    }
     const size_t byte = ((size_t)b * npx + q) * sizeof(T);
     uint32_t* word = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(img) + (byte & ~(size_t)3));
     atomicXor(word, 1u << ((byte & 3) * 8 + p));
@@ -2063,14 +2122,13 @@ int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps
     }
     if (payload_out) {
         if (P->payload_words < 1) return set_err(CODEC_EINVAL, "payload_words must be >= 1");
-        const long long maxbits = (long long)P->payload_words * 64;
-        dim3 grid((unsigned)((maxbits + 255) / 256), P->B);
         ProfScope prof(st, CODEC_K_GATHER);
+        dim3 grid(P->B);
         if (P->in_bytes == 2)
-            hipLaunchKernelGGL(k_gather<uint16_t>, grid, dim3(256), 0, st, static_cast<const uint16_t*>(stego), npx,
+            hipLaunchKernelGGL(k_gather<uint16_t>, grid, dim3(1024), 0, st, static_cast<const uint16_t*>(stego), npx,
                                meta, reinterpret_cast<u64*>(payload_out), P->payload_words);
         else
-            hipLaunchKernelGGL(k_gather<uint8_t>, grid, dim3(256), 0, st, static_cast<const uint8_t*>(stego), npx,
+            hipLaunchKernelGGL(k_gather<uint8_t>, grid, dim3(1024), 0, st, static_cast<const uint8_t*>(stego), npx,
                                meta, reinterpret_cast<u64*>(payload_out), P->payload_words);
         LAUNCH_CHECK("k_gather");
     }
