@@ -238,3 +238,28 @@ def test_scan_sweeps_agree_with_oracle(monkeypatch, kind, h, w, sb, sweep, wgs):
     enc2 = codec.encode(buf, msgs, stego=buf)
     np.testing.assert_array_equal(buf.cpu().numpy(), stego)
     assert [r.start_offset for r in enc2.records()] == [r.start_offset for r in recs]
+
+
+@pytest.mark.parametrize("kind,h,w,chars", [("ct12", 512, 512, 3000), ("u8", 300, 200, 2600), ("ct12", 5, 24, 4),
+                                            ("ct12", 40, 8, 9), ("u16", 64, 2048, 2100)])
+def test_long_payloads_and_tiny_shapes(kind, h, w, chars, decide_path):
+    """Payloads longer than one 8192-bit round of the fused embed / gather loops, and shapes
+    with no full 16x16 block (H or W < 16): bit-exact vs the oracle, exact recovery."""
+    gen = synth.GENERATORS[kind]
+    bsz = 2
+    covers = np.stack([gen(h, w, 900 + i) for i in range(bsz)])
+    msgs = [synth.payload(chars - 3 * i, 60 + i) for i in range(bsz)]
+    codec = Codec(bsz, h, w, dtype=str(covers.dtype), beta=0.4, block=16)
+    enc = codec.encode(torch.from_numpy(covers).cuda(), msgs)
+    stego = enc.stego.cpu().numpy()
+    recs = enc.records()
+    bits, cover = K.decode(enc)
+    for i in range(bsz):
+        mb = R.message_to_bits(msgs[i])
+        exp = R.encode_slice(covers[i], mb, beta=0.4, sb=16)
+        assert recs[i].s == exp["s"] and recs[i].start_offset == exp["start_offset"]
+        np.testing.assert_array_equal(stego[i], exp["stego"])
+        n = sum(exp["segments_lengths"]) if min(exp["segments_lengths"]) >= 0 else None
+        if n == len(mb) and max(exp["segments_lengths"]) <= h * w:
+            assert framing.bits_to_str(bits[i]) == mb
+    np.testing.assert_array_equal(cover.cpu().numpy(), covers)
