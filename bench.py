@@ -79,9 +79,13 @@ def pmc_traffic(kernel: str, b: int, h: int, w: int, kind: str):
     cfg = d.get("config", {})
     if (cfg.get("batch"), cfg.get("h"), cfg.get("w"), cfg.get("kind")) != (b, h, w, kind):
         return None
-    k = d.get("kernels", {}).get(kernel)
-    if not k:
-        return None
+    ks = d.get("kernels", {})
+    k = ks.get(kernel)
+    if not k:   # keyed per template instantiation: accept the unique one of this kernel
+        hits = [v for n, v in ks.items() if n.split("<")[0] == kernel]
+        if len(hits) != 1:
+            return None
+        k = hits[0]
     return {"hbm_bytes_per_launch": k["hbm_bytes_per_launch"], "source": d.get("source", path)}
 
 

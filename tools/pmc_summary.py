@@ -24,9 +24,9 @@ vals = {}
 for C in ("FETCH_SIZE", "WRITE_SIZE"):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(os.path.join(a.src, f"pmc_{C}", "run_counter_collection.csv"))):
-        name = r["Kernel_Name"].split("(")[0].replace("void ", "")
-        if name.startswith("k_"):
-            agg[name.split("<")[0]].append(float(r["Counter_Value"]))
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "").strip()
+        if name.startswith("k_"):      # keyed per template instantiation (copy vs in place differ)
+            agg[name].append(float(r["Counter_Value"]))
     vals[C] = {k: sum(v) / len(v) for k, v in agg.items()}
 out = {"config": {"batch": a.batch, "h": a.h, "w": a.w, "kind": a.kind},
        "source": f"profiles/{a.round}/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
