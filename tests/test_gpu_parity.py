@@ -263,3 +263,28 @@ def test_long_payloads_and_tiny_shapes(kind, h, w, chars, decide_path):
         if n == len(mb) and max(exp["segments_lengths"]) <= h * w:
             assert framing.bits_to_str(bits[i]) == mb
     np.testing.assert_array_equal(cover.cpu().numpy(), covers)
+
+
+@pytest.mark.parametrize("sweep", ["0", "1"])
+def test_histogram_wraps_on_flat_slices(monkeypatch, sweep):
+    """Flat regions put > 65 535 pixels of one value into one workgroup's 16-bit LDS bin
+    halves (and equal-neighbour runs into single adds): the exact wrap bookkeeping must still
+    give the oracle's entropy / MI decisions, offsets and stego."""
+    monkeypatch.setenv("CODEC_SCAN_KIND", sweep)
+    h = w = 1024
+    a = np.full((h, w), 1234, np.uint16)                       # constant slice
+    b = synth.ct12(h, w, 5).copy()
+    b[:, : w // 2] = 0                                         # half black (air), half tissue
+    c = synth.ct12(h, w, 6).copy()
+    c[::2, ::2] = 4095                                         # a dense saturated lattice
+    covers = np.stack([a, b, c])
+    msgs = [synth.payload(300 + 50 * i, 80 + i) for i in range(3)]
+    codec = Codec(3, h, w, dtype="uint16", beta=0.4, block=16, all_mi=True)
+    enc = codec.encode(torch.from_numpy(covers).cuda(), msgs)
+    stego = enc.stego.cpu().numpy()
+    recs = enc.records()
+    for i in range(3):
+        exp = R.encode_slice(covers[i], R.message_to_bits(msgs[i]), beta=0.4, sb=16)
+        assert recs[i].s == exp["s"] and recs[i].start_offset == exp["start_offset"]
+        np.testing.assert_array_equal(stego[i], exp["stego"])
+        assert recs[i].entropy == R.entropy(covers[i])
