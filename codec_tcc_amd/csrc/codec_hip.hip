@@ -548,30 +548,48 @@ __device__ __forceinline__ void scan_rows_body(const T* __restrict__ cover, T* _
                 if (whole || i < nvec) stv<NT>(d + i, v[u]);
             }
         }
+        // block LSB counts: a lane's U vectors often sit in one block (W = 2048: rows q,
+        // q+4, q+8, q+12 of one band, same column pair), so a count is carried while the next
+        // vector's block is the same and one LDS add is issued per block change
+        int kk[U];
+        bool fl[U];
+        uint32_t on[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const long long i = base + (long long)u * NT_ + threadIdx.x;
             const bool ok = whole || i < nvec;
             uint32_t ones = ok ? lsb_count(v[u]) : 0u;
             if (ok) vor |= vor_of(v[u]);
-            // block of this vector (row is region-local)
             const int by = rr[u] >> LSB_, bx = cc[u] >> LG;
-            const bool full = ok && (band0 + by) < fullby && bx < fullbx;
-            if (DIAG == 4) {
-                vor ^= v[u].x;
-                continue;
-            }
+            fl[u] = ok && (band0 + by) < fullby && bx < fullbx;
+            kk[u] = by * fullbx + bx;
             if (grouped) {
 #pragma unroll
                 for (int o = 1; o < G; o <<= 1) ones += __shfl_xor(ones, o, 64);
-                if (full && (lane & (G - 1)) == 0) {
-                    const int k = by * fullbx + bx;
-                    atomicAdd(&cnt[k >> 1], ones << ((k & 1) * 16));
-                }
-            } else if (full && ones) {
-                const int k = by * fullbx + bx;
-                atomicAdd(&cnt[k >> 1], ones << ((k & 1) * 16));
+                fl[u] = fl[u] && (lane & (G - 1)) == 0;
             }
+            on[u] = ones;
+        }
+        if (DIAG != 4) {
+            uint32_t carry = 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!fl[u]) continue;
+                carry += on[u];
+                const bool same_next = (u + 1 < U) && fl[u + 1] && kk[u + 1] == kk[u];
+                if (!same_next && carry) {
+                    atomicAdd(&cnt[kk[u] >> 1], carry << ((kk[u] & 1) * 16));
+                    carry = 0;
+                } else if (!same_next) {
+                    carry = 0;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long i = base + (long long)u * NT_ + threadIdx.x;
+            const bool ok = whole || i < nvec;
+            if (DIAG == 4) { vor ^= v[u].x; continue; }
             if (DIAG == 0)
                 if (ok) hist_add8<T>(lds, ghist, v[u]);
         }
