@@ -1852,7 +1852,12 @@ static int launch_scan_fast(const codec_params* P, const void* cover, void* steg
     // so small regions cost more than they stream: measured 256 x 512^2 0.066 ms at one
     // workgroup per slice vs 0.108 at four; 256 x 2048^2 best at four)
     const long long slice_bytes = (long long)P->H * P->W * sizeof(T);
-    const int per_slice = (int)std::max<long long>((256 + P->B - 1) / P->B, (slice_bytes + (2 << 20) - 1) / (2 << 20));
+    // batches under 128 MiB (e.g. 1..8 slices of 2048^2): 128 workgroups in the band order
+    // measured best (1 x 2048^2: 0.020 ms vs 0.032 for the row sweep; 8 x 2048^2: 0.056 vs
+    // 0.074 at 256 workgroups)
+    const bool small = (long long)P->B * slice_bytes < (128LL << 20);
+    const int per_slice = small ? (128 + P->B - 1) / P->B
+                                : (int)std::max<long long>((256 + P->B - 1) / P->B, (slice_bytes + (2 << 20) - 1) / (2 << 20));
     const int target = (int)knob("CODEC_SCAN_WGS", (long long)per_slice * P->B);   // tools/tune.py
     const bool nt = knob("CODEC_NT", 1) != 0;
     int wgps = (target + P->B - 1) / P->B;
@@ -1867,7 +1872,7 @@ static int launch_scan_fast(const codec_params* P, const void* cover, void* steg
     // Measured (tools/tune.py): the row sweep wins for the copying scan (0.77 vs 0.80-0.83
     // ms at 256 x 2048^2), the column-band sweep for the read-only scan, which is bound by
     // LDS atomic throughput (0.54 vs 0.61 ms: concurrent waves of one band hit the same bins)
-    const long long kind = s ? knob("CODEC_SCAN_KIND", 1) : knob("CODEC_SCAN_READ_KIND", 0);
+    const long long kind = s ? knob("CODEC_SCAN_KIND", small ? 0 : 1) : knob("CODEC_SCAN_READ_KIND", 0);
     if (kind == 1 && P->W / sb <= 2 * SCAN_ROWS_CNT_WORDS) {
         // row-major sweep: bands per workgroup from CODEC_SCAN_ROWS_WGS, capped by the LDS
         // block-counter capacity

@@ -135,9 +135,12 @@ def test_kat_2048(kat, decide_path):
     np.testing.assert_array_equal(cover.cpu().numpy()[0], img)
 
 
-def test_roundtrip_full_size_batch():
+@pytest.mark.parametrize("sweep", ["0", "1"])
+def test_roundtrip_full_size_batch(monkeypatch, sweep):
     """256-slice-class property check at bench size, smaller batch: encode->decode is the
-    identity on cover and payload (size-independent property)."""
+    identity on cover and payload (size-independent property); both scan sweeps (this
+    64 MiB batch would take the band sweep by default)."""
+    monkeypatch.setenv("CODEC_SCAN_KIND", sweep)
     B, H, W = 8, 2048, 2048
     covers = torch.stack([torch.from_numpy(synth.ct12(H, W, i)) for i in range(B)]).cuda()
     msgs = [synth.payload(1024, 7 + i) for i in range(B)]
