@@ -783,7 +783,7 @@ struct ListTerm {
 };
 
 #ifdef DECIDE_TS   // diagnostic build only (tools/decide_phases.py): phase timestamps into the term scratch
-#define DTS(k) do { if (threadIdx.x == 0) reinterpret_cast<long long*>(gterms + (size_t)blockIdx.x * HistCfg<T>::kBins)[HistCfg<T>::kBins - 8 + (k)] = wall_clock64(); } while (0)
+#define DTS(k) do { if (threadIdx.x == 0) reinterpret_cast<long long*>(gterms + (size_t)blockIdx.x * HistCfg<T>::kBins)[HistCfg<T>::kBins - 16 + (k)] = wall_clock64(); } while (0)
 #else
 #define DTS(k) do { } while (0)
 #endif
@@ -970,6 +970,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
             }
         }
         __syncthreads();
+        DTS(8);
         // planes per round: enough for the usual s (5 on 12-bit data, 7 on uniform 16-bit),
         // few enough that the round's waves are not sharing SIMDs 4 to 1 (each list build and
         // sum is VALU-issue bound); H(Y) runs on the last wave meanwhile
@@ -1005,16 +1006,17 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
                             const uint32_t zy = __shfl_up(zi, o, 64), oy = __shfl_up(oi, o, 64);
                             if (lane >= o) { zi += zy; oi += oy; }
                         }
-                        const uint32_t zx = zi - zc, ox = oi - oc;
-                        const int gend = min(ngrp - blk, 64);
-                        for (int j = 0; j < gend; ++j) {
-                            const u64 mg = __shfl(mk, j, 64);
-                            const uint32_t zb = zbase + __shfl(zx, j, 64);
-                            const uint32_t ob = obase + __shfl(ox, j, 64);
-                            const int r = (blk + j) * 64 + lane;
-                            if (r < (int)m) {
-                                const bool one = (mg >> lane) & 1ull;
-                                L[one ? ob + __popcll(mg & lt) : zb + __popcll(~mg & lt)] = (uint16_t)r;
+                        if (i0 == 0 && wv == 0 && blk == 0) DTS(9);
+                        // lane j places the ranks of its own group j in order (no cross-lane
+                        // traffic: a shuffle-broadcast per group costs 4 LDS permutes)
+                        uint32_t zp = zbase + zi - zc, op = obase + oi - oc;
+                        const int r0 = g * 64;
+                        for (int e = 0; e < 64; ++e) {
+                            if (e < nr) {
+                                const bool one = (mk >> e) & 1ull;
+                                L[one ? op : zp] = (uint16_t)(r0 + e);
+                                op += one ? 1u : 0u;
+                                zp += one ? 0u : 1u;
                             }
                         }
                         zbase += __shfl(zi, 63, 64);

@@ -37,11 +37,12 @@ def main():
     cap = nby * ((W + 15) // 16)
     terms = (exact + B * cap * 8 + 255) // 256 * 256
     ws = codec.workspace.cpu().numpy()
-    raw = ws[terms: terms + B * R * 8].view(np.int64).reshape(B, R)[:, R - 8:]
+    raw = ws[terms: terms + B * R * 8].view(np.int64).reshape(B, R)[:, R - 16:]
     t = raw[:, :6]
     w0 = raw[:, 6:8]   # wave 0 (plane 0): after its H(X,Y) sum, after its joint-order list
-    print("wave0: masks+list %.2f us, sum %.2f us, then to round end %.2f us" % (
-        np.median(w0[:, 1] - raw[:, 2]) * 0.01, np.median(w0[:, 0] - w0[:, 1]) * 0.01,
+    print("wave0: masks %.2f us, counts+scans %.2f us, list %.2f us, sum %.2f us, then to round end %.2f us" % (
+        np.median(raw[:, 8] - raw[:, 2]) * 0.01, np.median(raw[:, 9] - raw[:, 8]) * 0.01,
+        np.median(w0[:, 1] - raw[:, 9]) * 0.01, np.median(w0[:, 0] - w0[:, 1]) * 0.01,
         np.median(raw[:, 3] - w0[:, 0]) * 0.01))
     d = np.diff(t, axis=1)
     names = ["pass1+scan", "terms", "H(Y)+MI", "offset argmax", "windows/meta"]
