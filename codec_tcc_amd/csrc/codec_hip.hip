@@ -1182,6 +1182,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     if constexpr (EMBED) {
         __shared__ SliceWin W;
         load_win(M, &W);                      // thread 0 wrote M; barrier inside
+        DTS(10);
         const T* cv = static_cast<const T*>(E.cover) + (size_t)b * npx;
         T* sv = static_cast<T*>(E.stego) + (size_t)b * npx;
         const u64* pay = E.payload + (size_t)b * E.pw;
@@ -1230,6 +1231,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
                 if ((t & 63) == 0 && (j >> 6) < E.mw) E.maps[(size_t)b * E.mw + (j >> 6)] = bal;
             }
         }
+        DTS(11);
     }
 }
 

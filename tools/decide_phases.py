@@ -51,6 +51,8 @@ def main():
     for n, v in zip(names, med):
         print(f"  {n:16s} {v:8.0f} ticks = {v * 0.01:7.2f} us")
     print(f"  total            {np.median(t[:, -1] - t[:, 0]) * 0.01:7.2f} us")
+    print("embed (fused): load_win %.2f us, embed loop %.2f us" % (np.median(raw[:, 10] - raw[:, 5]) * 0.01,
+                                                                np.median(raw[:, 11] - raw[:, 10]) * 0.01))
 
 
 if __name__ == "__main__":
