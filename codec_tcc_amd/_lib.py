@@ -86,6 +86,8 @@ _SIGS = {
     "codec_pee_embed": (C.c_int, [C.POINTER(PeeParams), _VP, _VP, _VP, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),
     "codec_pee_extract": (C.c_int, [C.POINTER(PeeParams), _VP, _VP, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),
     "codec_quality_moments": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP, _VP, _VP, _VP]),
+    "codec_block_variance": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP, _VP, _VP]),
+    "codec_lsb_runs": (C.c_int, [C.c_int32, C.c_int64, C.c_int32, _VP, _VP, _VP, C.c_int64, _VP, C.c_int32, _VP]),
     "codec_profile_begin": (C.c_int, [C.c_int32]),
     "codec_profile_end": (C.c_int, [_VP, _VP, C.c_int32]),
 }

@@ -12,6 +12,7 @@
 | adaptive_modalities_decomposition :561-599   | codec_plan + codec_unpack_planes        |
 | lsb_embed_multi_plane           :276-318     | codec_merge_planes + plan + embed + expand |
 | lsb_embed_block_then_multiplane :412-487     | codec_merge_planes + plan + embed + expand |
+| lsb_embed_block_adaptive        :320-410     | codec_block_variance + host sort + codec_lsb_runs |
 | merge_modalities                :215-237     | codec_merge_planes                      |
 | extract_local_planes            :789-793     | codec_unpack_planes                     |
 | decode_message                  :752-787     | codec_refdecode_dense                   |
@@ -37,6 +38,7 @@ from .framing import distribute_message_segments, message_to_bits  # noqa: F401 
 __all__ = [
     "message_to_bits", "distribute_message_segments", "calculate_entropy", "calculate_mutual_information",
     "adaptive_modalities_decomposition", "lsb_embed_multi_plane", "lsb_embed_block_then_multiplane",
+    "lsb_embed_block_adaptive",
     "merge_modalities", "extract_local_planes", "decode_message", "decode_positional",
 ]
 
@@ -193,6 +195,82 @@ def lsb_embed_block_then_multiplane(local_planes, message_bits, search_block_siz
 def lsb_embed_multi_plane(local_planes, message_bits):
     """codec.py:276-318 -> (stego_planes, bitmaps, total_used, segments_lengths, segment_indices)."""
     return _embed(local_planes, message_bits, mode="multi", block=16, align=False)
+
+
+def lsb_embed_block_adaptive(local_planes, message_bits, block_size=8):
+    """codec.py:320-410 -> (stego_planes, bitmaps, total_used, segments_lengths, segment_indices).
+
+    Every block's float(np.var(block)) comes from the device (codec_block_variance,
+    numpy-exact); each plane's blocks are ordered by a stable descending sort of those
+    scores on the host (Python's `list.sort(reverse=True)` keeps equal scores in raster
+    order, as numpy's stable argsort of the negated scores does); the segment's bits are
+    walked over the blocks in that order and the writes go back to the device as runs
+    (codec_lsb_runs).  The reference's ravel-copy quirk is reproduced: `ravel()` of a block
+    view is a view only when the block is C-contiguous (one row high, or the full image
+    width), so only those blocks are written (codec.py:383-384, 397-398), while the bits of
+    every visited block are consumed (:402) and counted in segments_lengths (:406)."""
+    _require_gpu()
+    st, shape, dt = _planes_stack(local_planes, need01=True)
+    if len(shape) != 2:
+        raise ValueError("planes must be 2-D (H, W)")
+    if any(ch not in "01" for ch in message_bits):
+        raise ValueError("message_bits must be a '0'/'1' string")
+    bs = int(block_size)
+    if bs < 1:
+        raise ValueError("block_size must be >= 1")     # range(0, h, 0) raises in the reference
+    s = st.shape[0]
+    h, w = shape
+    n = h * w
+    segments, _sizes, perm = framing.distribute_message_segments(list(local_planes), message_bits)
+    torch = _torch()
+    dev = _dev()
+    nb = st.dtype.itemsize
+    planes_t = _to_dev(st.reshape(s, n))
+    nby, nbx = -(-h // bs), -(-w // bs)
+    scores = torch.empty((s, nby * nbx), dtype=torch.float64, device=dev)
+    lib = _lib.load()
+    _lib.check(lib.codec_block_variance(s, h, w, nb, bs, planes_t.data_ptr(), scores.data_ptr(), _stream()),
+               "codec_block_variance")
+    sc = scores.cpu().numpy()
+    by, bx = np.divmod(np.arange(nby * nbx, dtype=np.int64), nbx)
+    bh = np.minimum(bs, h - by * bs)
+    bw = np.minimum(bs, w - bx * bs)
+    cap = bh * bw
+    contiguous = (bh == 1) | (bw == w)
+    first = by * bs * w + bx * bs
+    lens = [0] * s
+    used = 0
+    runs = []
+    seg_bits = np.zeros((s, max(1, max((min(len(g), n) for g in segments), default=0))), dtype=np.uint8)
+    for seg, dest in zip(segments, perm):
+        nseg = min(len(seg), n)                                       # codec.py:365
+        if nseg:
+            seg_bits[dest, :nseg] = np.frombuffer(seg[:nseg].encode("ascii"), dtype=np.uint8) - ord("0")
+        order = np.argsort(-sc[dest], kind="stable")                  # codec.py:361
+        c = cap[order]
+        before = np.cumsum(c) - c                                     # bits consumed before each block
+        visit = before < nseg                                         # codec.py:373-374
+        k = np.minimum(nseg - before[visit], c[visit])
+        cur = int(k.sum())
+        lens[dest] = cur
+        used += cur
+        o = order[visit]
+        wr = contiguous[o] & (k > 0)
+        if wr.any():
+            runs.append(np.stack([np.full(int(wr.sum()), dest, np.int64), first[o][wr], k[wr], before[visit][wr]], 1))
+    out = planes_t
+    bitmaps_t = torch.zeros((s, n), dtype=torch.uint8, device=dev)
+    if runs:
+        rr = np.ascontiguousarray(np.concatenate(runs, 0).astype(np.int64))
+        runs_t = _to_dev(rr)
+        bits_t = _to_dev(seg_bits)
+        _lib.check(lib.codec_lsb_runs(s, n, nb, out.data_ptr(), bitmaps_t.data_ptr(), bits_t.data_ptr(),
+                                      seg_bits.shape[1], runs_t.data_ptr(), rr.shape[0], _stream()), "codec_lsb_runs")
+    host_planes = out.cpu().numpy()
+    host_maps = bitmaps_t.cpu().numpy()
+    stego_planes = [host_planes[p].reshape(h, w).astype(dt, copy=False) for p in range(s)]
+    bitmaps = [host_maps[p].reshape(h, w) for p in range(s)]
+    return stego_planes, bitmaps, used, lens, list(perm)
 
 
 def merge_modalities(global_planes, local_planes) -> np.ndarray:

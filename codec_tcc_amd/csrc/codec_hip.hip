@@ -742,6 +742,27 @@ __global__ __launch_bounds__(256) void k_block_exact(const T* __restrict__ img, 
     scores[(size_t)b * cap + e] = sum / (double)n;
 }
 
+// ------------------------------------------------------------------ block-adaptive writes
+// lsb_embed_block_adaptive (codec.py:372-404): run r = {plane, first pixel, length, first
+// segment bit}; LSB := bit, bitmap := old ^ new (both as uint8, codec.py:395-399).  Runs
+// never overlap (distinct blocks of one plane), so every pixel has one writer.
+template <typename T>
+__global__ __launch_bounds__(256) void k_lsb_runs(T* __restrict__ planes, uint8_t* __restrict__ bitmaps, long long npx,
+                                                  const uint8_t* __restrict__ bits, long long bits_stride,
+                                                  const long long* __restrict__ runs) {
+    const long long* r = runs + 4 * (size_t)blockIdx.x;
+    const long long p = r[0], off = r[1], len = r[2], src = r[3];
+    T* px = planes + p * npx + off;
+    uint8_t* bm = bitmaps + p * npx + off;
+    const uint8_t* b = bits + p * bits_stride + src;
+    for (long long i = threadIdx.x; i < len; i += 256) {
+        const uint8_t old = (uint8_t)px[i];
+        const uint8_t nw = (uint8_t)((old & 0xFE) | (b[i] & 1));
+        px[i] = (T)nw;
+        bm[i] = old ^ nw;
+    }
+}
+
 // ------------------------------------------------------------------ per-slice window cache
 struct SliceWin {
     int s, tot, npix;
@@ -2287,6 +2308,47 @@ int codec_merge_planes(const codec_params* P, const void* planes, int32_t nplane
     else MRG(uint8_t, uint8_t);
 #undef MRG
     LAUNCH_CHECK("k_merge");
+    return 0;
+}
+
+int codec_block_variance(int32_t B, int32_t H, int32_t W, int32_t bytes, int32_t block, const void* planes,
+                         double* scores, void* stream) {
+    if (B < 1 || H < 1 || W < 1 || block < 1 || (bytes != 1 && bytes != 2) || !planes || !scores)
+        return set_err(CODEC_EINVAL, "codec_block_variance: bad arguments");
+    if ((long long)block * block > (1LL << 30))
+        return set_err(CODEC_EINVAL, "codec_block_variance: block too large");
+    const long long nby = (H + (long long)block - 1) / block, nbx = (W + (long long)block - 1) / block;
+    const long long cnt = nby * nbx;
+    if (cnt > INT32_MAX - 255) return set_err(CODEC_EINVAL, "codec_block_variance: too many blocks");
+    hipStream_t st = as_stream(stream);
+    dim3 grid((unsigned)((cnt + 255) / 256), (unsigned)B);
+    ProfScope prof(st, CODEC_K_BLOCK_EXACT);
+    if (bytes == 2)
+        hipLaunchKernelGGL(k_block_exact<uint16_t>, grid, dim3(256), 0, st, static_cast<const uint16_t*>(planes), H, W,
+                           block, 0, scores, (int)cnt);
+    else
+        hipLaunchKernelGGL(k_block_exact<uint8_t>, grid, dim3(256), 0, st, static_cast<const uint8_t*>(planes), H, W,
+                           block, 0, scores, (int)cnt);
+    LAUNCH_CHECK("k_block_exact");
+    return 0;
+}
+
+int codec_lsb_runs(int32_t nplanes, int64_t npx, int32_t bytes, void* planes, uint8_t* bitmaps, const uint8_t* bits,
+                   int64_t bits_stride, const int64_t* runs, int32_t nruns, void* stream) {
+    if (nplanes < 1 || npx < 1 || (bytes != 1 && bytes != 2) || !planes || !bitmaps || nruns < 0 || bits_stride < 0)
+        return set_err(CODEC_EINVAL, "codec_lsb_runs: bad arguments");
+    if (nruns == 0) return 0;
+    if (!bits || !runs) return set_err(CODEC_EINVAL, "codec_lsb_runs: bad arguments");
+    hipStream_t st = as_stream(stream);
+    ProfScope prof(st, CODEC_K_EMBED);
+    const long long* rr = reinterpret_cast<const long long*>(runs);
+    if (bytes == 2)
+        hipLaunchKernelGGL(k_lsb_runs<uint16_t>, dim3((unsigned)nruns), dim3(256), 0, st, static_cast<uint16_t*>(planes),
+                           bitmaps, (long long)npx, bits, (long long)bits_stride, rr);
+    else
+        hipLaunchKernelGGL(k_lsb_runs<uint8_t>, dim3((unsigned)nruns), dim3(256), 0, st, static_cast<uint8_t*>(planes),
+                           bitmaps, (long long)npx, bits, (long long)bits_stride, rr);
+    LAUNCH_CHECK("k_lsb_runs");
     return 0;
 }
 

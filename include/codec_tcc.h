@@ -171,6 +171,19 @@ int codec_unpack_planes(const codec_params* P, const void* img, int32_t first, i
 int codec_merge_planes(const codec_params* P, const void* planes, int32_t nplanes,
                        int32_t plane_bytes, void* out, void* stream);
 
+/* ---- lsb_embed_block_adaptive (codec.py:320-410).
+ * Step 1 (codec.py:349-358): scores[b][by*nbx+bx] = float(np.var(block)) of every
+ * block x block tile (partial at the right/bottom edges) of each of the B planes, planes
+ * [B][H][W] of `bytes` holding 0/1 values, numpy-exact (pairwise float64 order). */
+int codec_block_variance(int32_t B, int32_t H, int32_t W, int32_t bytes, int32_t block, const void* planes,
+                         double* scores, void* stream);
+/* Step 2 (codec.py:372-404), after the host's stable descending sort of each plane's
+ * scores and its walk of the blocks: runs[r] = {plane, first pixel, length, first bit}
+ * (int64 x 4, device).  planes[p][off+i] := (old & 0xFE) | bits[p*bits_stride+src+i],
+ * bitmaps[p][off+i] := old ^ new, for i < length.  Runs must not overlap. */
+int codec_lsb_runs(int32_t nplanes, int64_t npx, int32_t bytes, void* planes, uint8_t* bitmaps, const uint8_t* bits,
+                   int64_t bits_stride, const int64_t* runs, int32_t nruns, void* stream);
+
 /* ---- MED-predictor prediction-error expansion (the north star's PEE).
  * Not present in the reference: this build's own scheme, specified in
  * oracle/pee_cpu.py (parity unpinned; checked bit-exact against that spec and by

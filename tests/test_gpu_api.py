@@ -83,3 +83,55 @@ def test_errors_like_reference():
         api.adaptive_modalities_decomposition(np.zeros((4, 4), np.float32))
     with pytest.raises(ValueError):
         api.lsb_embed_block_then_multiplane([np.full((4, 4), 2, np.uint16)], "1")
+
+
+ADAPTIVE = [c for c in ALL if str(c["embedder"]) == "adaptive"]
+
+
+@pytest.mark.parametrize("case", ADAPTIVE, ids=[c["name"] for c in ADAPTIVE])
+def test_block_adaptive_matches_reference(case):
+    """lsb_embed_block_adaptive (codec.py:320-410) against the reference's own outputs,
+    ravel-copy quirk included (writes only in one-row or full-width blocks)."""
+    cover = case["cover"]
+    nb = int(case["nbits"])
+    gl, loc = api.adaptive_modalities_decomposition(cover, beta=float(case["beta"]),
+                                                    nbits=None if nb < 0 else nb)
+    st, maps, used, lens, perm = api.lsb_embed_block_adaptive(loc, _bits(case), block_size=int(case["sb"]))
+    assert used == int(case["total_used"])
+    assert lens == list(case["sizes"]) and perm == list(case["perm"])
+    np.testing.assert_array_equal(np.stack(maps, 0), golden_io.dense_bitmaps(case))
+    np.testing.assert_array_equal(api.merge_modalities(gl, st), golden_io.stego(case))
+
+
+def _rand_planes(rng, s, h, w, p_one, dtype):
+    return [(rng.random((h, w)) < p_one).astype(dtype) for _ in range(s)]
+
+
+@pytest.mark.parametrize("h,w,bs,s,nbits,p_one,dtype", [
+    (64, 64, 8, 3, 3000, 0.5, np.uint8),       # interior blocks never written (2-D views)
+    (65, 40, 8, 2, 900, 0.3, np.uint16),       # bottom block row one pixel high: written
+    (200, 6, 8, 4, 1000, 0.5, np.uint8),       # w <= block: every block full-width
+    (1, 700, 16, 2, 500, 0.5, np.uint16),      # one row
+    (33, 33, 1, 2, 2000, 0.5, np.uint8),       # 1x1 blocks: every block contiguous
+    (48, 48, 4, 3, 50000, 0.5, np.uint8),      # payload longer than every plane
+    (40, 40, 8, 2, 600, 0.0, np.uint8),        # all-zero planes: ties everywhere (stable order)
+    (37, 91, 5, 5, 4000, 0.07, np.uint16),
+    (20, 20, 8, 1, 0, 0.5, np.uint8),          # empty message
+])
+def test_block_adaptive_matches_oracle(h, w, bs, s, nbits, p_one, dtype):
+    rng = np.random.default_rng(h * 1000 + w + bs)
+    loc = _rand_planes(rng, s, h, w, p_one, dtype)
+    bits = "".join("1" if b else "0" for b in rng.integers(0, 2, nbits))
+    got = api.lsb_embed_block_adaptive(loc, bits, block_size=bs)
+    exp = R.embed_block_adaptive(loc, bits, block_size=bs)
+    assert got[2:] == exp[2:]
+    for a, b in zip(got[0], exp[0]):
+        assert a.dtype == b.dtype
+        np.testing.assert_array_equal(a, b)
+    for a, b in zip(got[1], exp[1]):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_block_adaptive_rejects_non_binary_planes():
+    with pytest.raises(ValueError):
+        api.lsb_embed_block_adaptive([np.full((4, 4), 2, np.uint8)], "1")
