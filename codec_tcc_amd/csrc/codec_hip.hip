@@ -148,6 +148,34 @@ __device__ __forceinline__ double np_sum_wave(const F& f, int m) {
     return res;
 }
 
+// The chunk trees' internal nodes, bottom-up in numpy's order, from the depth-7 slot sums
+// vals[chunk * 128 + slot] (1024 threads, m <= 8 chunks); the chunk sums are then added
+// serially.  Returns the sum to all threads.
+__device__ double np_tree_combine1024(int m, double* vals) {
+    const int t = threadIdx.x;
+    const int c = t >> 7, j = t & 127;
+    const int r = min(NP_CHUNK, max(0, m - c * NP_CHUNK));
+    for (int d = 6; d >= 0; --d) {
+        const bool act = (r > 0) && (j < (1 << d));
+        double nv = 0.0;
+        if (act) {
+            int a;
+            const int n = np_node_size(r, d, j, &a);
+            const double L = vals[c * 128 + 2 * j];
+            const double R = vals[c * 128 + 2 * j + 1];
+            nv = (n > NP_LEAF) ? (L + R) : L;
+        }
+        __syncthreads();
+        if (act) vals[c * 128 + j] = nv;
+        __syncthreads();
+    }
+    double res = -0.0;
+    const int nchunks = (m + NP_CHUNK - 1) / NP_CHUNK;
+    for (int k = 0; k < nchunks; ++k) res += vals[k * 128];
+    __syncthreads();
+    return res;
+}
+
 // np.sum semantics over m <= 65536 elements, computed by a 1024-thread block.
 // Slot t = (chunk t/128, bottom slot t%128 of that chunk's depth-7 tree); leaves reached
 // above depth 7 are carried down the left spine.  Leaves are summed wave-cooperatively:
@@ -196,27 +224,160 @@ __device__ double np_sum_block1024(const F& f, int m, double* vals /*[1024]*/) {
         }
     }
     __syncthreads();
-    const int c = t >> 7, j = t & 127;
-    const int r = min(NP_CHUNK, max(0, m - c * NP_CHUNK));
-    for (int d = 6; d >= 0; --d) {
-        const bool act = (r > 0) && (j < (1 << d));
-        double nv = 0.0;
-        if (act) {
-            int a;
-            const int n = np_node_size(r, d, j, &a);
-            const double L = vals[c * 128 + 2 * j];
-            const double R = vals[c * 128 + 2 * j + 1];
-            nv = (n > NP_LEAF) ? (L + R) : L;
-        }
-        __syncthreads();
-        if (act) vals[c * 128 + j] = nv;
-        __syncthreads();
+    return np_tree_combine1024(m, vals);
+}
+
+// ---- wide slices (k_decide's walk path): the non-zero bins of a slice are kept as 64-bin
+// group masks nz[g] (bin v = 64 g + e) and per-bin count codes cv[v] (the count if below
+// kTermCodes, else kBigCode); a term is tc[code] (p * log2 p of that count, computed once
+// per slice) or, for big counts, computed from the histogram.  The k-th element of a
+// plane's joint order (codec.py:546-551: bit-clear bins ascending, then bit-set bins) is
+// reached by walking the group masks, so neither a rank list nor a term array is stored.
+constexpr int kTermCodes = 1024;
+constexpr uint16_t kBigCode = 0xFFFF;
+// LDS slot of bin v's code: bits 1..6 XOR-swizzled with bits 7..12, so that the leaves'
+// walkers (128 positions apart) read different banks
+__device__ __forceinline__ int cv_slot(int v) { return v ^ (((v >> 7) & 63) << 1); }
+
+struct JointWalk {
+    const u64* nz;
+    const uint16_t* cv;
+    const double* tc;
+    const uint32_t* hist;
+    const double* lut;
+    double N;
+    int plane;      // -1: identity order (all bins in half 0)
+    int ng;         // groups
+    u64 lm;         // plane < 6: the lanes e of a group whose bit `plane` is set
+    int h, g;
+    u64 mk;         // bins of (h, g) still to visit
+    __device__ void init(int pl) {
+        plane = pl;
+        lm = 0;
+        if (pl >= 0 && pl < 6)
+            for (int e = 0; e < 64; ++e) lm |= (u64)((e >> pl) & 1) << e;
     }
-    double res = -0.0;
-    const int nchunks = (m + NP_CHUNK - 1) / NP_CHUNK;
-    for (int k = 0; k < nchunks; ++k) res += vals[k * 128];
+    __device__ __forceinline__ u64 mask(int hh, int gg) const {
+        const u64 w = nz[gg];
+        if (plane < 0) return hh ? 0ull : w;
+        if (plane >= 6) return ((((gg << 6) >> plane) & 1) == hh) ? w : 0ull;
+        return hh ? (w & lm) : (w & ~lm);
+    }
+    // the next bin of the order (-1 past the end: never for a valid leaf)
+    __device__ __forceinline__ int nextv() {
+        while (!mk) {
+            if (++g == ng) {
+                g = 0;
+                if (++h > 1) return -1;
+            }
+            mk = mask(h, g);
+        }
+        const int e = __ffsll((long long)mk) - 1;
+        mk &= mk - 1;
+        return (g << 6) + e;
+    }
+    __device__ __forceinline__ double term(int v, uint16_t c) const {
+        if (v < 0) return 0.0;
+        if (c != kBigCode) return tc[c];
+        const uint32_t n = hist[v];
+        const double p = (double)n / N;
+        return p * lut[n - 1];
+    }
+    // the next 8 terms: bins, then their codes, then the table terms (loads batched), big
+    // counts patched afterwards (rare)
+    __device__ __forceinline__ void next8(double* tv) {
+        int v[8];
+        uint32_t c[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = nextv();
+#pragma unroll
+        for (int q = 0; q < 8; ++q) c[q] = cv[cv_slot(v[q] & 0xFFFF)];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) tv[q] = tc[c[q] & (kTermCodes - 1)];
+        bool big = false;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) big |= c[q] == kBigCode || v[q] < 0;
+        if (big) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (c[q] == kBigCode || v[q] < 0) tv[q] = term(v[q], (uint16_t)c[q]);
+        }
+    }
+    __device__ __forceinline__ double next() {
+        const int v = nextv();
+        return term(v, v >= 0 ? cv[cv_slot(v)] : (uint16_t)0);
+    }
+};
+
+// np.sum of one plane's joint order (or the identity order) over the m non-zero bins of a
+// wide slice, 1024 threads: group counts of each half are scanned into start positions
+// (kept in `vals`, free until the leaves are written), every depth-7 slot (one per thread)
+// finds its first element by binary search and walks its leaf with numpy's 8 accumulators,
+// then np_tree_combine1024.  Returns the sum to all threads.
+#ifdef DECIDE_TS
+#define WTS(k) do { if (threadIdx.x == 0 && wts) wts[k] = wall_clock64(); } while (0)
+#else
+#define WTS(k) do { } while (0)
+#endif
+__device__ __forceinline__ double np_sum_walk1024(JointWalk wk, int m, double* vals, uint32_t* sh, long long* wts) {
+    const int t = threadIdx.x;
+    uint32_t c0 = 0, c1 = 0;
+    if (t < wk.ng) {
+        c1 = (uint32_t)__popcll(wk.mask(1, t));
+        c0 = (uint32_t)__popcll(wk.mask(0, t));
+    }
+    uint32_t z, tot1;
+    const uint32_t p0 = block_excl_scan<1024>(c0, sh, &z);
+    const uint32_t p1 = block_excl_scan<1024>(c1, sh, &tot1) + z;
+    uint32_t* P0 = reinterpret_cast<uint32_t*>(vals);
+    uint32_t* P1 = P0 + 1024;
+    if (t < wk.ng) { P0[t] = p0; P1[t] = p1; }
     __syncthreads();
-    return res;
+    WTS(0);
+    // even depth-7 slots on threads 0..511, odd ones on 512..1023: a full chunk's leaves are
+    // its even slots, so the walking lanes are packed into half the waves
+    const int c = (t >> 6) & 7, j = 2 * (t & 63) + (t >> 9);
+    const int r = min(NP_CHUNK, max(0, m - c * NP_CHUNK));
+    int a = 0, n = 0;
+    if (r > 0) n = np_node_size(r, 7, j, &a);
+    a += c * NP_CHUNK;
+    if (n > 0) {                                  // seek position a
+        const int hh = (uint32_t)a >= z ? 1 : 0;
+        const uint32_t* Pp = hh ? P1 : P0;
+        int lo = 0, hi = wk.ng - 1;               // last group starting at or before a
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (Pp[mid] <= (uint32_t)a) lo = mid; else hi = mid - 1;
+        }
+        u64 mk = wk.mask(hh, lo);
+        for (uint32_t k = (uint32_t)a - Pp[lo]; k > 0; --k) mk &= mk - 1;
+        wk.h = hh; wk.g = lo; wk.mk = mk;
+    }
+    __syncthreads();                              // P0/P1 read; vals free again
+    WTS(1);
+    double res = 0.0;
+    if (n >= 8) {                                 // numpy's leaf: 8 accumulators, then the tail
+        double acc[8];
+        wk.next8(acc);
+        const int lim = n - (n % 8);
+        for (int i = 8; i < lim; i += 8) {
+            double tv[8];
+            wk.next8(tv);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[q] += tv[q];
+        }
+        res = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+        for (int i = lim; i < n; ++i) res += wk.next();
+    } else if (n > 0) {
+        res = -0.0;
+        for (int i = 0; i < n; ++i) res += wk.next();
+    }
+    vals[c * 128 + j] = n > 0 ? res : 0.0;
+    __syncthreads();
+    WTS(2);
+    const double sum = np_tree_combine1024(m, vals);
+    WTS(3);
+    return sum;
 }
 
 // ------------------------------------------------------------------ histogram helpers
@@ -869,6 +1030,10 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     __shared__ int best_ix[16];
     __shared__ double hxy_sh[16], hx_sh[16], hy_sh;
     __shared__ int ctl_sh[4];
+    // walk path (wide 16-bit slices): non-zero masks per 64-bin group, terms by count
+    constexpr bool kWideT = sizeof(T) == 2;
+    __shared__ u64 nzs[kWideT ? R / 64 : 1];
+    __shared__ double tcs[kWideT ? kTermCodes : 1];
 
     const int b = blockIdx.x;
     const int t = threadIdx.x;
@@ -891,7 +1056,38 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     uint32_t pop[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) pop[i] = 0;
-    for (int k0 = 0; k0 < bpt; k0 += 16) {
+    // wide slices (>= 16384 possible values): coalesced pass, one 64-bin group per wave
+    // step, writing the group masks and the count codes (into the `list` arena) as well
+    const bool wide = kWideT && Rp >= 16384 && !(P.reserved & 3);
+    if (wide) {
+        const int lane = t & 63, wv = t >> 6;
+        for (int g0 = wv; g0 < Rp / 64; g0 += 16 * 8) {       // 8 group loads in flight
+            uint32_t cc[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int g = g0 + 16 * u;
+                cc[u] = g < Rp / 64 ? hist[(g << 6) + lane] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int g = g0 + 16 * u;
+                if (g >= Rp / 64) break;                          // uniform
+                const int v = (g << 6) + lane;
+                const uint32_t c = cc[u];
+                list[cv_slot(v)] = c < (uint32_t)kTermCodes ? (uint16_t)c : kBigCode;
+                const u64 bm = __ballot(c != 0u);
+                if (lane == 0) nzs[g] = bm;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) pop[i] += ((v >> i) & 1) ? c : 0u;
+            }
+        }
+        for (int c = t; c < kTermCodes; c += 1024)
+            tcs[c] = (c >= 1 && (long long)c <= npx && lut_len >= c) ? plogp(lut, (uint32_t)c, Nd) : 0.0;
+        __syncthreads();
+        const u64 w = nzs[v0 >> 6];
+        nzmask = bpt == 64 ? w : (w >> (v0 & 63)) & ((1ull << bpt) - 1);
+    }
+    for (int k0 = 0; k0 < bpt && !wide; k0 += 16) {
         uint32_t cc[16];
 #pragma unroll
         for (int u = 0; u < 16; ++u) {            // 16 loads in flight, then the adds
@@ -930,13 +1126,14 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     const size_t off_jl = off_pm + (size_t)ngrp * 128;
     const int wplanes = (m > 1 && off_jl + 2 * (size_t)m <= arena) ? (int)min((size_t)16, (arena - off_jl) / (2 * (size_t)m)) : 0;
     const bool wfast = lut_ok && wplanes >= 1 && knob_dev_decide_fast(P);
+    const bool walk = wide && lut_ok && !wfast && m > 1;
     double* tl = reinterpret_cast<double*>(list);
     uint16_t* rv = reinterpret_cast<uint16_t*>(tl + (wfast ? m : 0));
     u64* pm = reinterpret_cast<u64*>(reinterpret_cast<char*>(list) + off_pm);
     uint16_t* jl = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(list) + off_jl);
     if (wfast) terms = tl;
     // terms of the non-zero bins in ascending value order, computed once
-    if (lut_ok) {
+    if (lut_ok && !walk) {
         uint32_t r = rank0;
         u64 msk = nzmask;
         while (msk) {
@@ -1081,17 +1278,53 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
         }
         Hy = hy_sh;
     }
-    if (lut_ok && !wfast) Hy = -np_sum_block1024(RankTerm{terms}, (int)m, vals);
+    if (walk) {
+        // joint orders walked from the group masks (np_sum_walk1024): H(Y) (i = -1), then
+        // the planes in sequence (one call site, so the walk inlines once)
+        JointWalk wk{nzs, list, tcs, hist, lut, Nd, -1, Rp / 64, 0, 0, 0, 0ull};
+        double tg = 0.0;
+        for (int i = -1; i < P.nbits && i < 16; ++i) {
+            if (i >= 0 && !(need_decision && !decided) && !P.all_mi) break;
+            const uint32_t pp = i >= 0 ? pops_sh[i] : 0u;
+            const bool run = i < 0 || (pp != 0 && (long long)pp != npx);   // codec.py:520-523
+            double h = 0.0;
+            if (run) {
+                wk.init(i);
+#ifdef DECIDE_TS
+                long long* wts = i == 0 ? reinterpret_cast<long long*>(gterms + (size_t)b * R) + R - 4 : nullptr;
+#else
+                long long* wts = nullptr;
+#endif
+                h = -np_sum_walk1024(wk, (int)m, vals, sh, wts);
+            }
+            if (i < 0) { Hy = h; tg = P.beta * Hy; DTS(6); continue; }
+            if (i == 0) DTS(7);
+            double mi = 0.0;
+            if (run) {
+                const double hx = -(plogp(lut, (uint32_t)(npx - pp), Nd) + plogp(lut, pp, Nd));
+                mi = (hx + Hy) - h;                              // codec.py:554
+                if (!(mi > 0.0)) mi = 0.0;
+            }
+            if (t == 0) mis_sh[i] = mi;
+            if (need_decision && !decided) {
+                cum += mi;
+                if (cum >= tg) { s = i + 1; decided = true; }
+            }
+        }
+    }
+    if (lut_ok && !wfast && !walk) Hy = -np_sum_block1024(RankTerm{terms}, (int)m, vals);
     const double target = P.beta * Hy;
 
     // ---- the s decision (codec.py:580-593)
-    for (int i = 0; i < P.nbits && i < 16 && lut_ok && !wfast; ++i) {
+    for (int i = 0; i < P.nbits && i < 16 && lut_ok && !wfast && !walk; ++i) {
         if (!(need_decision && !decided) && !P.all_mi) break;
         const uint32_t pp = pops_sh[i];
         double mi = 0.0;
         if (m > 1 && pp != 0 && (long long)pp != npx) {          // codec.py:520-523
             build_joint_order(nzmask, v0, rank0, i, list, sh);
+            if (i == 0) DTS(6);
             const double hxy = -np_sum_block1024(ListTerm{terms, list}, (int)m, vals);
+            if (i == 0) DTS(7);
             const double hx = -(plogp(lut, (uint32_t)(npx - pp), Nd) + plogp(lut, pp, Nd));
             mi = (hx + Hy) - hxy;                                // codec.py:554
             if (!(mi > 0.0)) mi = 0.0;                           // max(0.0, mi)
@@ -2028,7 +2261,8 @@ static int plan_impl(const codec_params* P, const void* cover, void* stego, cons
         LAUNCH_CHECK("k_block_exact");
     }
     codec_params Pv = *P;
-    Pv.reserved = knob("CODEC_DECIDE_WAVES", 1) ? 0 : 1;   // bit 0: force the block-sequential decision
+    // bit 0: force the block-sequential decision; bit 1: no walk path for wide slices
+    Pv.reserved = (knob("CODEC_DECIDE_WAVES", 1) ? 0 : 1) | (knob("CODEC_DECIDE_WALK", 1) ? 0 : 2);
     ProfScope prof(st, E ? CODEC_K_DECIDE_EMBED : CODEC_K_DECIDE);
     const EmbedArgs Ev = E ? *E : EmbedArgs{nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
 #define DEC(TT, EM) hipLaunchKernelGGL((k_decide<TT, EM>), dim3(P->B), dim3(1024), 0, st, Pv, hist, orv, terms, keys, exact, \

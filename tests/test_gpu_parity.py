@@ -291,3 +291,40 @@ def test_histogram_wraps_on_flat_slices(monkeypatch, sweep):
         assert recs[i].s == exp["s"] and recs[i].start_offset == exp["start_offset"]
         np.testing.assert_array_equal(stego[i], exp["stego"])
         assert recs[i].entropy == R.entropy(covers[i])
+
+
+def _wide_cover(kind, h, w, seed):
+    rng = np.random.default_rng(seed)
+    if kind == "dense":                       # every 16-bit value present, small counts
+        return rng.integers(0, 65536, (h, w)).astype(np.uint16)
+    if kind == "sparse":                      # ~12k distinct values spread over the range
+        vals = np.sort(rng.choice(65536, 12000, replace=False)).astype(np.uint16)
+        return vals[rng.integers(0, vals.size, (h, w))]
+    if kind == "bigcounts":                   # half the pixels on 10 values (counts >> 1024)
+        img = rng.integers(0, 65536, (h, w)).astype(np.uint16)
+        mask = rng.random((h, w)) < 0.5
+        img[mask] = rng.choice(np.array([0, 1, 7, 1000, 4095, 4096, 30000, 32768, 65534, 65535], np.uint16),
+                               int(mask.sum()))
+        return img
+    if kind == "halfrange":                   # values < 32768 (Rp = 32768, 32 bins per thread)
+        return rng.integers(0, 32768, (h, w)).astype(np.uint16)
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind,h,w", [("dense", 512, 512), ("sparse", 384, 512), ("bigcounts", 512, 512),
+                                      ("halfrange", 300, 700), ("dense", 97, 211)])
+def test_wide_slices_information_exact(kind, h, w, decide_path):
+    """Slices with too many distinct values for the wave path's LDS arena: k_decide's walk
+    path (default) and the block path agree with numpy's entropy / MI bit for bit."""
+    cover = _wide_cover(kind, h, w, 5)
+    codec = Codec(1, h, w, dtype="uint16", beta=0.8, block=16, all_mi=True)
+    enc = codec.encode(torch.from_numpy(cover[None].copy()).cuda(), [synth.payload(100, 1)])
+    m = enc.records()[0]
+    assert m.status == 0
+    assert m.nonzero_bins == np.unique(cover).size
+    assert m.entropy == R.entropy(cover)
+    for i in range(16):
+        assert m.mi[i] == R.mutual_information((cover >> i) & 1, cover), i
+    exp = R.encode_slice(cover, R.message_to_bits(synth.payload(100, 1)), beta=0.8, sb=16)
+    assert m.s == exp["s"]
+    np.testing.assert_array_equal(enc.stego.cpu().numpy()[0], exp["stego"])
