@@ -233,7 +233,7 @@ __device__ double np_sum_block1024(const F& f, int m, double* vals /*[1024]*/) {
 // per slice) or, for big counts, computed from the histogram.  The k-th element of a
 // plane's joint order (codec.py:546-551: bit-clear bins ascending, then bit-set bins) is
 // reached by walking the group masks, so neither a rank list nor a term array is stored.
-constexpr int kTermCodes = 1024;
+constexpr int kTermCodes = 512;
 constexpr uint16_t kBigCode = 0xFFFF;
 // LDS slot of bin v's code: bits 1..6 XOR-swizzled with bits 7..12, so that the leaves'
 // walkers (128 positions apart) read different banks
@@ -309,54 +309,10 @@ struct JointWalk {
     }
 };
 
-// np.sum of one plane's joint order (or the identity order) over the m non-zero bins of a
-// wide slice, 1024 threads: group counts of each half are scanned into start positions
-// (kept in `vals`, free until the leaves are written), every depth-7 slot (one per thread)
-// finds its first element by binary search and walks its leaf with numpy's 8 accumulators,
-// then np_tree_combine1024.  Returns the sum to all threads.
-#ifdef DECIDE_TS
-#define WTS(k) do { if (threadIdx.x == 0 && wts) wts[k] = wall_clock64(); } while (0)
-#else
-#define WTS(k) do { } while (0)
-#endif
-__device__ __forceinline__ double np_sum_walk1024(JointWalk wk, int m, double* vals, uint32_t* sh, long long* wts) {
-    const int t = threadIdx.x;
-    uint32_t c0 = 0, c1 = 0;
-    if (t < wk.ng) {
-        c1 = (uint32_t)__popcll(wk.mask(1, t));
-        c0 = (uint32_t)__popcll(wk.mask(0, t));
-    }
-    uint32_t z, tot1;
-    const uint32_t p0 = block_excl_scan<1024>(c0, sh, &z);
-    const uint32_t p1 = block_excl_scan<1024>(c1, sh, &tot1) + z;
-    uint32_t* P0 = reinterpret_cast<uint32_t*>(vals);
-    uint32_t* P1 = P0 + 1024;
-    if (t < wk.ng) { P0[t] = p0; P1[t] = p1; }
-    __syncthreads();
-    WTS(0);
-    // even depth-7 slots on threads 0..511, odd ones on 512..1023: a full chunk's leaves are
-    // its even slots, so the walking lanes are packed into half the waves
-    const int c = (t >> 6) & 7, j = 2 * (t & 63) + (t >> 9);
-    const int r = min(NP_CHUNK, max(0, m - c * NP_CHUNK));
-    int a = 0, n = 0;
-    if (r > 0) n = np_node_size(r, 7, j, &a);
-    a += c * NP_CHUNK;
-    if (n > 0) {                                  // seek position a
-        const int hh = (uint32_t)a >= z ? 1 : 0;
-        const uint32_t* Pp = hh ? P1 : P0;
-        int lo = 0, hi = wk.ng - 1;               // last group starting at or before a
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (Pp[mid] <= (uint32_t)a) lo = mid; else hi = mid - 1;
-        }
-        u64 mk = wk.mask(hh, lo);
-        for (uint32_t k = (uint32_t)a - Pp[lo]; k > 0; --k) mk &= mk - 1;
-        wk.h = hh; wk.g = lo; wk.mk = mk;
-    }
-    __syncthreads();                              // P0/P1 read; vals free again
-    WTS(1);
+// numpy's pairwise leaf over n elements of a walk (8 accumulators, then the tail)
+__device__ __forceinline__ double np_leaf_walk(JointWalk& wk, int n) {
     double res = 0.0;
-    if (n >= 8) {                                 // numpy's leaf: 8 accumulators, then the tail
+    if (n >= 8) {
         double acc[8];
         wk.next8(acc);
         const int lim = n - (n % 8);
@@ -372,12 +328,114 @@ __device__ __forceinline__ double np_sum_walk1024(JointWalk wk, int m, double* v
         res = -0.0;
         for (int i = 0; i < n; ++i) res += wk.next();
     }
-    vals[c * 128 + j] = n > 0 ? res : 0.0;
+    return res;
+}
+
+// np.sum of TWO orders at once (a plane's joint order, or the identity order) over the
+// m0 / m1 non-zero bins of a wide slice (m = 0: order not summed), 1024 threads, order o
+// on threads 512 o .. 512 o + 511.  The group counts of both halves of both orders are
+// scanned (packed, one 64-bit scan per half) into start positions, kept in `vals` as u16
+// deficits 64 g - prefix (a prefix never exceeds 64 g); each thread then seeks its two
+// depth-7 slots (even j, then odd j: a full chunk's leaves are its even slots) by binary
+// search, walks the leaves and the chunk trees are combined per order.  vals: 2048 doubles.
+#ifdef DECIDE_TS
+#define WTS(k) do { if (threadIdx.x == 0 && wts) wts[k] = wall_clock64(); } while (0)
+#else
+#define WTS(k) do { } while (0)
+#endif
+__device__ __forceinline__ void np_sum_walk2(JointWalk wk, int pl0, int m0, int pl1, int m1, double* vals,
+                                             u64* sh64, double* out, long long* wts) {
+    const int t = threadIdx.x;
+    const int ng = wk.ng;
+    u64 xz = 0, xo = 0;
+    if (t < ng) {
+        wk.init(pl0);
+        if (m0) { xz |= (u64)__popcll(wk.mask(0, t)); xo |= (u64)__popcll(wk.mask(1, t)); }
+        wk.init(pl1);
+        if (m1) { xz |= (u64)__popcll(wk.mask(0, t)) << 32; xo |= (u64)__popcll(wk.mask(1, t)) << 32; }
+    }
+    u64 tz, tone;
+    const u64 pz = block_excl_scan64<1024>(xz, sh64, &tz);
+    const u64 po = block_excl_scan64<1024>(xo, sh64, &tone);
+    uint16_t* D = reinterpret_cast<uint16_t*>(vals);          // [order][half][1024]
+    if (t < ng) {
+        const uint32_t base = 64u * (uint32_t)t;
+        D[t] = (uint16_t)(base - (uint32_t)pz);
+        D[1024 + t] = (uint16_t)(base - (uint32_t)po);
+        D[2048 + t] = (uint16_t)(base - (uint32_t)(pz >> 32));
+        D[3072 + t] = (uint16_t)(base - (uint32_t)(po >> 32));
+    }
+    __syncthreads();
+    WTS(0);
+    const int o = t >> 9, tt = t & 511;
+    wk.init(o ? pl1 : pl0);
+    const int m = o ? m1 : m0;
+    const uint32_t z = o ? (uint32_t)(tz >> 32) : (uint32_t)tz;
+    int cs[2], js[2], ns[2], hs[2] = {0, 0}, gs[2] = {0, 0};
+    u64 mks[2] = {0ull, 0ull};
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+        const int c = tt >> 6, j = 2 * (tt & 63) + sl;
+        const int r = min(NP_CHUNK, max(0, m - c * NP_CHUNK));
+        int a = 0, n = 0;
+        if (r > 0) n = np_node_size(r, 7, j, &a);
+        a += c * NP_CHUNK;
+        cs[sl] = c; js[sl] = j; ns[sl] = n;
+        if (n > 0) {                              // seek position a
+            const int hh = (uint32_t)a >= z ? 1 : 0;
+            const uint16_t* Dp = D + o * 2048 + hh * 1024;
+            const uint32_t base = hh ? z : 0u;
+            int lo = 0, hi = ng - 1;              // last group starting at or before a
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (base + 64u * (uint32_t)mid - Dp[mid] <= (uint32_t)a) lo = mid; else hi = mid - 1;
+            }
+            u64 mk = wk.mask(hh, lo);
+            for (uint32_t k = (uint32_t)a - (base + 64u * (uint32_t)lo - Dp[lo]); k > 0; --k) mk &= mk - 1;
+            hs[sl] = hh; gs[sl] = lo; mks[sl] = mk;
+        }
+    }
+    __syncthreads();                              // deficits read; vals free again
+    WTS(1);
+    double* vo = vals + o * 1024;
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+        double res = 0.0;
+        if (ns[sl] > 0) {
+            wk.h = hs[sl]; wk.g = gs[sl]; wk.mk = mks[sl];
+            res = np_leaf_walk(wk, ns[sl]);
+        }
+        vo[cs[sl] * 128 + js[sl]] = ns[sl] > 0 ? res : 0.0;
+    }
     __syncthreads();
     WTS(2);
-    const double sum = np_tree_combine1024(m, vals);
+    {   // both orders' chunk trees (np_tree_combine1024's order), 64 threads per chunk
+        const int c = (t >> 6) & 7, j = t & 63;
+        const int r = min(NP_CHUNK, max(0, m - c * NP_CHUNK));
+        for (int d = 6; d >= 0; --d) {
+            const bool act = (r > 0) && (j < (1 << d));
+            double nv = 0.0;
+            if (act) {
+                int a;
+                const int n = np_node_size(r, d, j, &a);
+                const double L = vo[c * 128 + 2 * j];
+                const double R = vo[c * 128 + 2 * j + 1];
+                nv = (n > NP_LEAF) ? (L + R) : L;
+            }
+            __syncthreads();
+            if (act) vo[c * 128 + j] = nv;
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int mq = q ? m1 : m0;
+        double res = -0.0;
+        for (int k = 0; k < (mq + NP_CHUNK - 1) / NP_CHUNK; ++k) res += vals[q * 1024 + k * 128];
+        out[q] = res;
+    }
+    __syncthreads();
     WTS(3);
-    return sum;
 }
 
 // ------------------------------------------------------------------ histogram helpers
@@ -1022,8 +1080,9 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     // `list` doubles as the wave-parallel path's arena: terms (8m B), rank -> value (2m B),
     // one joint-order list per plane in flight (2m B each)
     __shared__ __align__(16) uint16_t list[R];
-    __shared__ double vals[1024];
+    __shared__ double vals[sizeof(T) == 2 ? 2048 : 1024];   // 2048: the walk path's two orders
     __shared__ uint32_t sh[20];
+    __shared__ u64 sh64[17];
     __shared__ uint32_t pops_sh[16];
     __shared__ double mis_sh[16];
     __shared__ double best_sc[16];
@@ -1061,26 +1120,36 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     const bool wide = kWideT && Rp >= 16384 && !(P.reserved & 3);
     if (wide) {
         const int lane = t & 63, wv = t >> 6;
-        for (int g0 = wv; g0 < Rp / 64; g0 += 16 * 8) {       // 8 group loads in flight
-            uint32_t cc[8];
+        // bin v = 64 g + lane, g = wv + 16 k: plane bits 0..5 are the lane's, 6..9 the
+        // wave's, 10..15 those of k; only the lane total and the 6 k-bit sums are kept
+        uint32_t tot = 0, pk[6] = {0, 0, 0, 0, 0, 0};
+        const int ng = Rp / 64;
+        for (int k0 = 0; wv + 16 * k0 < ng; k0 += 16) {       // 16 group loads in flight
+            uint32_t cc[16];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int g = g0 + 16 * u;
-                cc[u] = g < Rp / 64 ? hist[(g << 6) + lane] : 0u;
+            for (int u = 0; u < 16; ++u) {
+                const int g = wv + 16 * (k0 + u);
+                cc[u] = g < ng ? hist[(g << 6) + lane] : 0u;
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int g = g0 + 16 * u;
-                if (g >= Rp / 64) break;                          // uniform
-                const int v = (g << 6) + lane;
+            for (int u = 0; u < 16; ++u) {
+                const int k = k0 + u, g = wv + 16 * k;
+                if (g >= ng) break;                               // uniform
                 const uint32_t c = cc[u];
-                list[cv_slot(v)] = c < (uint32_t)kTermCodes ? (uint16_t)c : kBigCode;
+                list[cv_slot((g << 6) + lane)] = c < (uint32_t)kTermCodes ? (uint16_t)c : kBigCode;
                 const u64 bm = __ballot(c != 0u);
                 if (lane == 0) nzs[g] = bm;
+                tot += c;
 #pragma unroll
-                for (int i = 0; i < 16; ++i) pop[i] += ((v >> i) & 1) ? c : 0u;
+                for (int q = 0; q < 6; ++q) pk[q] += ((k >> q) & 1) ? c : 0u;
             }
         }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) pop[i] = ((lane >> i) & 1) ? tot : 0u;
+#pragma unroll
+        for (int i = 6; i < 10; ++i) pop[i] = ((wv >> (i - 6)) & 1) ? tot : 0u;
+#pragma unroll
+        for (int i = 10; i < 16; ++i) pop[i] = pk[i - 10];
         for (int c = t; c < kTermCodes; c += 1024)
             tcs[c] = (c >= 1 && (long long)c <= npx && lut_len >= c) ? plogp(lut, (uint32_t)c, Nd) : 0.0;
         __syncthreads();
@@ -1279,37 +1348,47 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
         Hy = hy_sh;
     }
     if (walk) {
-        // joint orders walked from the group masks (np_sum_walk1024): H(Y) (i = -1), then
-        // the planes in sequence (one call site, so the walk inlines once)
-        JointWalk wk{nzs, list, tcs, hist, lut, Nd, -1, Rp / 64, 0, 0, 0, 0ull};
+        // joint orders walked from the group masks, two per np_sum_walk2: (H(Y), plane 0),
+        // (1, 2), (3, 4), ...; the planes are then taken in order as the sequential loop does
+        const JointWalk w0{nzs, list, tcs, hist, lut, Nd, -1, Rp / 64, 0, 0, 0, 0ull};
         double tg = 0.0;
-        for (int i = -1; i < P.nbits && i < 16; ++i) {
-            if (i >= 0 && !(need_decision && !decided) && !P.all_mi) break;
-            const uint32_t pp = i >= 0 ? pops_sh[i] : 0u;
-            const bool run = i < 0 || (pp != 0 && (long long)pp != npx);   // codec.py:520-523
-            double h = 0.0;
-            if (run) {
-                wk.init(i);
+        const int nb = min(P.nbits, 16);
+        bool stop = false;
+        for (int i0 = -1; i0 < nb && !stop; i0 += 2) {
+            if (i0 >= 0 && !(need_decision && !decided) && !P.all_mi) break;
+            int run[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int i = i0 + q;
+                const uint32_t pp = (i >= 0 && i < nb) ? pops_sh[i] : 0u;
+                run[q] = i < 0 || (i < nb && pp != 0 && (long long)pp != npx);   // codec.py:520-523
+            }
 #ifdef DECIDE_TS
-                long long* wts = i == 0 ? reinterpret_cast<long long*>(gterms + (size_t)b * R) + R - 4 : nullptr;
+            long long* wts = i0 < 0 ? reinterpret_cast<long long*>(gterms + (size_t)b * R) + R - 4 : nullptr;
 #else
-                long long* wts = nullptr;
+            long long* wts = nullptr;
 #endif
-                h = -np_sum_walk1024(wk, (int)m, vals, sh, wts);
+            double hs2[2];
+            np_sum_walk2(w0, i0, run[0] ? (int)m : 0, i0 + 1, run[1] ? (int)m : 0, vals, sh64, hs2, wts);
+            for (int q = 0; q < 2; ++q) {
+                const int i = i0 + q;
+                if (i >= nb) break;
+                if (i < 0) { Hy = -hs2[0]; tg = P.beta * Hy; DTS(6); continue; }
+                if (!(need_decision && !decided) && !P.all_mi) { stop = true; break; }
+                const uint32_t pp = pops_sh[i];
+                double mi = 0.0;
+                if (run[q]) {
+                    const double hx = -(plogp(lut, (uint32_t)(npx - pp), Nd) + plogp(lut, pp, Nd));
+                    mi = (hx + Hy) - (-hs2[q]);                  // codec.py:554
+                    if (!(mi > 0.0)) mi = 0.0;
+                }
+                if (t == 0) mis_sh[i] = mi;
+                if (need_decision && !decided) {
+                    cum += mi;
+                    if (cum >= tg) { s = i + 1; decided = true; }
+                }
             }
-            if (i < 0) { Hy = h; tg = P.beta * Hy; DTS(6); continue; }
-            if (i == 0) DTS(7);
-            double mi = 0.0;
-            if (run) {
-                const double hx = -(plogp(lut, (uint32_t)(npx - pp), Nd) + plogp(lut, pp, Nd));
-                mi = (hx + Hy) - h;                              // codec.py:554
-                if (!(mi > 0.0)) mi = 0.0;
-            }
-            if (t == 0) mis_sh[i] = mi;
-            if (need_decision && !decided) {
-                cum += mi;
-                if (cum >= tg) { s = i + 1; decided = true; }
-            }
+            if (i0 < 0) DTS(7);
         }
     }
     if (lut_ok && !wfast && !walk) Hy = -np_sum_block1024(RankTerm{terms}, (int)m, vals);
