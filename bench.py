@@ -419,6 +419,38 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # ---- N > 1: the all-gather alone and the step without it (kernel-only
+    # scaling and the collective reported separately), same barrier + max-over-ranks timing
+    dist_split = None
+    if world > 1:
+        def timed(fn):
+            dist.barrier()
+            torch.cuda.synchronize()
+            t_a = time.perf_counter()
+            for _ in range(args.steps):
+                fn()
+            torch.cuda.synchronize()
+            dist.barrier()
+            tt = torch.tensor([time.perf_counter() - t_a], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            return float(tt.item()) / args.steps
+
+        def gather_only():
+            D.pack_records(meta, maps, out=record)
+            D.gather_records(record, out=gathered)
+
+        def kernels_only():
+            codec.encode(covers, pl, stego=stego, maps=maps, meta=meta)
+            codec.decode(stego, maps, meta, payload_words=pl.payload_words, map_words=pl.map_words,
+                         cover=cover_out, payload=payload_out)
+
+        t_g = timed(gather_only)
+        t_k = timed(kernels_only)
+        dist_split = {"allgather_ms": round(t_g * 1e3, 4),
+                      "allgather_bytes": int(gathered.numel() * gathered.element_size()),
+                      "kernels_only_ms_per_step": round(t_k * 1e3, 4),
+                      "kernels_only_value": round(B * H * W * world / t_k / 1e6, 1)}
+
     # ---- per-kernel device time (HIP events on the launch stream), separate timed pass
     kernels = {}
     if not args.no_profile:
@@ -472,7 +504,8 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"{args.kind} {H}x{W} uint16 x {B} slices/GPU, {args.payload_chars}-char "
                                    f"payload/slice, beta=0.4, block=16; encode(plan+embed)+decode(restore+gather)"
-                                   + (" + RCCL all-gather of slice records/maps" if world > 1 else ""),
+                                   + (f" + {'RCCL' if args.backend == 'nccl' else args.backend} all-gather of slice records/maps"
+                                      if world > 1 else ""),
                        "global_batch": B * world, "slice": f"{H}x{W}", "parallelism": f"slices/{world} GPUs"},
             "roofline": roof,
             "step_hbm_gbs": round(step_bytes * world / (elapsed / args.steps) / 1e9 / world, 1),
@@ -480,6 +513,8 @@ def main():
             "s_values": s_vals,
             "roundtrip_ok": ok,
         }
+        if dist_split is not None:
+            out["distributed"] = dist_split
         out["inplace"] = lsb_inplace
         out["quality"] = quality
         if c3 is not None:
