@@ -881,8 +881,12 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
         if (tid == 0) {
             uint32_t cc = PEE_SKIP;
             if (!INPLACE) {
+                // the flag load goes out with the ticket (one round trip): a flag seen set was
+                // set before this ticket was drawn, so `end` lies in an earlier chunk; a flag
+                // set meanwhile but not seen only costs this chunk the full path
+                const uint32_t dn = ld_agent(tick + 1);
                 cc = atomicAdd(tick, 1u);
-                if (ld_agent(tick + 1)) {   // `end` already placed: this chunk is a plain copy
+                if (dn) {   // `end` already placed: this chunk is a plain copy
                     lb_store(st + cc, LB_INC | (u64)L);
                     cc |= 0x80000000u;
                 }
