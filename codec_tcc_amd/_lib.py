@@ -63,6 +63,7 @@ class PeeMeta(C.Structure):
 PEE_PARTIAL = 1
 META_BYTES = C.sizeof(SliceMeta)
 PEE_META_BYTES = C.sizeof(PeeMeta)
+CODEC_PEE_ELOOKBACK = 2  # meta.status: look-back gave up (include/codec_tcc.h)
 LAYOUT_BYTES = C.sizeof(Layout)
 
 _VP = C.c_void_p

@@ -774,11 +774,30 @@ __device__ __forceinline__ uint32_t ld_agent(uint32_t* p) {
 // `done` (optional): the slice's finished flag.  It can only be set once every chunk before
 // the one holding `end` has published, so a waiter that sees it set lies past `end` and
 // returns `sat` (>= L) instead of waiting for predecessors that may never publish.
+#ifndef PEE_LB_SLEEP
+#define PEE_LB_SLEEP 1
+#endif
+#ifndef PEE_LB_POLL1
+#define PEE_LB_POLL1 0
+#endif
 __device__ uint32_t lb_exclusive(u64* st, int c, bool* timeout, uint32_t* done = nullptr, uint32_t sat = 0) {
     const int lane = threadIdx.x & 63;
     uint32_t excl = 0;
     int p = c - 1;
     uint32_t spins = 0;
+#if PEE_LB_POLL1
+    // wait on the nearest predecessor alone first (one lane polls, not 64)
+    for (;;) {
+        const u64 w0 = lb_load(st + p);
+        if (__builtin_amdgcn_readfirstlane((uint32_t)(w0 >> 62)) != 0u) break;
+        if (done && ld_agent(done)) return sat;
+        if (++spins > (1u << 22)) {
+            *timeout = true;
+            return excl;
+        }
+        __builtin_amdgcn_s_sleep(PEE_LB_SLEEP);
+    }
+#endif
     for (;;) {
         const int idx = p - lane;
         const u64 w = idx >= 0 ? lb_load(st + idx) : LB_INC;
@@ -793,7 +812,7 @@ __device__ uint32_t lb_exclusive(u64* st, int c, bool* timeout, uint32_t* done =
                 *timeout = true;
                 return excl;
             }
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(PEE_LB_SLEEP);
             continue;
         }
         uint32_t v = lane <= first ? (uint32_t)w : 0u;
@@ -801,6 +820,10 @@ __device__ uint32_t lb_exclusive(u64* st, int c, bool* timeout, uint32_t* done =
         for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
         excl += v;
         if (first < 64) return excl;
+        // embed (done != nullptr): a partial sum that already reaches `sat` (= L) places the
+        // chunk past `end`; the caller only compares the prefix with L, and publishes it as a
+        // saturated inclusive value, as the done-flag path does
+        if (done && excl >= sat) return excl;
         p -= 64;
     }
 }
@@ -843,6 +866,13 @@ __device__ __forceinline__ bool pee_slot(uint32_t v, int B, int nchunks, bool ch
 // Out of place: one workgroup per (slice, chunk) slot, slice-major.  In place: persistent
 // workgroups walk the slots chunk-major, so a slice's later chunks are only reached after
 // its earlier ones, and skip (without a ticket) once the slice is finished.
+// launch mode of the out-of-place single pass: chunk-major slot order, and chunk = slot
+// (no ticket).  Without the ticket the look-back's forward progress rests on in-order
+// workgroup dispatch within an XCD (a slice's chunks all sit on one XCD, pee_slot): every
+// predecessor of a resident workgroup has then been dispatched; lb_exclusive's bounded spin
+// still turns a violation into CODEC_PEE_ELOOKBACK instead of a hang.
+#define PEE_MODE_CMAJOR 1
+#define PEE_MODE_NOTICKET 2
 #define PEE_CTL_WORDS(B) (32 + 32 * (size_t)(B))
 #define PEE_SKIP 0xFFFFFFFFu
 #define PEE_STOP 0xFFFFFFFEu
@@ -851,7 +881,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                                                     int maxval, const int32_t* __restrict__ lengths,
                                                     const u64* __restrict__ payload_all, int pw, int nchunks, int B,
                                                     u64* status_all, uint32_t* ctl, codec_pee_meta* meta_all,
-                                                    u64* __restrict__ lm_all, int lmw, int cmajor) {
+                                                    u64* __restrict__ lm_all, int lmw, int mode) {
     typedef typename Vec8<T>::type V;
     __shared__ u64 sh64[8];
     __shared__ uint32_t sh[8];
@@ -866,7 +896,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
     const int tid = threadIdx.x;
     for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
         int b, j;
-        if (!pee_slot(v, B, nchunks, INPLACE || cmajor, &b, &j)) continue;   // uniform; no barrier passed
+        if (!pee_slot(v, B, nchunks, INPLACE || (mode & PEE_MODE_CMAJOR), &b, &j)) continue;   // uniform; no barrier passed
         uint32_t* tick = ctl + 32 + 32 * (size_t)b;
         u64* st = status_all + (size_t)b * nchunks;
         const uint32_t L = (uint32_t)max(0, lengths[b]);
@@ -885,7 +915,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                 // set before this ticket was drawn, so `end` lies in an earlier chunk; a flag
                 // set meanwhile but not seen only costs this chunk the full path
                 const uint32_t dn = ld_agent(tick + 1);
-                cc = atomicAdd(tick, 1u);
+                cc = (mode & PEE_MODE_NOTICKET) ? (uint32_t)j : atomicAdd(tick, 1u);
                 if (dn) {   // `end` already placed: this chunk is a plain copy
                     lb_store(st + cc, LB_INC | (u64)L);
                     cc |= 0x80000000u;
@@ -1056,7 +1086,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
                                                       const codec_pee_meta* __restrict__ meta_all,
                                                       const u64* __restrict__ lm_all, int lmw, int nchunks, int B,
                                                       u64* status_all, uint32_t* ctl, u64* __restrict__ payload_all,
-                                                      int pw, int cmajor) {
+                                                      int pw, int mode) {
     typedef typename Vec8<T>::type V;
     __shared__ u64 sh64[8];
     __shared__ uint32_t s_v, s_excl;
@@ -1081,7 +1111,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
     }
     for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
         int b, j;
-        const bool valid = pee_slot(v, B, nchunks, INPLACE || cmajor, &b, &j);
+        const bool valid = pee_slot(v, B, nchunks, INPLACE || (mode & PEE_MODE_CMAJOR), &b, &j);
         if (j > cmax) return;                           // in place: a lane's chunks only grow
         if (!valid) continue;
         const codec_pee_meta* M = meta_all + b;
@@ -1096,7 +1126,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
         // `end`); in place only the ticketed chunk is read
         if (!INPLACE) pee_load_chunk<T, NT>(src, W, CR, items, j, a0, a1, o0);
         int c = j;
-        if (j <= cend) {   // exactly cend+1 slots take tickets 0..cend
+        if (j <= cend && (INPLACE || !(mode & PEE_MODE_NOTICKET))) {   // exactly cend+1 slots take tickets 0..cend
             if (tid == 0) s_v = atomicAdd(ctl + 32 + 32 * (size_t)b, 1u);
             __syncthreads();
             c = (int)s_v;
@@ -1261,6 +1291,9 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
     // 0.82 ms at 256 x 2048^2, where the two-pass scan + prefix embed takes 0.85 ms).  Small
     // batches keep the two-pass path (a lone slice's chain would be the critical path).
     // CODEC_PEE_ONEPASS: -1 auto, 0 never, 1 always; CODEC_PEE_1P_CHUNK_MAJOR=0: slice-major.
+    // Out of place the chunk is the slot's own (CODEC_PEE_1P_NOTICKET=1, default): the per-slice
+    // ticket atomic cost 2-3 % (0.78 -> 0.76 ms at 256 x 2048^2, tools/tune_pee_mode2_cfg.json);
+    // extract keeps it (equal times: only the chunks up to `end` take one there).
     const long long onepass = knob("CODEC_PEE_ONEPASS", -1);
     if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && (onepass > 0 || (onepass < 0 && (inplace || P->B >= 32)))) {
         u64* stw = reinterpret_cast<u64*>(static_cast<char*>(workspace) + L.st);
@@ -1276,8 +1309,9 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
 #define PE1(TT, NTV, IP) hipLaunchKernelGGL((k_pee_embed1<TT, NTV, IP>), dim3((unsigned)g), dim3(256), 0, st, \
             static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, \
             reinterpret_cast<const u64*>(payload), P->payload_words, L.nchunks, P->B, stw, ctl, meta, \
-            reinterpret_cast<u64*>(lm), P->lm_words, cmajor)
-        const int cmajor = (int)knob("CODEC_PEE_1P_CHUNK_MAJOR", 1);
+            reinterpret_cast<u64*>(lm), P->lm_words, mode)
+        const int mode = (knob("CODEC_PEE_1P_CHUNK_MAJOR", 1) ? PEE_MODE_CMAJOR : 0) |
+                         (knob("CODEC_PEE_1P_NOTICKET", 1) ? PEE_MODE_NOTICKET : 0);
         if (P->bytes == 2) {
             if (inplace) { if (nt) PE1(uint16_t, true, true); else PE1(uint16_t, false, true); }
             else { if (nt) PE1(uint16_t, true, false); else PE1(uint16_t, false, false); }
@@ -1385,8 +1419,9 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
         g = (g + 7) / 8 * 8;
 #define PX1(TT, NTV, IP) hipLaunchKernelGGL((k_pee_extract1<TT, NTV, IP>), dim3((unsigned)g), dim3(256), 0, st, \
             static_cast<const TT*>(stego), static_cast<TT*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm), \
-            P->lm_words, L.nchunks, P->B, stw, ctl, reinterpret_cast<u64*>(payload_out), P->payload_words, cmajor)
-        const int cmajor = (int)knob("CODEC_PEE_1P_CHUNK_MAJOR", 1);
+            P->lm_words, L.nchunks, P->B, stw, ctl, reinterpret_cast<u64*>(payload_out), P->payload_words, mode)
+        const int mode = (knob("CODEC_PEE_X_CHUNK_MAJOR", knob("CODEC_PEE_1P_CHUNK_MAJOR", 1)) ? PEE_MODE_CMAJOR : 0) |
+                         (knob("CODEC_PEE_X_NOTICKET", 0) ? PEE_MODE_NOTICKET : 0);
         if (P->bytes == 2) {
             if (inplace) { if (nt) PX1(uint16_t, true, true); else PX1(uint16_t, false, true); }
             else { if (nt) PX1(uint16_t, true, false); else PX1(uint16_t, false, false); }

@@ -99,6 +99,10 @@ class PeeCodec:
     def decode(self, enc: PeeEncoded):
         """(list of 0/1 bit vectors, restored cover tensor); raises if a slice overflowed."""
         recs = enc.records()
+        lost = [i for i, r in enumerate(recs) if r.status == _lib.CODEC_PEE_ELOOKBACK]
+        if lost:
+            raise RuntimeError(f"codec_pee_embed: cursor look-back timed out in slices {lost} "
+                               "(out-of-order workgroup dispatch); re-run with CODEC_PEE_ONEPASS=0")
         bad = [i for i, r in enumerate(recs) if r.status != 0]
         if bad:
             raise ValueError(f"payload exceeds PEE capacity in slices {bad} (T={self.T})")

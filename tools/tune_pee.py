@@ -22,8 +22,12 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--size", type=int, default=2048)
     ap.add_argument("--kind", default="ct12")
+    ap.add_argument("--lib", default=None, help="alternative build of libcodec_hip.so")
     a = ap.parse_args()
     import torch
+    if a.lib:
+        from codec_tcc_amd import _lib
+        _lib.load(os.path.abspath(a.lib))
 
     import bench
     configs = json.loads(a.configs)
