@@ -850,15 +850,28 @@ __device__ __forceinline__ void pee_load_chunk(const T* src, int W, int CR, uint
 // tickets come back in slot order, which is what lets the speculative load of chunk j be
 // the ticketed chunk (correctness never depends on it: the ticket decides the chunk).
 // Out of place the lane walks its slices slice-major, in place chunk-major.
-__device__ __forceinline__ bool pee_slot(uint32_t v, int B, int nchunks, bool chunk_major, int* b, int* j) {
-    const int B8 = (B + 7) / 8;
+__device__ __forceinline__ bool pee_slot(uint32_t v, int B, int nchunks, int g8, int* b, int* j) {
+    // g8 slice lanes per group: the groups follow one another, chunk-major inside a group
+    // (g8 = B8: chunk-major over the batch; g8 = 1: slice-major)
     const int x = (int)(v & 7u);
     const uint32_t k = v >> 3;
-    int bi;
-    if (chunk_major) { *j = (int)(k / (uint32_t)B8); bi = (int)(k - (uint32_t)*j * B8); }
-    else { bi = (int)(k / (uint32_t)nchunks); *j = (int)(k - (uint32_t)bi * nchunks); }
+    const uint32_t per = (uint32_t)g8 * (uint32_t)nchunks;
+    const uint32_t grp = k / per, r = k - grp * per;
+    *j = (int)(r / (uint32_t)g8);
+    const int bi = (int)(grp * (uint32_t)g8 + (r - (uint32_t)*j * g8));
     *b = x + 8 * bi;
     return *b < B;
+}
+__host__ __device__ __forceinline__ int pee_group8(int B, int mode, bool inplace) {
+    const int B8 = (B + 7) / 8;
+    if (inplace) return B8;
+    const int g = mode >> 8;
+    if (g > 0) return g < B8 ? g : B8;
+    return (mode & 1) ? B8 : 1;   // PEE_MODE_CMAJOR
+}
+__host__ __device__ __forceinline__ uint32_t pee_total_slots(int B, int nchunks, int g8) {
+    const int B8 = (B + 7) / 8;
+    return 8u * (uint32_t)((B8 + g8 - 1) / g8 * g8) * (uint32_t)nchunks;
 }
 
 // ctl[0] = slices finished (in place); slice b: chunk ticket ctl[32 + 32 b], finished flag
@@ -891,12 +904,13 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
     const uint32_t items = (uint32_t)(H / 2) * (uint32_t)CR;
     const int nc = (H / 2) * (W / 2);
     const int ntiles = (nc + PEE_TILE - 1) / PEE_TILE;
-    const uint32_t total = 8u * (uint32_t)((B + 7) / 8) * (uint32_t)nchunks;
+    const int g8 = pee_group8(B, mode, INPLACE);
+    const uint32_t total = pee_total_slots(B, nchunks, g8);
     const size_t npx = (size_t)H * W;
     const int tid = threadIdx.x;
     for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
         int b, j;
-        if (!pee_slot(v, B, nchunks, INPLACE || (mode & PEE_MODE_CMAJOR), &b, &j)) continue;   // uniform; no barrier passed
+        if (!pee_slot(v, B, nchunks, g8, &b, &j)) continue;   // uniform; no barrier passed
         uint32_t* tick = ctl + 32 + 32 * (size_t)b;
         u64* st = status_all + (size_t)b * nchunks;
         const uint32_t L = (uint32_t)max(0, lengths[b]);
@@ -1095,7 +1109,8 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
     const uint32_t items = (uint32_t)(H / 2) * (uint32_t)CR;
     const size_t npx = (size_t)H * W;
     const int tid = threadIdx.x;
-    const uint32_t total = 8u * (uint32_t)((B + 7) / 8) * (uint32_t)nchunks;
+    const int g8 = pee_group8(B, mode, INPLACE);
+    const uint32_t total = pee_total_slots(B, nchunks, g8);
     int cmax = nchunks - 1;
     if (INPLACE) {   // chunk-major slots: nothing past the last chunk any slice needs
         if (tid == 0) s_cmax = -1;
@@ -1111,7 +1126,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
     }
     for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
         int b, j;
-        const bool valid = pee_slot(v, B, nchunks, INPLACE || (mode & PEE_MODE_CMAJOR), &b, &j);
+        const bool valid = pee_slot(v, B, nchunks, g8, &b, &j);
         if (j > cmax) return;                           // in place: a lane's chunks only grow
         if (!valid) continue;
         const codec_pee_meta* M = meta_all + b;
@@ -1294,6 +1309,11 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
     // Out of place the chunk is the slot's own (CODEC_PEE_1P_NOTICKET=1, default): the per-slice
     // ticket atomic cost 2-3 % (0.78 -> 0.76 ms at 256 x 2048^2, tools/tune_pee_mode2_cfg.json);
     // extract keeps it (equal times: only the chunks up to `end` take one there).
+    // CODEC_PEE_1P_GROUP (slices, multiple of 8; default 32): the batch is walked in groups of
+    // that many slices, chunk-major inside a group -- 4 slices per XCD stream at once instead
+    // of 32 (full chunk-major) or 1 (slice-major, whose look-back waits on the in-flight loads
+    // of the 64 chunks before it): embed 0.81 -> 0.74 ms at 256 x 2048^2
+    // (tools/tune_pee_group*_cfg.json); extract is fastest chunk-major (CODEC_PEE_X_GROUP=0).
     const long long onepass = knob("CODEC_PEE_ONEPASS", -1);
     if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && (onepass > 0 || (onepass < 0 && (inplace || P->B >= 32)))) {
         u64* stw = reinterpret_cast<u64*>(static_cast<char*>(workspace) + L.st);
@@ -1302,7 +1322,10 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
         HIP_TRY(hipMemsetAsync(meta, 0, (size_t)P->B * sizeof(codec_pee_meta), st));
         if (inplace) HIP_TRY(hipMemsetAsync(lm, 0, (size_t)P->B * P->lm_words * 8, st));
         ProfScope prof(st, CODEC_K_PEE_EMBED1);
-        const long long total = 8LL * ((P->B + 7) / 8) * L.nchunks;
+        const int mode = (knob("CODEC_PEE_1P_CHUNK_MAJOR", 1) ? PEE_MODE_CMAJOR : 0) |
+                         (knob("CODEC_PEE_1P_NOTICKET", 1) ? PEE_MODE_NOTICKET : 0) |
+                         ((int)(knob("CODEC_PEE_1P_GROUP", 32) / 8) << 8);
+        const long long total = pee_total_slots(P->B, L.nchunks, pee_group8(P->B, mode, inplace));
         long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));
         if (g > total) g = total;
         g = (g + 7) / 8 * 8;   // keep every workgroup on one slot lane (pee_slot)
@@ -1310,8 +1333,6 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
             static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, \
             reinterpret_cast<const u64*>(payload), P->payload_words, L.nchunks, P->B, stw, ctl, meta, \
             reinterpret_cast<u64*>(lm), P->lm_words, mode)
-        const int mode = (knob("CODEC_PEE_1P_CHUNK_MAJOR", 1) ? PEE_MODE_CMAJOR : 0) |
-                         (knob("CODEC_PEE_1P_NOTICKET", 1) ? PEE_MODE_NOTICKET : 0);
         if (P->bytes == 2) {
             if (inplace) { if (nt) PE1(uint16_t, true, true); else PE1(uint16_t, false, true); }
             else { if (nt) PE1(uint16_t, true, false); else PE1(uint16_t, false, false); }
@@ -1413,15 +1434,16 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
         uint32_t* ctl = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.ctl);
         HIP_TRY(hipMemsetAsync(stw, 0, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4, st));
         ProfScope prof(st, CODEC_K_PEE_EXTRACT1);
-        const long long total = 8LL * ((P->B + 7) / 8) * L.nchunks;
+        const int mode = (knob("CODEC_PEE_X_CHUNK_MAJOR", knob("CODEC_PEE_1P_CHUNK_MAJOR", 1)) ? PEE_MODE_CMAJOR : 0) |
+                         (knob("CODEC_PEE_X_NOTICKET", 0) ? PEE_MODE_NOTICKET : 0) |
+                         ((int)(knob("CODEC_PEE_X_GROUP", 0) / 8) << 8);
+        const long long total = pee_total_slots(P->B, L.nchunks, pee_group8(P->B, mode, inplace));
         long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));
         if (g > total) g = total;
         g = (g + 7) / 8 * 8;
 #define PX1(TT, NTV, IP) hipLaunchKernelGGL((k_pee_extract1<TT, NTV, IP>), dim3((unsigned)g), dim3(256), 0, st, \
             static_cast<const TT*>(stego), static_cast<TT*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm), \
             P->lm_words, L.nchunks, P->B, stw, ctl, reinterpret_cast<u64*>(payload_out), P->payload_words, mode)
-        const int mode = (knob("CODEC_PEE_X_CHUNK_MAJOR", knob("CODEC_PEE_1P_CHUNK_MAJOR", 1)) ? PEE_MODE_CMAJOR : 0) |
-                         (knob("CODEC_PEE_X_NOTICKET", 0) ? PEE_MODE_NOTICKET : 0);
         if (P->bytes == 2) {
             if (inplace) { if (nt) PX1(uint16_t, true, true); else PX1(uint16_t, false, true); }
             else { if (nt) PX1(uint16_t, true, false); else PX1(uint16_t, false, false); }

@@ -209,3 +209,45 @@ def test_gpu_real_dicom_matches_oracle(name, maxval, T, inplace, pee_path):
     for i in range(2):
         np.testing.assert_array_equal(framing.unpack_bits(host[i], len(payloads[i])), payloads[i])
     np.testing.assert_array_equal(cover.cpu().numpy(), covers)
+
+
+# single-pass slot orders over a batch of many slices: slice groups (padded when the group
+# does not divide the batch's 8-slice lanes), chunk-major, slice-major, with and without
+# the per-slice ticket; `end` lands in different chunks, one slice is empty, one overflows
+SLOT_ORDERS = [{}, {"CODEC_PEE_1P_GROUP": "16", "CODEC_PEE_X_GROUP": "24"},
+               {"CODEC_PEE_1P_GROUP": "0", "CODEC_PEE_1P_CHUNK_MAJOR": "0", "CODEC_PEE_X_CHUNK_MAJOR": "0"},
+               {"CODEC_PEE_1P_GROUP": "0", "CODEC_PEE_1P_NOTICKET": "0", "CODEC_PEE_X_NOTICKET": "1"},
+               {"CODEC_PEE_1P_GROUP": "8", "CODEC_PEE_1P_WGS": "40", "CODEC_PEE_X_GROUP": "16"}]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", range(len(SLOT_ORDERS)))
+def test_gpu_onepass_slot_orders(cfg, monkeypatch):
+    torch = pytest.importorskip("torch")
+    from codec_tcc_amd import framing
+    from codec_tcc_amd.pee import PeeCodec, lm_bits
+    for k, v in SLOT_ORDERS[cfg].items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("CODEC_PEE_ONEPASS", "1")
+    bsz, h, w, T = 41, 256, 256, 2          # 4 chunks per slice
+    covers = np.stack([synth.ct12(h, w, 900 + i) for i in range(bsz)])
+    caps = [P.capacity(c, T) for c in covers]
+    lens = [(caps[i] * (i % 9)) // 8 for i in range(bsz)]
+    lens[5] = 0
+    lens[17] = caps[17] + 40                # overflows: truncated, status 1
+    payloads = [_bits(n, 300 + i) for i, n in enumerate(lens)]
+    codec = PeeCodec(bsz, h, w, T=T)
+    enc = codec.embed(torch.from_numpy(covers).cuda(), payloads)
+    recs = enc.records()
+    stego = enc.stego.cpu().numpy()
+    for i in range(bsz):
+        st, side = P.pee_embed(covers[i], payloads[i], T, truncate=True)
+        assert recs[i].status == (1 if i == 17 else 0) and recs[i].end == side["end"], i
+        np.testing.assert_array_equal(stego[i], st)
+        np.testing.assert_array_equal(lm_bits(enc, i), side["lm"])
+    words, cover = codec.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words)
+    host = words.cpu().numpy()
+    for i in range(bsz):
+        n = min(lens[i], caps[i])
+        np.testing.assert_array_equal(framing.unpack_bits(host[i], n), payloads[i][:n])
+    np.testing.assert_array_equal(cover.cpu().numpy(), covers)
