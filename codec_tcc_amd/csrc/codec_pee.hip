@@ -1131,7 +1131,12 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
         if (!valid) continue;
         const codec_pee_meta* M = meta_all + b;
         const int end = M->end, Tthr = M->T;
+#ifdef PEE_X_COPYONLY   // diagnostic build (tools): every chunk a plain copy
+        const int cend = -1;
+        (void)end;
+#else
         const int cend = end >= 0 ? (end >> 2) / PEE_CHUNK : -1;
+#endif
         if (INPLACE && j > cend) continue;              // uniform: no barrier passed yet
         const T* src = stego + b * npx;
         T* dst = cover + b * npx;
@@ -1140,22 +1145,31 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
         // out of place chunk j is loaded while the ticket is in flight (a plain copy when past
         // `end`); in place only the ticketed chunk is read
         if (!INPLACE) pee_load_chunk<T, NT>(src, W, CR, items, j, a0, a1, o0);
+        const u64* lm = lm_all + (size_t)b * lmw;
+        const bool noticket = !INPLACE && (mode & PEE_MODE_NOTICKET);
+        u64 lwv[4] = {0, 0, 0, 0};   // location-map word of each item (4 bits of it used)
+        if (noticket && j <= cend) {   // the chunk is known: its map words go out with its pixels
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t it = (uint32_t)j * PEE_CHUNK + u * 256u + tid;
+                if (it < items) lwv[u] = lm[(4 * it) >> 6];
+            }
+        }
         int c = j;
-        if (j <= cend && (INPLACE || !(mode & PEE_MODE_NOTICKET))) {   // exactly cend+1 slots take tickets 0..cend
+        if (j <= cend && !noticket) {   // exactly cend+1 slots take tickets 0..cend
             if (tid == 0) s_v = atomicAdd(ctl + 32 + 32 * (size_t)b, 1u);
             __syncthreads();
             c = (int)s_v;
             if (INPLACE || c != j) pee_load_chunk<T, NT>(src, W, CR, items, c, a0, a1, o0);
         }
         if (c <= cend) {
-            const u64* lm = lm_all + (size_t)b * lmw;
             uint32_t actm = 0, innm = 0;
             u64 packed = 0;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const uint32_t it = (uint32_t)c * PEE_CHUNK + u * 256u + tid;
                 if (it >= items) continue;
-                const u64 lw = lm[(4 * it) >> 6] >> ((4 * it) & 63);   // 4 bits, same word
+                const u64 lw = (noticket ? lwv[u] : lm[(4 * it) >> 6]) >> ((4 * it) & 63);   // 4 bits, same word
                 uint32_t n = 0;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -1308,12 +1322,14 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
     // CODEC_PEE_ONEPASS: -1 auto, 0 never, 1 always; CODEC_PEE_1P_CHUNK_MAJOR=0: slice-major.
     // Out of place the chunk is the slot's own (CODEC_PEE_1P_NOTICKET=1, default): the per-slice
     // ticket atomic cost 2-3 % (0.78 -> 0.76 ms at 256 x 2048^2, tools/tune_pee_mode2_cfg.json);
-    // extract keeps it (equal times: only the chunks up to `end` take one there).
+    // extract drops it too, and then loads the chunk's location-map words together with
+    // its pixels (0.76 -> 0.74 ms).
     // CODEC_PEE_1P_GROUP (slices, multiple of 8; default 32): the batch is walked in groups of
     // that many slices, chunk-major inside a group -- 4 slices per XCD stream at once instead
     // of 32 (full chunk-major) or 1 (slice-major, whose look-back waits on the in-flight loads
     // of the 64 chunks before it): embed 0.81 -> 0.74 ms at 256 x 2048^2
-    // (tools/tune_pee_group*_cfg.json); extract is fastest chunk-major (CODEC_PEE_X_GROUP=0).
+    // (tools/tune_pee_group*_cfg.json); extract (CODEC_PEE_X_GROUP, default 32 as well)
+    // 0.74 -> 0.73 ms (tools/tune_pee_xnt_cfg.json).
     const long long onepass = knob("CODEC_PEE_ONEPASS", -1);
     if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && (onepass > 0 || (onepass < 0 && (inplace || P->B >= 32)))) {
         u64* stw = reinterpret_cast<u64*>(static_cast<char*>(workspace) + L.st);
@@ -1435,8 +1451,8 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
         HIP_TRY(hipMemsetAsync(stw, 0, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4, st));
         ProfScope prof(st, CODEC_K_PEE_EXTRACT1);
         const int mode = (knob("CODEC_PEE_X_CHUNK_MAJOR", knob("CODEC_PEE_1P_CHUNK_MAJOR", 1)) ? PEE_MODE_CMAJOR : 0) |
-                         (knob("CODEC_PEE_X_NOTICKET", 0) ? PEE_MODE_NOTICKET : 0) |
-                         ((int)(knob("CODEC_PEE_X_GROUP", 0) / 8) << 8);
+                         (knob("CODEC_PEE_X_NOTICKET", 1) ? PEE_MODE_NOTICKET : 0) |
+                         ((int)(knob("CODEC_PEE_X_GROUP", 32) / 8) << 8);
         const long long total = pee_total_slots(P->B, L.nchunks, pee_group8(P->B, mode, inplace));
         long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));
         if (g > total) g = total;

@@ -216,7 +216,7 @@ def test_gpu_real_dicom_matches_oracle(name, maxval, T, inplace, pee_path):
 # the per-slice ticket; `end` lands in different chunks, one slice is empty, one overflows
 SLOT_ORDERS = [{}, {"CODEC_PEE_1P_GROUP": "16", "CODEC_PEE_X_GROUP": "24"},
                {"CODEC_PEE_1P_GROUP": "0", "CODEC_PEE_1P_CHUNK_MAJOR": "0", "CODEC_PEE_X_CHUNK_MAJOR": "0"},
-               {"CODEC_PEE_1P_GROUP": "0", "CODEC_PEE_1P_NOTICKET": "0", "CODEC_PEE_X_NOTICKET": "1"},
+               {"CODEC_PEE_1P_GROUP": "0", "CODEC_PEE_1P_NOTICKET": "0", "CODEC_PEE_X_NOTICKET": "0", "CODEC_PEE_X_GROUP": "0"},
                {"CODEC_PEE_1P_GROUP": "8", "CODEC_PEE_1P_WGS": "40", "CODEC_PEE_X_GROUP": "16"}]
 
 

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--size", type=int, default=2048)
     ap.add_argument("--kind", default="ct12")
+    ap.add_argument("--no-check", action="store_true", help="diagnostic builds: skip the round-trip check")
     ap.add_argument("--lib", default=None, help="alternative build of libcodec_hip.so")
     a = ap.parse_args()
     import torch
@@ -42,7 +43,7 @@ def main():
             os.environ.update(cfg)
             for mode in (False, True):
                 r = bench.bench_pee(args, torch, None, 1, dev, covers, B, H, W, inplace=mode)
-                assert r["roundtrip_ok"], (cfg, mode)
+                assert a.no_check or r["roundtrip_ok"], (cfg, mode)
                 d = res.setdefault((i, mode), {})
                 for k, v in r["kernels_ms"].items():
                     d.setdefault(k, []).append(v)
