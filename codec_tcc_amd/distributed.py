@@ -68,3 +68,55 @@ def gather_records(local_records, group=None, out=None):
     else:
         dist.all_gather_into_tensor(out, local_records.contiguous(), group=group)
     return out
+
+
+class RecordExchange:
+    """The record all-gather of one batch, overlapped with that batch's decode.
+
+    The records depend only on what encode wrote (meta + packed maps), so they are packed
+    and gathered on a side stream while decode's kernels run on the launch stream:
+    ``mark()`` right after encode is queued (records an event), then decode, then
+    ``start(meta, maps)`` (the side stream waits for the event only, so a host-blocking
+    backend such as gloo does not hold back decode's launches either), and ``join()`` (the
+    current stream waits for the gather, so the next encode cannot overwrite meta/maps under
+    the pack).  On RCCL the collective runs on its own stream ordered after the side stream.
+    CPU tensors (gloo tests) run synchronously."""
+
+    def __init__(self, batch: int, map_words: int, world: int, device, group=None):
+        import torch
+        self.group = group
+        words = record_words(map_words)
+        self.record = torch.zeros((batch, words), dtype=torch.int64, device=device)
+        self.gathered = torch.empty((world * batch, words), dtype=torch.int64, device=device)
+        dev = torch.device(device)
+        self.stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+        self.event = torch.cuda.Event() if self.stream is not None else None
+        self._marked = False
+
+    def mark(self):
+        """Record the point after encode on the current stream (no-op on CPU)."""
+        import torch
+        if self.stream is not None:
+            self.event.record(torch.cuda.current_stream(self.gathered.device))
+            self._marked = True
+
+    def start(self, meta, maps):
+        import torch
+        if self.stream is None:
+            pack_records(meta, maps, out=self.record)
+            gather_records(self.record, self.group, out=self.gathered)
+            return
+        if self._marked:
+            self.stream.wait_event(self.event)
+            self._marked = False
+        else:
+            self.stream.wait_stream(torch.cuda.current_stream(meta.device))
+        with torch.cuda.stream(self.stream):
+            pack_records(meta, maps, out=self.record)
+            gather_records(self.record, self.group, out=self.gathered)
+
+    def join(self):
+        import torch
+        if self.stream is not None:
+            torch.cuda.current_stream(self.gathered.device).wait_stream(self.stream)
+        return self.gathered

@@ -58,6 +58,10 @@ def _worker(rank, world, port, n_slices, mw, q):
     for g in range(n_slices):
         ok &= int.from_bytes(bytes(gm[g, :4].tolist()), "little") == g
         ok &= torch.equal(gp[g], torch.arange(g * mw, (g + 1) * mw, dtype=torch.int64))
+    # the overlapped exchange (CPU tensors: synchronous) yields the same records
+    xch = D.RecordExchange(B, mw, world, "cpu")
+    xch.start(meta, maps)
+    ok &= torch.equal(xch.join(), allrec)
     q.put((rank, bool(ok), tuple(allrec.shape)))
     dist.destroy_process_group()
 
