@@ -90,6 +90,18 @@ def pmc_traffic(kernel: str, b: int, h: int, w: int, kind: str):
     return {"hbm_bytes_per_launch": k["hbm_bytes_per_launch"], "source": d.get("source", path)}
 
 
+def _cpu_model() -> str:
+    """The host CPU (report the model beside the core count)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(size: int, kind: str, chars: int, budget_s: float):
     """The oracle (numpy restatement of the reference, bit-identical to it) timed on this
     host: decomposition + hybrid embed + merge + extract_local_planes + decode_message
@@ -114,7 +126,7 @@ def cpu_baseline(size: int, kind: str, chars: int, budget_s: float):
         "value": round(px / t_work / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
         "sample": f"{n} x {size}x{size} {kind} uint16 slices, {chars}-char payloads, numpy oracle "
                   f"(decompose+hybrid embed+merge+extract_local_planes+decode_message), 1 process",
-        "seconds": round(t_work, 2),
+        "seconds": round(t_work, 2), "cpu_model": _cpu_model(),
     }
 
 
@@ -144,7 +156,7 @@ def cpu_baseline_pool(size: int, kind: str, chars: int, workers: int, per_worker
     px = sum(r[0] for r in res)
     return {"value": round(px / wall / 1e6, 3), "unit": "Mpixels/s", "cores": workers, "kind": "port",
             "sample": f"{len(jobs)} x {size}x{size} {kind} slices over a {workers}-process pool (fork), wall clock",
-            "seconds": round(wall, 2)}
+            "seconds": round(wall, 2), "cpu_model": _cpu_model()}
 
 
 def _profile(lib, _lib, fn, steps):
