@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--cpu-pool", type=int, default=16,
                     help="workers of the pooled CPU baseline (the box's CPU share per GPU is 16; 0 = skip)")
     ap.add_argument("--c3", type=int, default=1, help="also time BASELINE config C3 (256 x 512^2)")
+    ap.add_argument("--c2", type=int, default=1, help="also time BASELINE config C2 (1 x 2048^2, latency)")
     return ap.parse_args()
 
 
@@ -341,6 +342,58 @@ def bench_c3(args, torch, dist, world, dev, rank):
     return res
 
 
+def bench_c2(args, torch, dev, rank):
+    """BASELINE config C2: ONE 2048^2 ct12 slice (a latency case: one workgroup's worth of
+    decisions, a handful of launches).  The LSB step and the MED-PEE step (two-pass path at
+    this batch size) timed separately, wall clock per step over many steps."""
+    import codec_tcc_amd as ct
+    from codec_tcc_amd import _lib, synth
+    from codec_tcc_amd.pee import PeeCodec
+    B, H, W = 1, 2048, 2048
+    covers = make_covers(torch, args.kind, B, H, W, dev, seed=7000 + rank)
+    codec = ct.Codec(B, H, W, dtype="uint16", beta=0.4, block=16, device=dev)
+    pl = ct.make_payloads([synth.payload(args.payload_chars, 7000 + rank)], dev)
+    stego = torch.empty_like(covers)
+    cov2 = torch.empty_like(covers)
+    maps = torch.empty((B, pl.map_words), dtype=torch.int64, device=dev)
+    meta = torch.empty((B, _lib.META_BYTES), dtype=torch.uint8, device=dev)
+    pay = torch.empty((B, pl.payload_words), dtype=torch.int64, device=dev)
+    pc = PeeCodec(B, H, W, dtype="uint16", T=args.pee_T, device=dev)
+    packed = pc.pack_payloads([synth.payload(args.payload_chars, 7100 + rank)])
+    lm = torch.empty((B, pc.lm_words), dtype=torch.int64, device=dev)
+    pmeta = torch.empty((B, _lib.PEE_META_BYTES), dtype=torch.uint8, device=dev)
+    pw = packed[0].shape[1]
+    pout = torch.empty((B, pw), dtype=torch.int64, device=dev)
+    pst = torch.empty_like(covers)
+    pcov = torch.empty_like(covers)
+
+    def lsb():
+        codec.encode(covers, pl, stego=stego, maps=maps, meta=meta)
+        codec.decode(stego, maps, meta, payload_words=pl.payload_words, map_words=pl.map_words, cover=cov2,
+                     payload=pay)
+
+    def pee():
+        pc.embed(covers, None, stego=pst, lm=lm, meta=pmeta, packed=packed)
+        pc.extract(pst, pmeta, lm, payload_words=pw, cover=pcov, payload=pout)
+
+    res = {"workload": f"{args.kind} 2048x2048 uint16 x 1 slice (C2)"}
+    steps = 10 * args.steps
+    for name, fn, outc in (("lsb", lsb, cov2), ("pee", pee, pcov)):
+        for _ in range(args.warmup):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        kern = _profile(_lib.load(), _lib, fn, steps) if not args.no_profile else {}
+        res[name] = {"ms_per_step": round(el / steps * 1e3, 4), "value": round(H * W * steps / el / 1e6, 1),
+                     "unit": "Mpixels/s", "roundtrip_ok": bool(torch.equal(outc.view(torch.int16), covers.view(torch.int16))),
+                     "kernels_ms": {k: round(v, 4) for k, v in kern.items()}}
+    return res
+
+
 def bench_quality(args, torch, covers, stego, B, H, W):
     """Stego quality of the LSB leg's output (reference src/mse.py metrics): one read-only
     pass over cover + stego (k_quality), metrics from exact moments on the host."""
@@ -486,6 +539,7 @@ def main():
 
     quality = bench_quality(args, torch, covers, stego, B, H, W) if rank == 0 else None
     c3 = bench_c3(args, torch, dist, world, dev, rank) if (rank == 0 and args.c3) else None
+    c2 = bench_c2(args, torch, dev, rank) if (rank == 0 and args.c2 and world == 1) else None
     lsb_inplace = bench_lsb_inplace(args, torch, dist, world, dev, covers, codec, pl, B, H, W)
     pee = None
     if args.pee:
@@ -536,6 +590,8 @@ def main():
         out["quality"] = quality
         if c3 is not None:
             out["c3"] = c3
+        if c2 is not None:
+            out["c2"] = c2
         if pee is not None:
             out["pee"] = pee
         if args.cpu_seconds > 0 and world == 1:

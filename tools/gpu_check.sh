@@ -23,7 +23,7 @@ fi
 if has prof; then
   R="$GRAFT_REPO_ROOT"
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
-      -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --cpu-seconds 0 --c3 0 \
+      -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --cpu-seconds 0 --c3 0 --c2 0 \
       > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof.log" ); rc=$?
   echo "rocprof rc=$rc"; tail -3 gpurun_out/prof.log
   find gpurun_out/prof -name "*stats*" | head
@@ -41,7 +41,7 @@ if has pmc; then
   R="$GRAFT_REPO_ROOT"
   for C in FETCH_SIZE WRITE_SIZE; do
     ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --pmc $C --kernel-trace --output-format csv \
-        -d "$R/gpurun_out/pmc_$C" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --no-profile --c3 0 \
+        -d "$R/gpurun_out/pmc_$C" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --no-profile --c3 0 --c2 0 \
         > "$R/gpurun_out/pmc_$C.log" 2>&1 ); rc=$?
     echo "pmc $C rc=$rc"; tail -2 "gpurun_out/pmc_$C.log"
     [ $rc -eq 0 ] || exit $rc
