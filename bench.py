@@ -279,16 +279,21 @@ def bench_pee(args, torch, dist, world, dev, covers, B, H, W, inplace=False):
         res["algorithmic_bytes_per_step_half"] = by
         t_e = kern.get("k_pee_embed1", 0.0) / 1e3
         if t_e > 0:
+            tr = pmc_traffic("k_pee_embed1<unsigned short, true, true>", B, H, W, args.kind)
             res["roofline"] = {"bound": "hbm", "kernel": "k_pee_embed1", "achieved": round(by / t_e / 1e9, 1),
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(by / t_e / 1e9 / HBM_PEAK_GBS, 4),
+                               "traffic": tr["hbm_bytes_per_launch"] if tr else None,
                                "algorithmic_bytes_per_launch": by}
         return res
     for kname in ("k_pee_embed1", "k_pee_scan"):
         if kname in kern:
             t_k = kern[kname] / 1e3
             by = B * H * W * 4
+            tr = pmc_traffic(kname + "<unsigned short, true, false>" if kname == "k_pee_embed1" else kname,
+                             B, H, W, args.kind)
             res["roofline"] = {"bound": "hbm", "kernel": kname, "achieved": round(by / t_k / 1e9, 1),
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(by / t_k / 1e9 / HBM_PEAK_GBS, 4),
+                               "traffic": tr["hbm_bytes_per_launch"] if tr else None,
                                "algorithmic_bytes_per_launch": by}
             break
     t_emb = sum(kern.get(k, 0.0) for k in ("k_pee_embed1", "k_pee_scan", "k_pee_locate", "k_pee_embed")) / 1e3

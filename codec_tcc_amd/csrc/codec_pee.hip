@@ -852,7 +852,14 @@ __device__ __forceinline__ void pee_load_chunk(const T* src, int W, int CR, uint
 // Out of place the lane walks its slices slice-major, in place chunk-major.
 __device__ __forceinline__ bool pee_slot(uint32_t v, int B, int nchunks, int g8, int* b, int* j) {
     // g8 slice lanes per group: the groups follow one another, chunk-major inside a group
-    // (g8 = B8: chunk-major over the batch; g8 = 1: slice-major)
+    // (g8 = B8: chunk-major over the batch; g8 = 1: slice-major).  g8 = 0 (PEE_MODE_FLAT,
+    // small batches): slot v = slice-major over every XCD, the chunk then comes from the
+    // per-slice ticket (a lone slice's chunks would otherwise all sit on one XCD)
+    if (g8 == 0) {
+        *b = (int)(v / (uint32_t)nchunks);
+        *j = (int)(v - (uint32_t)*b * (uint32_t)nchunks);
+        return *b < B;
+    }
     const int x = (int)(v & 7u);
     const uint32_t k = v >> 3;
     const uint32_t per = (uint32_t)g8 * (uint32_t)nchunks;
@@ -862,14 +869,17 @@ __device__ __forceinline__ bool pee_slot(uint32_t v, int B, int nchunks, int g8,
     *b = x + 8 * bi;
     return *b < B;
 }
+#define PEE_MODE_FLAT 4
 __host__ __device__ __forceinline__ int pee_group8(int B, int mode, bool inplace) {
     const int B8 = (B + 7) / 8;
     if (inplace) return B8;
+    if (mode & PEE_MODE_FLAT) return 0;
     const int g = mode >> 8;
     if (g > 0) return g < B8 ? g : B8;
     return (mode & 1) ? B8 : 1;   // PEE_MODE_CMAJOR
 }
 __host__ __device__ __forceinline__ uint32_t pee_total_slots(int B, int nchunks, int g8) {
+    if (g8 == 0) return (uint32_t)B * (uint32_t)nchunks;
     const int B8 = (B + 7) / 8;
     return 8u * (uint32_t)((B8 + g8 - 1) / g8 * g8) * (uint32_t)nchunks;
 }
@@ -1313,13 +1323,13 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
     const bool nt = knob("CODEC_NT", 1) != 0;
     const bool inplace = cover == stego;
     const long long items = (long long)(P->H / 2) * (P->W / 8);
-    // single pass: in place (it stops reading after `end`), and out of place for batches of
-    // >= 32 slices, with chunk-major slot order (all slices' chunk 0 first, then chunk 1 ...:
-    // every slice's look-back chain advances one hop per generation of resident workgroups;
-    // slice-major order left whole generations spinning on one slice's chain, 1.4 ms vs
-    // 0.82 ms at 256 x 2048^2, where the two-pass scan + prefix embed takes 0.85 ms).  Small
-    // batches keep the two-pass path (a lone slice's chain would be the critical path).
-    // CODEC_PEE_ONEPASS: -1 auto, 0 never, 1 always; CODEC_PEE_1P_CHUNK_MAJOR=0: slice-major.
+    // single pass (default wherever W % 8 == 0 and the buffers are 16-B aligned): in place it
+    // stops reading after `end`; out of place large batches walk chunk-major slot order (all
+    // slices' chunk 0 first, then chunk 1 ...: every slice's look-back chain advances one hop
+    // per generation of resident workgroups; slice-major order left whole generations
+    // spinning on one slice's chain, 1.4 ms vs 0.82 ms at 256 x 2048^2, where the two-pass
+    // scan + prefix embed takes 0.85 ms).
+    // CODEC_PEE_ONEPASS: 0 forces the two-pass path; CODEC_PEE_1P_CHUNK_MAJOR=0: slice-major.
     // Out of place the chunk is the slot's own (CODEC_PEE_1P_NOTICKET=1, default): the per-slice
     // ticket atomic cost 2-3 % (0.78 -> 0.76 ms at 256 x 2048^2, tools/tune_pee_mode2_cfg.json);
     // extract drops it too, and then loads the chunk's location-map words together with
@@ -1330,17 +1340,26 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
     // of the 64 chunks before it): embed 0.81 -> 0.74 ms at 256 x 2048^2
     // (tools/tune_pee_group*_cfg.json); extract (CODEC_PEE_X_GROUP, default 32 as well)
     // 0.74 -> 0.73 ms (tools/tune_pee_xnt_cfg.json).
+    // Small out-of-place batches run the single pass too (one launch instead of scan + locate
+    // + prefix embed, which are launch/latency bound there; tools/pee_small_batch.py, 2048²
+    // embed+extract step: B=1 50 -> 32 us, B=4 65 -> 47, B=8 93 -> 74, B=31 229 -> 207).
+    // B <= CODEC_PEE_FLAT_MAXB (7) uses flat slice-major slots over all XCDs (PEE_MODE_FLAT:
+    // a lone slice's chunks would otherwise all sit on one XCD); no ticket by default (the
+    // predecessors of a chunk have lower slot numbers, so in-order dispatch per XCD keeps the
+    // look-back progressing, as in the lane order; 256 tickets on one line cost 8 us at B=1).
     const long long onepass = knob("CODEC_PEE_ONEPASS", -1);
-    if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && (onepass > 0 || (onepass < 0 && (inplace || P->B >= 32)))) {
+    const bool flat = !inplace && P->B < 32 && P->B <= knob("CODEC_PEE_FLAT_MAXB", 7);
+    if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && onepass != 0) {
         u64* stw = reinterpret_cast<u64*>(static_cast<char*>(workspace) + L.st);
         uint32_t* ctl = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.ctl);
         HIP_TRY(hipMemsetAsync(stw, 0, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4, st));
         HIP_TRY(hipMemsetAsync(meta, 0, (size_t)P->B * sizeof(codec_pee_meta), st));
         if (inplace) HIP_TRY(hipMemsetAsync(lm, 0, (size_t)P->B * P->lm_words * 8, st));
         ProfScope prof(st, CODEC_K_PEE_EMBED1);
-        const int mode = (knob("CODEC_PEE_1P_CHUNK_MAJOR", 1) ? PEE_MODE_CMAJOR : 0) |
-                         (knob("CODEC_PEE_1P_NOTICKET", 1) ? PEE_MODE_NOTICKET : 0) |
-                         ((int)(knob("CODEC_PEE_1P_GROUP", 32) / 8) << 8);
+        const int mode = flat ? PEE_MODE_FLAT | (knob("CODEC_PEE_FLAT_TICKET", 0) ? 0 : PEE_MODE_NOTICKET)
+                              : (knob("CODEC_PEE_1P_CHUNK_MAJOR", 1) ? PEE_MODE_CMAJOR : 0) |
+                                    (knob("CODEC_PEE_1P_NOTICKET", 1) ? PEE_MODE_NOTICKET : 0) |
+                                    ((int)(knob("CODEC_PEE_1P_GROUP", 32) / 8) << 8);
         const long long total = pee_total_slots(P->B, L.nchunks, pee_group8(P->B, mode, inplace));
         long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));
         if (g > total) g = total;
@@ -1445,14 +1464,16 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
     const long long items = (long long)(P->H / 2) * (P->W / 8);
     const bool inplace = stego == cover_out;
     const long long onepass = knob("CODEC_PEE_ONEPASS", -1);   // as in codec_pee_embed
-    if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && (onepass > 0 || (onepass < 0 && (inplace || P->B >= 32)))) {
+    const bool flat = !inplace && P->B < 32 && P->B <= knob("CODEC_PEE_FLAT_MAXB", 7);
+    if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && onepass != 0) {
         u64* stw = reinterpret_cast<u64*>(static_cast<char*>(workspace) + L.st);
         uint32_t* ctl = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.ctl);
         HIP_TRY(hipMemsetAsync(stw, 0, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4, st));
         ProfScope prof(st, CODEC_K_PEE_EXTRACT1);
-        const int mode = (knob("CODEC_PEE_X_CHUNK_MAJOR", knob("CODEC_PEE_1P_CHUNK_MAJOR", 1)) ? PEE_MODE_CMAJOR : 0) |
-                         (knob("CODEC_PEE_X_NOTICKET", 1) ? PEE_MODE_NOTICKET : 0) |
-                         ((int)(knob("CODEC_PEE_X_GROUP", 32) / 8) << 8);
+        const int mode = flat ? PEE_MODE_FLAT | (knob("CODEC_PEE_FLAT_TICKET", 0) ? 0 : PEE_MODE_NOTICKET)
+                              : (knob("CODEC_PEE_X_CHUNK_MAJOR", knob("CODEC_PEE_1P_CHUNK_MAJOR", 1)) ? PEE_MODE_CMAJOR : 0) |
+                                    (knob("CODEC_PEE_X_NOTICKET", 1) ? PEE_MODE_NOTICKET : 0) |
+                                    ((int)(knob("CODEC_PEE_X_GROUP", 32) / 8) << 8);
         const long long total = pee_total_slots(P->B, L.nchunks, pee_group8(P->B, mode, inplace));
         long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));
         if (g > total) g = total;

@@ -59,10 +59,14 @@ def test_oracle_truncates_on_overflow():
     np.testing.assert_array_equal(cov, img)
 
 
-# single pass (decoupled look-back, W % 8 == 0): default for in-place embed and for extract;
-# "1" forces it everywhere, "0" forces the two-pass scan/locate/embed path; small
+# single pass (decoupled look-back, W % 8 == 0): the default wherever it applies;
+# "1" forces it, "0" forces the two-pass scan/locate/embed path; small
 # persistent grids exercise the slot loop
+# (batches under 32 run the single pass with flat slots + tickets by default;
+# "onepass_lanes" keeps the 8-lane slot mapping there)
 PATHS = {"auto": {}, "onepass": {"CODEC_PEE_ONEPASS": "1"}, "twopass": {"CODEC_PEE_ONEPASS": "0"},
+         "onepass_lanes": {"CODEC_PEE_ONEPASS": "1", "CODEC_PEE_FLAT_MAXB": "0"},
+         "onepass_flat_ticket": {"CODEC_PEE_ONEPASS": "1", "CODEC_PEE_FLAT_TICKET": "1", "CODEC_PEE_1P_WGS": "5"},
          "onepass_small_grid": {"CODEC_PEE_ONEPASS": "1", "CODEC_PEE_1P_WGS": "7", "CODEC_PEE_IP_WGS": "3"},
          # decode-side tile counts: workgroup-per-tile (block sums) instead of wave-per-tile,
          # and wave-per-tile with one workgroup per slice (every wave strides over tiles)
