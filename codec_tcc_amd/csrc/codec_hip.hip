@@ -696,8 +696,12 @@ __global__ __launch_bounds__(1024) void k_scan_read(const T* __restrict__ cover,
 // and are turned into argmax keys once the region is done.
 #define SCAN_ROWS_CNT_WORDS 7168   // 28 KiB of LDS = 14 336 block counters per workgroup
 // DIAG (timing diagnostics only, decisions are wrong): 1 = no histogram adds, 4 = copy with
-// the sweep's bookkeeping only, 5 = bare region copy (tools/ubench_stagger.hip's loop)
-template <typename T, int SB, bool NT, bool STORE, int DIAG = 0, bool PIPE = true>
+// the sweep's bookkeeping only, 5 = bare region copy (tools/ubench_stagger.hip's loop).
+// Measured in one process at 256 x 2048^2 (profiles/r01/ubench/scan_rows_diag.txt): full
+// kernel 0.800 ms, no histogram 0.762, bare region copy 0.757 -- the histogram, block
+// counts and key costs 5 % over the copy in this order.  U (vectors per thread per
+// iteration) = 4; U = 2 or 8 (pipelined or not) measured 0.83-0.84 ms.
+template <typename T, int SB, bool NT, bool STORE, int DIAG = 0, bool PIPE = true, int U = 4>
 __device__ __forceinline__ void scan_rows_body(const T* __restrict__ cover, T* __restrict__ stego,
                                                int H, int W, int bands_per_wg,
                                                uint32_t* __restrict__ ghist_all,
@@ -707,7 +711,7 @@ __device__ __forceinline__ void scan_rows_body(const T* __restrict__ cover, T* _
     constexpr int LG = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : 3;
     constexpr int LSB_ = SB == 8 ? 3 : SB == 16 ? 4 : SB == 32 ? 5 : 6;
     constexpr uint32_t NPB = (uint32_t)SB * SB;
-    constexpr int NT_ = 1024, U = 4;
+    constexpr int NT_ = 1024;
     __shared__ uint32_t lds[HistCfg<T>::kLdsWords];
     __shared__ uint32_t cnt[SCAN_ROWS_CNT_WORDS];
     __shared__ u64 wkey;
@@ -877,12 +881,12 @@ __device__ __forceinline__ void scan_rows_body(const T* __restrict__ cover, T* _
     if (threadIdx.x == 0 && wkey) atomicMax(&gkey[b], wkey);
 }
 
-template <typename T, int SB, bool NT, bool STORE, int DIAG = 0, bool PIPE = true>
+template <typename T, int SB, bool NT, bool STORE, int DIAG = 0, bool PIPE = true, int U = 4>
 __global__ __launch_bounds__(1024) void k_scan_rows(const T* __restrict__ cover, T* __restrict__ stego,
                                                     int H, int W, int bands_per_wg,
                                                     uint32_t* __restrict__ ghist_all,
                                                     u64* __restrict__ gkey, uint32_t* __restrict__ gor) {
-    scan_rows_body<T, SB, NT, STORE, DIAG, PIPE>(cover, stego, H, W, bands_per_wg, ghist_all, gkey, gor);
+    scan_rows_body<T, SB, NT, STORE, DIAG, PIPE, U>(cover, stego, H, W, bands_per_wg, ghist_all, gkey, gor);
 }
 
 // ------------------------------------------------------------------ K1': scan + copy (generic)
