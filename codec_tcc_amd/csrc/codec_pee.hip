@@ -1298,6 +1298,13 @@ static int pee_check(const codec_pee_params* P) {
     return 0;
 }
 
+// row H-1 of every slice, src -> dst (one strided 2-D copy)
+static hipError_t pee_copy_last_rows(const codec_pee_params* P, const void* src, void* dst, hipStream_t st) {
+    const size_t row = (size_t)P->W * P->bytes, pitch = (size_t)P->H * row, off = (size_t)(P->H - 1) * row;
+    return hipMemcpy2DAsync(static_cast<char*>(dst) + off, pitch, static_cast<const char*>(src) + off, pitch, row,
+                            (size_t)P->B, hipMemcpyDeviceToDevice, st);
+}
+
 extern "C" {
 
 size_t codec_pee_workspace_bytes(const codec_pee_params* P) {
@@ -1377,6 +1384,9 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
         }
 #undef PE1
         LAUNCH_CHECK("k_pee_embed1");
+        // odd H: the last row of each slice belongs to no row pair (no candidate, no MED
+        // neighbour); out of place it is copied verbatim
+        if ((P->H & 1) && !inplace) HIP_TRY(pee_copy_last_rows(P, cover, stego, st));
         return 0;
     }
     HIP_TRY(hipMemsetAsync(lm, 0, (size_t)P->B * P->lm_words * 8, st));
@@ -1490,6 +1500,7 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
         }
 #undef PX1
         LAUNCH_CHECK("k_pee_extract1");
+        if ((P->H & 1) && !inplace) HIP_TRY(pee_copy_last_rows(P, stego, cover_out, st));
         return 0;
     }
     const bool fused = vec && knob("CODEC_PEE_FUSED", 1) != 0 && (P->W % 8) == 0 && items > 0 && (items % 256) == 0 &&

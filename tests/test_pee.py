@@ -92,7 +92,7 @@ def _lengths(caps, bsz):
 @pytest.mark.parametrize("inplace", [False, True])
 @pytest.mark.parametrize("kind,h,w,bsz,T", [("ct12", 256, 256, 3, 2), ("ct12", 120, 136, 2, 1), ("u8", 96, 64, 2, 4),
                                             ("ct12", 37, 53, 2, 3), ("ct12", 2048, 2048, 2, 2), ("u16", 64, 64, 1, 8),
-                                            ("ct12", 66, 1024, 3, 2)])
+                                            ("ct12", 66, 1024, 3, 2), ("ct12", 65, 128, 3, 2), ("ct12", 33, 64, 33, 1)])
 def test_gpu_matches_oracle(kind, h, w, bsz, T, inplace, pee_path):
     torch = pytest.importorskip("torch")
     from codec_tcc_amd import _lib
