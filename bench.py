@@ -279,7 +279,7 @@ def bench_pee(args, torch, dist, world, dev, covers, B, H, W, inplace=False):
         res["algorithmic_bytes_per_step_half"] = by
         t_e = kern.get("k_pee_embed1", 0.0) / 1e3
         if t_e > 0:
-            tr = pmc_traffic("k_pee_embed1<unsigned short, true, true>", B, H, W, args.kind)
+            tr = pmc_traffic("k_pee_embed1<unsigned short, true, true>", B, H, W, getattr(args, "kind", "ct12"))
             res["roofline"] = {"bound": "hbm", "kernel": "k_pee_embed1", "achieved": round(by / t_e / 1e9, 1),
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(by / t_e / 1e9 / HBM_PEAK_GBS, 4),
                                "traffic": tr["hbm_bytes_per_launch"] if tr else None,
@@ -290,7 +290,7 @@ def bench_pee(args, torch, dist, world, dev, covers, B, H, W, inplace=False):
             t_k = kern[kname] / 1e3
             by = B * H * W * 4
             tr = pmc_traffic(kname + "<unsigned short, true, false>" if kname == "k_pee_embed1" else kname,
-                             B, H, W, args.kind)
+                             B, H, W, getattr(args, "kind", "ct12"))
             res["roofline"] = {"bound": "hbm", "kernel": kname, "achieved": round(by / t_k / 1e9, 1),
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(by / t_k / 1e9 / HBM_PEAK_GBS, 4),
                                "traffic": tr["hbm_bytes_per_launch"] if tr else None,
@@ -567,7 +567,7 @@ def main():
         roof = {"bound": "hbm", "kernel": sk, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "algorithmic_bytes_per_launch": bytes_scan, "avg_launch_ms": round(t_scan * 1e3, 4)}
-        tr = pmc_traffic(sk, B, H, W, args.kind)
+        tr = pmc_traffic(sk, B, H, W, getattr(args, "kind", "ct12"))
         if tr is not None:
             roof["traffic"] = tr["hbm_bytes_per_launch"]
             roof["traffic_source"] = tr["source"]

@@ -1041,11 +1041,26 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
             uint32_t base = excl;
             uint32_t unsafe_n = 0;
             const u64* payload = payload_all + (size_t)b * pw;
+            // an item's expandable candidates take consecutive ranks [rs, rs + n): the payload
+            // words holding them (one, or two across a word boundary) are loaded for all four
+            // items up front instead of one dependent load per embedded bit
+            uint32_t rs[4];
+            u64 plo[4], phi[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                rs[u] = base + (uint32_t)((pex >> (16 * u)) & 0xFFFFu);
+                base += (uint32_t)((ptot >> (16 * u)) & 0xFFFFu);
+                const uint32_t n = (uint32_t)((packed >> (16 * u)) & 0xFFFFu);
+                const uint32_t w = rs[u] >> 6;
+                const bool any = n && rs[u] < L;
+                plo[u] = any ? payload[w] : 0ull;
+                phi[u] = (any && (rs[u] & 63u) + n > 64u && (int)w + 1 < pw) ? payload[w + 1] : 0ull;
+            }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const uint32_t it = (uint32_t)c * PEE_CHUNK + u * 256u + tid;
-                uint32_t r = base + (uint32_t)((pex >> (16 * u)) & 0xFFFFu);
-                base += (uint32_t)((ptot >> (16 * u)) & 0xFFFFu);
+                uint32_t r = rs[u];
+                const uint32_t r64 = rs[u] & ~63u;
                 if (it >= items) continue;
                 bool touched = false;
                 uint32_t nib = 0;
@@ -1060,7 +1075,8 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                     int nv;
                     if (esm & bit) {
                         const int p = med3((int)get_px(a1[u], 2 * q), (int)get_px(a0[u], 2 * q + 1), (int)get_px(a0[u], 2 * q));
-                        const int pb = (int)((payload[r >> 6] >> (r & 63)) & 1ull);
+                        const uint32_t o = r - r64;        // < 64 + 4
+                        const int pb = (int)(((o < 64u ? plo[u] >> o : phi[u] >> (o - 64u))) & 1ull);
                         nv = p + 2 * (x - p) + pb;
                         if (r == L - 1) { M->end = k; M->tile_end = k / PEE_TILE; M->status = 0; }
                         ++r;
