@@ -1131,6 +1131,8 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
     __shared__ u64 sh64[8];
     __shared__ uint32_t s_v, s_excl;
     __shared__ int s_cmax;
+    // the chunk's recovered bits: ranks [excl, excl + agg), agg <= 4096, from word excl / 64
+    __shared__ u64 pbuf[PEE_CHUNK * 4 / 64 + 2];
     const int CR = W / 8;
     const uint32_t items = (uint32_t)(H / 2) * (uint32_t)CR;
     const size_t npx = (size_t)H * W;
@@ -1208,6 +1210,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
                 }
                 packed |= (u64)n << (16 * u);
             }
+            if (tid < PEE_CHUNK * 4 / 64 + 2) pbuf[tid] = 0;   // ordered by the scan's barriers
             u64 ptot;
             const u64 pex = block_excl_scan64<256>(packed, sh64, &ptot);
             const uint32_t agg = (uint32_t)((ptot & 0xFFFFu) + ((ptot >> 16) & 0xFFFFu) + ((ptot >> 32) & 0xFFFFu) + (ptot >> 48));
@@ -1227,7 +1230,9 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
                 }
             }
             __syncthreads();
-            uint32_t base = s_excl;
+            const uint32_t excl = s_excl;
+            const int w0 = (int)(excl >> 6);
+            uint32_t base = excl;
             u64* payload = payload_all + (size_t)b * pw;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -1247,7 +1252,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
                     if (innm & bit) {
                         if (e2 & 1) {
                             if (wi != (int)(r >> 6)) {
-                                if (wi >= 0) atomicOr(&payload[wi], word);
+                                if (wi >= 0) atomicOr(&pbuf[wi - w0], word);
                                 wi = (int)(r >> 6);
                                 word = 0;
                             }
@@ -1260,8 +1265,21 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
                     }
                     set_px(a1[u], 2 * q + 1, (uint32_t)nx);
                 }
-                if (wi >= 0 && word) atomicOr(&payload[wi], word);
+                if (wi >= 0 && word) atomicOr(&pbuf[wi - w0], word);
                 if (INPLACE) stv<NT>(reinterpret_cast<V*>(dst + o0[u] + W), a1[u]);
+            }
+            // one store per payload word instead of a global atomic per item: words wholly
+            // inside [excl, excl + agg) belong to this chunk alone; the first and last may be
+            // shared with the neighbouring chunks (OR-ed in); the host zeroed the payload
+            __syncthreads();
+            const int nw = (int)(((excl & 63u) + agg + 63u) >> 6);
+            if (tid < nw) {
+                const u64 wv = pbuf[tid];
+                if (wv) {
+                    const bool shared = (tid == 0 && (excl & 63u)) || (tid == nw - 1 && ((excl + agg) & 63u));
+                    if (shared) atomicOr(&payload[w0 + tid], wv);
+                    else payload[w0 + tid] = wv;
+                }
             }
         }
         if (!INPLACE) {
