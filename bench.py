@@ -578,6 +578,9 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u16",
             "data": "synthetic",
+            "value_path": "the reference's pixel path (bit-plane LSB embed + true decode, src/codec.py:412-487, "
+                          "752-793), bit-exact; the north star's MED-PEE embed+extract on the same batch is the "
+                          "'pee' object (the reference has no PEE code, SURVEY §0.1)",
             "config": {"workload": f"{args.kind} {H}x{W} uint16 x {B} slices/GPU, {args.payload_chars}-char "
                                    f"payload/slice, beta=0.4, block=16; encode(plan+embed)+decode(restore+gather)"
                                    + (f" + {'RCCL' if args.backend == 'nccl' else args.backend} all-gather of slice records/maps (side stream, overlapped with decode)"

@@ -16,7 +16,7 @@ def main():
     import torch
 
     from codec_tcc_amd import _lib
-    _lib.load(os.path.join(REPO, "tools", "bin", "libcodec_hip_dts.so"))
+    _lib.load(os.environ.get("DTS_LIB", os.path.join(REPO, "tools", "bin", "libcodec_hip_dts.so")))
     import bench
     import codec_tcc_amd as ct
     from codec_tcc_amd import synth
