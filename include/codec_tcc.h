@@ -208,8 +208,10 @@ typedef struct codec_pee_meta {
     int32_t reserved[3];
 } codec_pee_meta;
 
-/* meta.flags: the embed stopped reading after the chunk holding `end` (in-place embed),
- * so `capacity` counts expandable candidates up to that chunk only (a lower bound). */
+/* meta.flags: the single-pass embed (the default wherever W % 8 == 0 and the buffers are
+ * 16-B aligned) stopped counting after the chunk holding `end`, so `capacity` counts
+ * expandable candidates up to that chunk only (a lower bound; exact when the flag is clear,
+ * e.g. on overflow or on the two-pass path). */
 #define CODEC_PEE_PARTIAL 1
 /* meta.status values: 0 ok, 1 payload exceeds capacity (truncated, still reversible),
  * CODEC_PEE_ELOOKBACK: the single-pass cursor look-back gave up waiting for a predecessor
