@@ -53,11 +53,11 @@ struct ProfScope {   // records a start event now and the end event at scope exi
         if (g_prof.ev && g_prof.n < g_prof.cap) {
             slot = g_prof.n++;
             g_prof.tag[slot] = tag;
-            hipEventRecord(g_prof.ev[2 * slot], st);
+            (void)hipEventRecord(g_prof.ev[2 * slot], st);   // profiling only: a failed record leaves a 0 time
         }
     }
     ~ProfScope() {
-        if (slot >= 0) hipEventRecord(g_prof.ev[2 * slot + 1], st);
+        if (slot >= 0) (void)hipEventRecord(g_prof.ev[2 * slot + 1], st);
     }
 };
 
