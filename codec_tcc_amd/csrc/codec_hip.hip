@@ -42,6 +42,15 @@ __device__ __forceinline__ double np_leaf(const F& f, int a, int n) {
     double r4 = f(a + 4), r5 = f(a + 5), r6 = f(a + 6), r7 = f(a + 7);
     int i = 8;
     const int lim = n - (n % 8);
+    // two of numpy's 8-wide steps per iteration: all 16 (possibly indirect) loads are issued
+    // before the adds, which keep numpy's per-accumulator order (r_k += x_k, then x_{8+k})
+    for (; i + 8 < lim; i += 16) {
+        double x[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = f(a + i + k);
+        r0 += x[0]; r1 += x[1]; r2 += x[2]; r3 += x[3]; r4 += x[4]; r5 += x[5]; r6 += x[6]; r7 += x[7];
+        r0 += x[8]; r1 += x[9]; r2 += x[10]; r3 += x[11]; r4 += x[12]; r5 += x[13]; r6 += x[14]; r7 += x[15];
+    }
     for (; i < lim; i += 8) {
         r0 += f(a + i + 0); r1 += f(a + i + 1); r2 += f(a + i + 2); r3 += f(a + i + 3);
         r4 += f(a + i + 4); r5 += f(a + i + 5); r6 += f(a + i + 6); r7 += f(a + i + 7);
