@@ -1116,6 +1116,13 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
     codec_slice_meta* M = meta_all + b;
 
     DTS(0);
+    // fused embed: the slice's payload words (<= 2 KiB) go to LDS now, read by the embed
+    // loop after the decision instead of one dependent global load per bit
+    constexpr int kPaySh = EMBED ? 256 : 1;
+    __shared__ u64 pay_sh[kPaySh];
+    const bool pay_in_lds = EMBED && E.pw <= kPaySh;
+    if (EMBED && pay_in_lds)
+        for (int w = t; w < E.pw; w += 1024) pay_sh[w] = E.payload[(size_t)b * E.pw + w];
     // ---- bins that can be non-zero: [0, Rp), Rp = next power of two above OR(pixels)
     const uint32_t orv = gor[b];
     int Rp = orv ? (1 << (32 - __clz((int)orv))) : 1;
@@ -1552,7 +1559,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
                     const long long sbit = (long long)W.src[p] + i;
                     pl[k] = p;
                     ql[k] = q;
-                    mb[k] = (uint32_t)(pay[sbit >> 6] >> (sbit & 63)) & 1u;
+                    mb[k] = (uint32_t)((pay_in_lds ? pay_sh[sbit >> 6] : pay[sbit >> 6]) >> (sbit & 63)) & 1u;
                     orig[k] = cv[q];
                 }
             }
