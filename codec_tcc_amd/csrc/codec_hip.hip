@@ -1789,12 +1789,20 @@ template <typename T, bool NT, int NTH = 256>
 __global__ __launch_bounds__(NTH) void k_restore_gs(const T* __restrict__ stego, T* __restrict__ cover,
                                                     uint32_t npx, uint32_t nchunks, uint32_t total_chunks,
                                                     const codec_slice_meta* __restrict__ meta,
-                                                    const u64* __restrict__ maps_all, int mw) {
+                                                    const u64* __restrict__ maps_all, int mw,
+                                                    int gather_wgs, u64* __restrict__ payload_out, int pw) {
     typedef typename Vec8<T>::type V;
+    // the first gather_wgs workgroups gather the payload of slice blockIdx.x (dispatched first,
+    // they overlap the stream instead of a separate launch after it)
+    if ((int)blockIdx.x < gather_wgs) {
+        gather_body<T, NTH>(stego, (long long)npx, meta, payload_out, pw, (int)blockIdx.x);
+        return;
+    }
+    const uint32_t wg = blockIdx.x - (uint32_t)gather_wgs;
     const V* src = reinterpret_cast<const V*>(stego);
     V* dst = reinterpret_cast<V*>(cover);
-    const uint32_t stride = gridDim.x * (4u * NTH);
-    for (uint32_t base = blockIdx.x * (4u * NTH); base < total_chunks; base += stride) {
+    const uint32_t stride = (gridDim.x - (uint32_t)gather_wgs) * (4u * NTH);
+    for (uint32_t base = wg * (4u * NTH); base < total_chunks; base += stride) {
         const uint32_t cb = base + threadIdx.x;
         V vv[4];
 #pragma unroll
@@ -1860,21 +1868,23 @@ __global__ __launch_bounds__(256) void k_restore_scalar(const T* __restrict__ st
 // payload bits back out of the windows: one 1024-thread workgroup per slice, 8 bits per
 // thread per round with all loads issued first; every payload word is written (zeros past
 // total_used), so the caller needs no memset
-template <typename T>
-__global__ __launch_bounds__(1024) void k_gather(const T* __restrict__ stego, long long npx,
-                                                 const codec_slice_meta* __restrict__ meta,
-                                                 u64* __restrict__ out, int pw) {
+// payload bits of slice b back out of its windows (ballot-packed, 8 loads in flight per
+// thread per round); NTH threads.  Used by k_gather and as the leading workgroups of
+// k_restore_gs (codec_extract out of place: the two read the stego independently)
+template <typename T, int NTH>
+__device__ __forceinline__ void gather_body(const T* __restrict__ stego, long long npx,
+                                            const codec_slice_meta* __restrict__ meta,
+                                            u64* __restrict__ out, int pw, int b) {
     __shared__ SliceWin W;
-    const int b = blockIdx.x;
     load_win(meta + b, &W);
     const T* sv = stego + (size_t)b * npx;
     const int t = threadIdx.x;
-    for (int j0 = 0; j0 < pw * 64; j0 += 8 * 1024) {
+    for (int j0 = 0; j0 < pw * 64; j0 += 8 * NTH) {
         uint32_t v[8];
         int pl[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const int j = j0 + k * 1024 + t;
+            const int j = j0 + k * NTH + t;
             pl[k] = -1;
             v[k] = 0;
             if (j < W.tot) {
@@ -1888,12 +1898,19 @@ __global__ __launch_bounds__(1024) void k_gather(const T* __restrict__ stego, lo
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            if (j0 + k * 1024 >= pw * 64) break;                 // uniform
-            const int j = j0 + k * 1024 + t;
+            if (j0 + k * NTH >= pw * 64) break;                  // uniform
+            const int j = j0 + k * NTH + t;
             const u64 bal = __ballot(pl[k] >= 0 ? (v[k] >> pl[k]) & 1u : 0u);
             if ((t & 63) == 0 && (j >> 6) < pw) out[(size_t)b * pw + (j >> 6)] = bal;
         }
     }
+}
+
+template <typename T>
+__global__ __launch_bounds__(1024) void k_gather(const T* __restrict__ stego, long long npx,
+                                                 const codec_slice_meta* __restrict__ meta,
+                                                 u64* __restrict__ out, int pw) {
+    gather_body<T, 1024>(stego, npx, meta, out, pw, blockIdx.x);
 }
 
 // in-place restore: XOR every window bit with its location-map bit (only the <= T window
@@ -2437,6 +2454,8 @@ int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps
     const long long npx = (long long)P->H * P->W;
     hipStream_t st = as_stream(stream);
     const bool inplace = cover_out == stego;   // restore only the window pixels, after the gather
+    if (payload_out && P->payload_words < 1) return set_err(CODEC_EINVAL, "payload_words must be >= 1");
+    bool gathered = false;                     // done by k_restore_gs's leading workgroups
     if (cover_out && !inplace) {
         const size_t va = P->in_bytes == 2 ? 16 : 8;
         if ((uintptr_t)stego % va || (uintptr_t)cover_out % va || ((npx * P->in_bytes) % va)) {
@@ -2464,12 +2483,20 @@ int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps
             long long grid = (total + 4LL * nth - 1) / (4LL * nth);
             if (grid > g) grid = g;
             if (grid < 1) grid = 1;
+            // payload gather: B leading workgroups of the same launch (CODEC_FUSED_GATHER=0: a
+            // separate k_gather launch after the restore)
+            const int gw = (payload_out && knob("CODEC_FUSED_GATHER", 1) != 0) ? P->B : 0;
+            grid += gw;
+            gathered = gw > 0;
             ProfScope prof(st, CODEC_K_RESTORE);
             const u64* mp = reinterpret_cast<const u64*>(maps);
+            u64* po = reinterpret_cast<u64*>(payload_out);
 #define RGS(TT, NTV) if (nth == 1024) hipLaunchKernelGGL((k_restore_gs<TT, NTV, 1024>), dim3((unsigned)grid), dim3(1024), 0, st, \
-                static_cast<const TT*>(stego), static_cast<TT*>(cover_out), (uint32_t)npx, (uint32_t)nchunks, total, meta, mp, P->map_words); \
+                static_cast<const TT*>(stego), static_cast<TT*>(cover_out), (uint32_t)npx, (uint32_t)nchunks, total, meta, mp, P->map_words, \
+                gw, po, P->payload_words); \
             else hipLaunchKernelGGL((k_restore_gs<TT, NTV>), dim3((unsigned)grid), dim3(256), 0, st, \
-                static_cast<const TT*>(stego), static_cast<TT*>(cover_out), (uint32_t)npx, (uint32_t)nchunks, total, meta, mp, P->map_words)
+                static_cast<const TT*>(stego), static_cast<TT*>(cover_out), (uint32_t)npx, (uint32_t)nchunks, total, meta, mp, P->map_words, \
+                gw, po, P->payload_words)
             if (P->in_bytes == 2) { if (ntg) RGS(uint16_t, true); else RGS(uint16_t, false); }
             else { if (ntg) RGS(uint8_t, true); else RGS(uint8_t, false); }
 #undef RGS
@@ -2501,8 +2528,7 @@ int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps
         LAUNCH_CHECK("k_restore");
         }
     }
-    if (payload_out) {
-        if (P->payload_words < 1) return set_err(CODEC_EINVAL, "payload_words must be >= 1");
+    if (payload_out && !gathered) {
         ProfScope prof(st, CODEC_K_GATHER);
         dim3 grid(P->B);
         if (P->in_bytes == 2)
