@@ -203,7 +203,8 @@ class Codec:
         ws = lib.codec_workspace_bytes(C.byref(self.P))
         if ws == 0:
             _lib.check(-1, "codec_workspace_bytes")
-        self.workspace = torch.empty(int(ws), dtype=torch.uint8, device=self.device)
+        # zero once: codec_plan expects clean histogram words and leaves them clean
+        self.workspace = torch.zeros(int(ws), dtype=torch.uint8, device=self.device)
         self.lut = log2_table(self.H * self.W, self.device)
 
     # -- helpers

@@ -1081,9 +1081,9 @@ struct EmbedArgs {
 };
 
 template <typename T, bool EMBED = false>
-__global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t* __restrict__ ghist_all,
-                                                 const uint32_t* __restrict__ gor, double* __restrict__ gterms,
-                                                 const u64* __restrict__ gkey, const double* __restrict__ exact,
+__global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __restrict__ ghist_all,
+                                                 uint32_t* __restrict__ gor, double* __restrict__ gterms,
+                                                 u64* __restrict__ gkey, const double* __restrict__ exact,
                                                  int exact_cap, int exact_edge_only, int fast_blocks,
                                                  const double* __restrict__ lut, long long lut_len,
                                                  const codec_layout* __restrict__ table,
@@ -1585,6 +1585,22 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, const uint32_t*
             }
         }
         DTS(11);
+    }
+    // leave the workspace clean for the next call (codec_plan does not memset it): every
+    // histogram bin the scan can have touched lies below max(Rp, 2) (pixel values < Rp; a
+    // 16-bit wrap fix-up also writes bin v + 1 <= Rp - 1, or bin 1 when Rp = 1), plus the
+    // slice's block key and OR word.  All reads of them precede this barrier.
+    __syncthreads();
+    {
+        const int zr = Rp < 2 ? 2 : Rp;
+        uint32_t* hz = ghist_all + (size_t)b * R;
+        if ((zr & 3) == 0) {
+            uint4* h4 = reinterpret_cast<uint4*>(hz);
+            for (int v = t; v < zr / 4; v += 1024) h4[v] = make_uint4(0u, 0u, 0u, 0u);
+        } else {
+            for (int v = t; v < zr; v += 1024) hz[v] = 0u;
+        }
+        if (t == 0) { gkey[b] = 0ull; gor[b] = 0u; }
     }
 }
 
@@ -2343,7 +2359,14 @@ static int plan_impl(const codec_params* P, const void* cover, void* stego, cons
     uint32_t* orv = reinterpret_cast<uint32_t*>(ws + L.orv);
     double* exact = reinterpret_cast<double*>(ws + L.exact);
     double* terms = reinterpret_cast<double*>(ws + L.terms);
-    HIP_TRY(hipMemsetAsync(ws, 0, L.exact, st));   // histograms, block keys, OR words
+    // histograms, block keys, OR words: zero on entry.  The caller zero-initialises the
+    // workspace once and k_decide clears what it consumed, so no per-call memset
+    // (CODEC_HIST_MEMSET=1 restores it); an error after the scan re-clears it below.
+    if (knob("CODEC_HIST_MEMSET", 0)) HIP_TRY(hipMemsetAsync(ws, 0, L.exact, st));
+    auto reclear = [&](int err) {
+        (void)hipMemsetAsync(ws, 0, L.exact, st);
+        return err;
+    };
 
     if (stego == cover && P->in_bytes != P->out_bytes)
         return set_err(CODEC_EINVAL, "codec_plan: in place (stego == cover) needs one pixel dtype");
@@ -2360,7 +2383,7 @@ static int plan_impl(const codec_params* P, const void* cover, void* stego, cons
         rc = P->out_bytes == 2 ? launch_scan_generic<uint8_t, uint16_t>(P, cover, stego, hist, orv, st)
                                : launch_scan_generic<uint8_t, uint8_t>(P, cover, stego, hist, orv, st);
     }
-    if (rc) return rc;
+    if (rc) return reclear(rc);
 
     const bool need_blocks = P->mode == CODEC_MODE_HYBRID && P->fixed_offset < 0;
     const int edge_only = fast ? 1 : 0;
@@ -2374,7 +2397,8 @@ static int plan_impl(const codec_params* P, const void* cover, void* stego, cons
         else
             hipLaunchKernelGGL(k_block_exact<uint8_t>, grid, dim3(256), 0, st, static_cast<const uint8_t*>(cover),
                                P->H, P->W, P->block, edge_only, exact, L.exact_cap);
-        LAUNCH_CHECK("k_block_exact");
+        const hipError_t e1 = hipGetLastError();
+        if (e1 != hipSuccess) return reclear(set_err(-(int)e1, "launch k_block_exact: %s", hipGetErrorString(e1)));
     }
     codec_params Pv = *P;
     // bit 0: force the block-sequential decision; bit 1: no walk path for wide slices
@@ -2386,7 +2410,8 @@ static int plan_impl(const codec_params* P, const void* cover, void* stego, cons
     if (P->in_bytes == 2) { if (E) DEC(uint16_t, true); else DEC(uint16_t, false); }
     else { if (E) DEC(uint8_t, true); else DEC(uint8_t, false); }
 #undef DEC
-    LAUNCH_CHECK("k_decide");
+    const hipError_t e2 = hipGetLastError();
+    if (e2 != hipSuccess) return reclear(set_err(-(int)e2, "launch k_decide: %s", hipGetErrorString(e2)));
     return 0;
 }
 

@@ -93,7 +93,11 @@ typedef struct codec_slice_meta {
 int codec_abi_version(void);
 const char* codec_last_error(void);
 
-/* Bytes of scratch `codec_plan` needs for these parameters. */
+/* Bytes of scratch `codec_plan` needs for these parameters.  Zero-initialise the workspace
+ * once before its first use: codec_plan / codec_encode expect its histogram words clear and
+ * leave them clear (the decision kernel zeroes what the scan wrote), so no call memsets it
+ * (env CODEC_HIST_MEMSET=1 restores a per-call memset).  A call that fails after launching
+ * the scan re-clears it on the stream. */
 size_t codec_workspace_bytes(const codec_params* P);
 
 /* Decomposition + block search + segment plan, and the cover->stego copy:

@@ -328,3 +328,33 @@ def test_wide_slices_information_exact(kind, h, w, decide_path):
     exp = R.encode_slice(cover, R.message_to_bits(synth.payload(100, 1)), beta=0.8, sb=16)
     assert m.s == exp["s"]
     np.testing.assert_array_equal(enc.stego.cpu().numpy()[0], exp["stego"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,kinds", [("uint16", ["u16", "ct12", "zero", "ct12", "u16"]),
+                                         ("uint8", ["u8", "zero", "u8"])])
+def test_workspace_reuse_stays_clean(dtype, kinds, monkeypatch):
+    """codec_plan does not memset its workspace per call: k_decide clears the histogram
+    bins, block key and OR word it consumed.  One Codec over batches of different value
+    ranges (wide, narrow, constant zero, back to wide) must match the oracle on every call.
+    One scan workgroup per slice, so the 262 144 zeros of a slice wrap the 16-bit LDS bin
+    halves (the wrap fix-up writes bin 1, above Rp = 1)."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("CODEC_SCAN_WGS", "1")
+    monkeypatch.setenv("CODEC_SCAN_ROWS_WGS", "1")
+    B, H, W = 2, 512, 512
+    codec = Codec(B, H, W, dtype=dtype, beta=0.4, block=16, device="cuda")
+    for step, kind in enumerate(kinds):
+        if kind == "zero":
+            covers = np.zeros((B, H, W), dtype=dtype)
+        else:
+            covers = np.stack([synth.GENERATORS[kind](H, W, 60 + 7 * step + i) for i in range(B)]).astype(dtype)
+        msgs = [synth.payload(200 + 30 * i, 90 + step + i) for i in range(B)]
+        enc = codec.encode(torch.from_numpy(covers).cuda(), msgs)
+        recs = enc.records()
+        stego = enc.stego.cpu().numpy()
+        for i in range(B):
+            exp = R.encode_slice(covers[i], R.message_to_bits(msgs[i]), beta=0.4, sb=16)
+            assert recs[i].s == exp["s"], (step, kind, i)
+            assert recs[i].start_offset == exp["start_offset"], (step, kind, i)
+            np.testing.assert_array_equal(stego[i], exp["stego"])
