@@ -1436,6 +1436,18 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
     }
     if (!need_decision) s = P.fixed_s;
 
+    // the slice's segment layout for its s (64 ints), loaded by one wave in one round trip
+    // while the offset is found, instead of thread 0's dependent loads in the windows loop
+    __shared__ int32_t lay_sh[sizeof(codec_layout) / 4];
+    static_assert(sizeof(codec_layout) / 4 <= 64, "one wave loads the layout");
+    if (t == 0) ctl_sh[1] = s;
+    __syncthreads();
+    {
+        const int sl = min(max(ctl_sh[1], 1), 16);
+        if (t < (int)(sizeof(codec_layout) / 4))
+            lay_sh[t] = reinterpret_cast<const int32_t*>(table + (size_t)slice_class[b] * 16 + (sl - 1))[t];
+    }
+
     DTS(3);
     // ---- start offset: first maximal float(np.var) block in raster order (codec.py:441-453)
     const int sb = P.block;
@@ -1477,6 +1489,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
         }
     }
 
+    __syncthreads();   // lay_sh
     DTS(4);
     if (t == 0) {   // ---- windows and the slice record (thread 0)
     int offset = 0;
@@ -1485,7 +1498,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
     if (offset < 0 || (long long)offset >= npx) offset = 0;   // no block scored (never for valid stats)
 
     // ---- segment windows (codec.py:455-485 / 288-316)
-    const codec_layout& L = table[(size_t)slice_class[b] * 16 + (s - 1)];
+    const codec_layout& L = *reinterpret_cast<const codec_layout*>(lay_sh);
     uint32_t flags = 0;
     int pos = offset, cat = 0;
     for (int j = 0; j < s; ++j) {
