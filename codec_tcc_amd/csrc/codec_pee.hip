@@ -1225,7 +1225,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
                     if (tid == 0) {
                         if (c < cend) lb_store(st + c, LB_INC | (u64)(ex + agg));
                         s_excl = ex;
-                        if (to) atomicOr(ctl + 1, 1u);   // reported by codec_pee_extract's status word
+                        if (to) atomicOr(ctl + 1, 1u);   // host: codec_pee_extract_flag_offset
                     }
                 }
             }
@@ -1344,6 +1344,11 @@ extern "C" {
 size_t codec_pee_workspace_bytes(const codec_pee_params* P) {
     if (pee_check(P)) return 0;
     return pee_ws(P).total;
+}
+
+size_t codec_pee_extract_flag_offset(const codec_pee_params* P) {
+    if (pee_check(P)) return 0;
+    return pee_ws(P).ctl + 4;   // ctl[1]: set when an extract chunk's look-back gave up
 }
 
 int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, const uint64_t* payload,
@@ -1536,6 +1541,10 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
         LAUNCH_CHECK("k_pee_extract1");
         if ((P->H & 1) && !inplace) HIP_TRY(pee_copy_last_rows(P, stego, cover_out, st));
         return 0;
+    }
+    {   // the single pass's look-back flag (codec_pee_extract_flag_offset) stays clear here
+        uint32_t* ctl = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.ctl);
+        HIP_TRY(hipMemsetAsync(ctl + 1, 0, 4, st));
     }
     const bool fused = vec && knob("CODEC_PEE_FUSED", 1) != 0 && (P->W % 8) == 0 && items > 0 && (items % 256) == 0 &&
                        items * P->B < 0xFFFFFFFFLL;

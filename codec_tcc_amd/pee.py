@@ -108,6 +108,10 @@ class PeeCodec:
             raise ValueError(f"payload exceeds PEE capacity in slices {bad} (T={self.T})")
         words, cover = self.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words)
         host = words.cpu().numpy()
+        off = int(_lib.load().codec_pee_extract_flag_offset(C.byref(self._params(enc.payload_words))))
+        if off and int(self.workspace[off:off + 4].view(_torch().int32).item()) != 0:
+            raise RuntimeError("codec_pee_extract: cursor look-back timed out (out-of-order workgroup "
+                               "dispatch); re-run with CODEC_PEE_ONEPASS=0")
         return [framing.unpack_bits(host[i], enc.lengths[i]) for i in range(self.B)], cover
 
 

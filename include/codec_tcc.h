@@ -223,6 +223,10 @@ typedef struct codec_pee_meta {
 #define CODEC_PEE_ELOOKBACK 2
 
 size_t codec_pee_workspace_bytes(const codec_pee_params* P);
+/* Byte offset in the workspace of a uint32 flag that codec_pee_extract's single pass sets
+ * (non-zero) when a chunk's cursor look-back gave up (CODEC_PEE_ELOOKBACK on the decode
+ * side); cleared at the start of every codec_pee_extract.  0 on bad parameters. */
+size_t codec_pee_extract_flag_offset(const codec_pee_params* P);
 /* cover -> stego (full copy + expansion/shifting of candidates 0..end), lm, meta.
  * lengths[B] (device int32) = payload bits per slice.
  * stego == cover is allowed (in place): only the items up to `end` are read and

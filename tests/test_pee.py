@@ -255,3 +255,27 @@ def test_gpu_onepass_slot_orders(cfg, monkeypatch):
         n = min(lens[i], caps[i])
         np.testing.assert_array_equal(framing.unpack_bits(host[i], n), payloads[i][:n])
     np.testing.assert_array_equal(cover.cpu().numpy(), covers)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("onepass", ["1", "0"])
+def test_gpu_extract_lookback_flag_clear(onepass, monkeypatch):
+    """The decode-side look-back flag (codec_pee_extract_flag_offset) lies inside the
+    workspace and reads 0 after a normal extract on both paths; PeeCodec.decode checks it."""
+    torch = pytest.importorskip("torch")
+    import ctypes as C
+
+    from codec_tcc_amd import _lib
+    from codec_tcc_amd.pee import PeeCodec
+    monkeypatch.setenv("CODEC_PEE_ONEPASS", onepass)
+    covers = np.stack([synth.ct12(256, 256, 700 + i) for i in range(3)])
+    payloads = [_bits(900 + 50 * i, 800 + i) for i in range(3)]
+    codec = PeeCodec(3, 256, 256, T=2)
+    enc = codec.embed(torch.from_numpy(covers).cuda(), payloads)
+    bits, cover = codec.decode(enc)
+    off = int(_lib.load().codec_pee_extract_flag_offset(C.byref(codec._params(enc.payload_words))))
+    assert 0 < off and off + 4 <= codec.workspace.numel() and off % 4 == 0
+    assert int(codec.workspace[off:off + 4].view(torch.int32).item()) == 0
+    for i in range(3):
+        np.testing.assert_array_equal(np.asarray(bits[i]), payloads[i])
+    np.testing.assert_array_equal(cover.cpu().numpy(), covers)
