@@ -270,6 +270,9 @@ def bench_pee(args, torch, dist, world, dev, covers, B, H, W, inplace=False):
     res = {"value": round(B * H * W * world * args.steps / el / 1e6, 1), "unit": "Mpixels/s",
            "ms_per_step": round(el / args.steps * 1e3, 4), "T": args.pee_T, "roundtrip_ok": ok,
            "end_candidates_mean": float(np.mean([r.end + 1 for r in recs])),
+           # slices whose payload exceeds the T-capacity (truncated, still exactly reversible;
+           # roundtrip_ok then reads False): uniform-noise slices at T=2
+           "overflow_slices": int(sum(1 for r in recs if r.status == 1)),
            "kernels_ms": {k: round(v, 4) for k, v in kern.items()}}
     if inplace:
         # algorithmic bytes: every 8-px x 2-row item up to the one holding `end` is read
