@@ -85,6 +85,7 @@ _SIGS = {
     "codec_merge_planes": (C.c_int, [C.POINTER(Params), _VP, C.c_int32, C.c_int32, _VP, _VP]),
     "codec_pee_workspace_bytes": (C.c_size_t, [C.POINTER(PeeParams)]),
     "codec_pee_extract_flag_offset": (C.c_size_t, [C.POINTER(PeeParams)]),
+    "codec_pee_diag_offset": (C.c_size_t, [C.POINTER(PeeParams)]),
     "codec_pee_embed": (C.c_int, [C.POINTER(PeeParams), _VP, _VP, _VP, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),
     "codec_pee_extract": (C.c_int, [C.POINTER(PeeParams), _VP, _VP, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),
     "codec_quality_moments": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP, _VP, _VP, _VP]),

@@ -769,51 +769,134 @@ __device__ __forceinline__ uint32_t ld_agent(uint32_t* p) {
 }
 
 // wave 0 of the block: exclusive prefix of chunk c (>= 1) from st[0..c-1].  The spin is
-// bounded: a predecessor that never publishes (it would take out-of-order workgroup
-// dispatch) sets *timeout instead of hanging the GPU, and the caller flags the slice.
+// bounded (spin_max polls).  Out of place the source buffer is never written, so a
+// predecessor that has not published its aggregate by then (it would take out-of-order
+// workgroup dispatch, or a workgroup that is not resident) has it computed from its pixels
+// by this wave (`count`, e.g. EmbedCount) and published for the other waiters: the prefix
+// is exact either way and *fallback is set (a diagnostic count).  In place (NoFallback) the
+// predecessor may be rewriting its pixels, so a timeout sets *timeout and the caller flags
+// the slice (sticky status, the host raises) instead of hanging the GPU.
 // `done` (optional): the slice's finished flag.  It can only be set once every chunk before
 // the one holding `end` has published, so a waiter that sees it set lies past `end` and
 // returns `sat` (>= L) instead of waiting for predecessors that may never publish.
 #ifndef PEE_LB_SLEEP
 #define PEE_LB_SLEEP 1
 #endif
-#ifndef PEE_LB_POLL1
-#define PEE_LB_POLL1 0
-#endif
-__device__ uint32_t lb_exclusive(u64* st, int c, bool* timeout, uint32_t* done = nullptr, uint32_t sat = 0) {
+struct NoFallback {
+    static constexpr bool can = false;
+    __device__ uint32_t operator()(int) const { return 0u; }
+};
+
+// expandable, non-overflow candidates of chunk j (the embed's aggregate), counted by the
+// calling wave (16 items per lane) and returned to every lane
+template <typename T>
+struct EmbedCount {
+    static constexpr bool can = true;
+    const T* src;
+    int W, CR;
+    uint32_t items;
+    int Tthr, maxval;
+    __device__ uint32_t operator()(int j) const {
+        typedef typename Vec8<T>::type V;
+        const int lane = threadIdx.x & 63;
+        uint32_t n = 0;
+        for (int u = 0; u < PEE_CHUNK / 64; ++u) {
+            const uint32_t it = (uint32_t)j * PEE_CHUNK + (uint32_t)(u * 64 + lane);
+            if (it >= items) break;
+            const uint32_t r = it / (uint32_t)CR, cc = it - r * (uint32_t)CR;
+            const size_t o0 = (size_t)(2 * r) * W + (size_t)cc * 8;
+            const V v0 = *reinterpret_cast<const V*>(src + o0);
+            const V v1 = *reinterpret_cast<const V*>(src + o0 + W);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const PeeCand pc = pee_classify((int)get_px(v1, 2 * q + 1), (int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1),
+                                                (int)get_px(v0, 2 * q), Tthr, maxval);
+                n += (pc.expand && pc.safe) ? 1u : 0u;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) n += __shfl_xor(n, o, 64);
+        return n;
+    }
+};
+
+// inner candidates of chunk j (the extract's aggregate): not in the location map, k <= end,
+// -2T <= e' < 2T -- counted from the stego by the calling wave
+template <typename T>
+struct ExtractCount {
+    static constexpr bool can = true;
+    const T* src;
+    const u64* lm;
+    int W, CR;
+    uint32_t items;
+    int end, Tthr;
+    __device__ uint32_t operator()(int j) const {
+        typedef typename Vec8<T>::type V;
+        const int lane = threadIdx.x & 63;
+        uint32_t n = 0;
+        for (int u = 0; u < PEE_CHUNK / 64; ++u) {
+            const uint32_t it = (uint32_t)j * PEE_CHUNK + (uint32_t)(u * 64 + lane);
+            if (it >= items || (int)(4 * it) > end) break;
+            const uint32_t r = it / (uint32_t)CR, cc = it - r * (uint32_t)CR;
+            const size_t o0 = (size_t)(2 * r) * W + (size_t)cc * 8;
+            const V v0 = *reinterpret_cast<const V*>(src + o0);
+            const V v1 = *reinterpret_cast<const V*>(src + o0 + W);
+            const u64 lw = lm[(4 * it) >> 6] >> ((4 * it) & 63);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if ((int)(4 * it) + q > end || ((lw >> q) & 1ull)) continue;
+                const int e2 = (int)get_px(v1, 2 * q + 1) - med3((int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1), (int)get_px(v0, 2 * q));
+                n += (e2 >= -2 * Tthr && e2 < 2 * Tthr) ? 1u : 0u;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) n += __shfl_xor(n, o, 64);
+        return n;
+    }
+};
+
+template <typename F>
+__device__ uint32_t lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, uint32_t spin_max, const F& count,
+                                 uint32_t* done = nullptr, uint32_t sat = 0) {
     const int lane = threadIdx.x & 63;
     uint32_t excl = 0;
     int p = c - 1;
     uint32_t spins = 0;
-#if PEE_LB_POLL1
-    // wait on the nearest predecessor alone first (one lane polls, not 64)
-    for (;;) {
-        const u64 w0 = lb_load(st + p);
-        if (__builtin_amdgcn_readfirstlane((uint32_t)(w0 >> 62)) != 0u) break;
-        if (done && ld_agent(done)) return sat;
-        if (++spins > (1u << 22)) {
-            *timeout = true;
-            return excl;
-        }
-        __builtin_amdgcn_s_sleep(PEE_LB_SLEEP);
-    }
-#endif
     for (;;) {
         const int idx = p - lane;
-        const u64 w = idx >= 0 ? lb_load(st + idx) : LB_INC;
-        const uint32_t fl = (uint32_t)(w >> 62);
-        const u64 inc = __ballot(fl == 2u);
+        u64 w = idx >= 0 ? lb_load(st + idx) : LB_INC;
+        uint32_t fl = (uint32_t)(w >> 62);
+        u64 inc = __ballot(fl == 2u);
         const u64 notready = __ballot(fl == 0u);
-        const int first = inc ? (int)__builtin_ctzll(inc) : 64;          // nearest inclusive
-        const u64 need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);  // lanes 0..first
+        int first = inc ? (int)__builtin_ctzll(inc) : 64;                // nearest inclusive
+        u64 need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);       // lanes 0..first
         if (notready & need) {
             if (done && ld_agent(done)) return sat;
-            if (++spins > (1u << 22)) {
+            if (++spins <= spin_max) {
+                __builtin_amdgcn_s_sleep(PEE_LB_SLEEP);
+                continue;
+            }
+            if constexpr (!F::can) {
                 *timeout = true;
                 return excl;
+            } else {
+                // the missing aggregates from the pixels, one chunk per round of the wave; a
+                // chunk that published meanwhile keeps its own word (CAS from 0 only)
+                u64 m = notready & need;
+                while (m) {
+                    const int l = (int)__builtin_ctzll(m);
+                    m &= m - 1ull;
+                    const uint32_t a = count(p - l);
+                    if (lane == l) {
+                        const u64 mine = LB_AGG | (u64)a;
+                        atomicCAS(reinterpret_cast<unsigned long long*>(st + idx), 0ull, (unsigned long long)mine);
+                        w = mine;
+                        fl = 1u;
+                    }
+                }
+                *fallback = true;
+                spins = 0;
             }
-            __builtin_amdgcn_s_sleep(PEE_LB_SLEEP);
-            continue;
         }
         uint32_t v = lane <= first ? (uint32_t)w : 0u;
 #pragma unroll
@@ -892,8 +975,16 @@ __host__ __device__ __forceinline__ uint32_t pee_total_slots(int B, int nchunks,
 // launch mode of the out-of-place single pass: chunk-major slot order, and chunk = slot
 // (no ticket).  Without the ticket the look-back's forward progress rests on in-order
 // workgroup dispatch within an XCD (a slice's chunks all sit on one XCD, pee_slot): every
-// predecessor of a resident workgroup has then been dispatched; lb_exclusive's bounded spin
-// still turns a violation into CODEC_PEE_ELOOKBACK instead of a hang.
+// predecessor of a resident workgroup has then been dispatched.  Should that ever fail,
+// lb_exclusive's bounded spin falls back to counting the missing predecessors from their
+// pixels (the cover is read-only out of place), so the result stays exact and nothing hangs.
+// In place (ticketed: a predecessor always holds an earlier ticket and is resident) a
+// timeout flags the slice with the sticky status CODEC_PEE_ELOOKBACK.
+// dbg_skip >= 0 (CODEC_PEE_DEBUG_SKIP = chunk + 1, tests only): that chunk of slice 0 never
+// publishes its aggregate/prefix, so its successors time out and take the fallback (out of
+// place) or flag the slice (in place).
+// diag[0] / diag[2]: chunks whose look-back used the pixel fallback / timed out unrecovered
+// (cumulative since the workspace was zeroed; codec_pee_diag_offset).
 #define PEE_MODE_CMAJOR 1
 #define PEE_MODE_NOTICKET 2
 #define PEE_CTL_WORDS(B) (32 + 32 * (size_t)(B))
@@ -904,7 +995,8 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                                                     int maxval, const int32_t* __restrict__ lengths,
                                                     const u64* __restrict__ payload_all, int pw, int nchunks, int B,
                                                     u64* status_all, uint32_t* ctl, codec_pee_meta* meta_all,
-                                                    u64* __restrict__ lm_all, int lmw, int mode) {
+                                                    u64* __restrict__ lm_all, int lmw, int mode, uint32_t spin_max,
+                                                    int dbg_skip, uint32_t* diag) {
     typedef typename Vec8<T>::type V;
     __shared__ u64 sh64[8];
     __shared__ uint32_t sh[8];
@@ -1005,17 +1097,22 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
         u64 ptot;
         const u64 pex = block_excl_scan64<256>(packed, sh64, &ptot);
         const uint32_t agg = (uint32_t)((ptot & 0xFFFFu) + ((ptot >> 16) & 0xFFFFu) + ((ptot >> 32) & 0xFFFFu) + (ptot >> 48));
+        const bool publish = !(b == 0 && c == dbg_skip);
         if (c == 0) {
-            if (tid == 0) { lb_store(st, LB_INC | (u64)agg); s_excl = 0; }
+            if (tid == 0) { if (publish) lb_store(st, LB_INC | (u64)agg); s_excl = 0; }
         } else {
-            if (tid == 0) lb_store(st + c, LB_AGG | (u64)agg);
+            if (tid == 0 && publish) lb_store(st + c, LB_AGG | (u64)agg);
             if (tid < 64) {
-                bool to = false;
-                const uint32_t ex = lb_exclusive(st, c, &to, tick + 1, L);
+                bool to = false, fb = false;
+                uint32_t ex;
+                if (INPLACE) ex = lb_exclusive(st, c, &to, &fb, spin_max, NoFallback(), tick + 1, L);
+                else ex = lb_exclusive(st, c, &to, &fb, spin_max, EmbedCount<T>{src, W, CR, items, Tthr, maxval}, tick + 1, L);
                 if (tid == 0) {
-                    lb_store(st + c, LB_INC | (u64)(ex + agg));
+                    if (publish) lb_store(st + c, LB_INC | (u64)(ex + agg));
                     s_excl = ex;
-                    if (to) M->status = CODEC_PEE_ELOOKBACK;
+                    // sticky: the status words are only ever raised (atomicMax) after this
+                    if (to) { atomicMax(&M->status, CODEC_PEE_ELOOKBACK); atomicAdd(diag + 2, 1u); }
+                    if (fb) atomicAdd(diag, 1u);
                 }
             }
         }
@@ -1025,7 +1122,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
         if (tid == 0) {
             if (c == 0) {
                 M->T = Tthr; M->maxval = maxval; M->L = (int)L; M->nc = nc; M->ntiles = ntiles; M->h = H; M->w = W;
-                if (L == 0) { M->end = -1; M->tile_end = -1; M->status = 0; }
+                if (L == 0) { M->end = -1; M->tile_end = -1; }   // status stays 0 (memset)
             }
             // the chunk holding `end` (or the last one on overflow) reports the capacity seen so
             // far: exact when it is the last chunk, else a lower bound (later chunks are not counted)
@@ -1034,7 +1131,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                 M->capacity = (int)(excl + agg);
                 M->flags = last ? 0 : CODEC_PEE_PARTIAL;
             }
-            if (last && excl + agg < L) { M->end = nc - 1; M->tile_end = ntiles - 1; M->status = 1; }
+            if (last && excl + agg < L) { M->end = nc - 1; M->tile_end = ntiles - 1; atomicMax(&M->status, 1); }
         }
         __syncthreads();   // lm32 zeroing vs the ORs below
         if (excl < L) {   // some candidate of this chunk is active
@@ -1078,7 +1175,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                         const uint32_t o = r - r64;        // < 64 + 4
                         const int pb = (int)(((o < 64u ? plo[u] >> o : phi[u] >> (o - 64u))) & 1ull);
                         nv = p + 2 * (x - p) + pb;
-                        if (r == L - 1) { M->end = k; M->tile_end = k / PEE_TILE; M->status = 0; }
+                        if (r == L - 1) { M->end = k; M->tile_end = k / PEE_TILE; }   // status stays 0 (memset)
                         ++r;
                     } else {
                         nv = (rightm & bit) ? x + Tthr : x - Tthr;
@@ -1126,7 +1223,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
                                                       const codec_pee_meta* __restrict__ meta_all,
                                                       const u64* __restrict__ lm_all, int lmw, int nchunks, int B,
                                                       u64* status_all, uint32_t* ctl, u64* __restrict__ payload_all,
-                                                      int pw, int mode) {
+                                                      int pw, int mode, uint32_t spin_max, int dbg_skip, uint32_t* diag) {
     typedef typename Vec8<T>::type V;
     __shared__ u64 sh64[8];
     __shared__ uint32_t s_v, s_excl;
@@ -1215,17 +1312,21 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
             const u64 pex = block_excl_scan64<256>(packed, sh64, &ptot);
             const uint32_t agg = (uint32_t)((ptot & 0xFFFFu) + ((ptot >> 16) & 0xFFFFu) + ((ptot >> 32) & 0xFFFFu) + (ptot >> 48));
             u64* st = status_all + (size_t)b * nchunks;
+            const bool publish = c < cend && !(b == 0 && c == dbg_skip);
             if (c == 0) {
-                if (tid == 0) { if (cend > 0) lb_store(st, LB_INC | (u64)agg); s_excl = 0; }
+                if (tid == 0) { if (publish) lb_store(st, LB_INC | (u64)agg); s_excl = 0; }
             } else {
-                if (tid == 0 && c < cend) lb_store(st + c, LB_AGG | (u64)agg);
+                if (tid == 0 && publish) lb_store(st + c, LB_AGG | (u64)agg);
                 if (tid < 64) {
-                    bool to = false;
-                    const uint32_t ex = lb_exclusive(st, c, &to);
+                    bool to = false, fb = false;
+                    uint32_t ex;
+                    if (INPLACE) ex = lb_exclusive(st, c, &to, &fb, spin_max, NoFallback());
+                    else ex = lb_exclusive(st, c, &to, &fb, spin_max, ExtractCount<T>{src, lm, W, CR, items, end, Tthr});
                     if (tid == 0) {
-                        if (c < cend) lb_store(st + c, LB_INC | (u64)(ex + agg));
+                        if (publish) lb_store(st + c, LB_INC | (u64)(ex + agg));
                         s_excl = ex;
-                        if (to) atomicOr(ctl + 1, 1u);   // host: codec_pee_extract_flag_offset
+                        if (to) { atomicOr(ctl + 1, 1u); atomicAdd(diag + 3, 1u); }   // codec_pee_extract_flag_offset
+                        if (fb) atomicAdd(diag + 1, 1u);
                     }
                 }
             }
@@ -1298,7 +1399,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
 
 // ====================================================================== host side
 struct PeeWs {
-    size_t cnt, off, st, ctl, total;
+    size_t cnt, off, st, ctl, diag, total;
     int ntiles_max, nchunks;
 };
 
@@ -1314,7 +1415,9 @@ static PeeWs pee_ws(const codec_pee_params* P) {
     L.off = align_up((size_t)P->B * L.ntiles_max * 4, 256);
     L.st = align_up(L.off + (size_t)P->B * L.ntiles_max * 4, 256);
     L.ctl = L.st + (size_t)P->B * L.nchunks * 8;   // status words and ctl are cleared together
-    L.total = align_up(L.ctl + PEE_CTL_WORDS(P->B) * 4, 256);
+    // diag: 4 cumulative uint32 counters (codec_pee_diag_offset), outside the per-call memset
+    L.diag = align_up(L.ctl + PEE_CTL_WORDS(P->B) * 4, 16);
+    L.total = align_up(L.diag + 16, 256);
     return L;
 }
 
@@ -1349,6 +1452,11 @@ size_t codec_pee_workspace_bytes(const codec_pee_params* P) {
 size_t codec_pee_extract_flag_offset(const codec_pee_params* P) {
     if (pee_check(P)) return 0;
     return pee_ws(P).ctl + 4;   // ctl[1]: set when an extract chunk's look-back gave up
+}
+
+size_t codec_pee_diag_offset(const codec_pee_params* P) {
+    if (pee_check(P)) return 0;
+    return pee_ws(P).diag;
 }
 
 int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, const uint64_t* payload,
@@ -1410,10 +1518,13 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
         long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));
         if (g > total) g = total;
         g = (g + 7) / 8 * 8;   // keep every workgroup on one slot lane (pee_slot)
+        const uint32_t spin_max = (uint32_t)knob("CODEC_PEE_LB_SPINS", inplace ? (1 << 22) : (1 << 14));
+        const int dbg_skip = (int)knob("CODEC_PEE_DEBUG_SKIP", 0) - 1;
+        uint32_t* diag = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.diag);
 #define PE1(TT, NTV, IP) hipLaunchKernelGGL((k_pee_embed1<TT, NTV, IP>), dim3((unsigned)g), dim3(256), 0, st, \
             static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, \
             reinterpret_cast<const u64*>(payload), P->payload_words, L.nchunks, P->B, stw, ctl, meta, \
-            reinterpret_cast<u64*>(lm), P->lm_words, mode)
+            reinterpret_cast<u64*>(lm), P->lm_words, mode, spin_max, dbg_skip, diag)
         if (P->bytes == 2) {
             if (inplace) { if (nt) PE1(uint16_t, true, true); else PE1(uint16_t, false, true); }
             else { if (nt) PE1(uint16_t, true, false); else PE1(uint16_t, false, false); }
@@ -1527,9 +1638,13 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
         long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));
         if (g > total) g = total;
         g = (g + 7) / 8 * 8;
+        const uint32_t spin_max = (uint32_t)knob("CODEC_PEE_LB_SPINS", inplace ? (1 << 22) : (1 << 14));
+        const int dbg_skip = (int)knob("CODEC_PEE_DEBUG_SKIP", 0) - 1;
+        uint32_t* diag = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.diag);
 #define PX1(TT, NTV, IP) hipLaunchKernelGGL((k_pee_extract1<TT, NTV, IP>), dim3((unsigned)g), dim3(256), 0, st, \
             static_cast<const TT*>(stego), static_cast<TT*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm), \
-            P->lm_words, L.nchunks, P->B, stw, ctl, reinterpret_cast<u64*>(payload_out), P->payload_words, mode)
+            P->lm_words, L.nchunks, P->B, stw, ctl, reinterpret_cast<u64*>(payload_out), P->payload_words, mode, spin_max, \
+            dbg_skip, diag)
         if (P->bytes == 2) {
             if (inplace) { if (nt) PX1(uint16_t, true, true); else PX1(uint16_t, false, true); }
             else { if (nt) PX1(uint16_t, true, false); else PX1(uint16_t, false, false); }

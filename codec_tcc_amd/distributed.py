@@ -1,18 +1,27 @@
 """Multi-GPU sharding of a slice batch.
 
 Slices are independent (s, offset, plan and maps are per slice: codec.py:561-599,
-412-487), so rank r simply encodes/decodes its own contiguous share with no data-path
-collective ("weak" scaling).  The one exchange the north star asks for -- every rank
-holding every slice's location map -- is ONE `all_gather_into_tensor` of fixed-size
-records (codec_slice_meta + packed maps), latency-bound at ~1.6 KB per slice; never the
-dense s*H*W bitmaps (335 MB for 2048 x 512^2).
+412-487; the MED-PEE side information T, L, end and the location map are per slice too),
+so rank r simply encodes/decodes its own contiguous share with no data-path collective
+("weak" scaling).  The one exchange the north star asks for -- every rank holding every
+slice's location map -- is an `all_gather_into_tensor` of fixed-size records:
 
-Backend "nccl" is RCCL on ROCm (xGMI between the 8 MI355X); "gloo" is used by the CPU
-tests.  Everything here is shape/bookkeeping code: the kernels stay in codec.py.
+* LSB path (`RecordExchange`): codec_slice_meta + packed maps, ~1.6 KB per slice, one
+  collective; never the dense s*H*W bitmaps (335 MB for 2048 x 512^2).
+* MED-PEE path (`PeeRecordExchange`): two collectives -- the 64-byte codec_pee_meta of
+  every slice, then every slice's location-map prefix [0, end] padded to the longest one
+  in the whole job (read from the gathered metas, so every rank agrees on the width
+  without another collective).
+
+Uneven shards (e.g. 2049 slices over 8 ranks) are padded to ceil(N / world) rows per
+rank, the collective stays one equal-sized all-gather, and the padding rows are dropped
+on the way out.  Backend "nccl" is RCCL on ROCm (xGMI between the 8 MI355X); "gloo" is
+used by the CPU tests.  Everything here is shape/bookkeeping code: the kernels stay in
+codec.py / pee.py.
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import List, Optional, Tuple
 
 from . import _lib
 
@@ -24,22 +33,39 @@ def shard_range(n_items: int, world: int, rank: int) -> Tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+def shard_rows(n_items: int, world: int) -> int:
+    """Rows every rank contributes to a gather: the largest shard (ceil(n / world))."""
+    return max(1, -(-int(n_items) // int(world)))
+
+
+def valid_rows(n_items: int, world: int) -> List[int]:
+    """Indices of the real (non-padding) rows of a padded gather, in global slice order."""
+    rows = shard_rows(n_items, world)
+    out = []
+    for r in range(world):
+        lo, hi = shard_range(n_items, world, r)
+        out.extend(r * rows + i for i in range(hi - lo))
+    return out
+
+
 def record_words(map_words: int) -> int:
     """int64 words per slice record: meta (rounded up to 8 B) + packed location map."""
     return (_lib.META_BYTES + 7) // 8 + int(map_words)
 
 
 def pack_records(meta, maps, out=None):
-    """[B, META_BYTES] uint8 + [B, map_words] int64 -> [B, record_words] int64."""
+    """[B, META_BYTES] uint8 + [B, map_words] int64 -> [B, record_words] int64.
+    `out` may be wider than the maps (a job-wide map width): the extra words are zero."""
     import torch
     B = meta.shape[0]
     mw = maps.shape[1]
-    words = record_words(mw)
-    if out is None:
-        out = torch.zeros((B, words), dtype=torch.int64, device=meta.device)
     hdr = (_lib.META_BYTES + 7) // 8
-    out[:, :hdr].view(torch.uint8)[:, : _lib.META_BYTES].copy_(meta)
-    out[:, hdr:].copy_(maps)
+    if out is None:
+        out = torch.zeros((B, record_words(mw)), dtype=torch.int64, device=meta.device)
+    out[:B, :hdr].view(torch.uint8)[:, : _lib.META_BYTES].copy_(meta)
+    out[:B, hdr: hdr + mw].copy_(maps)
+    if out.shape[1] > hdr + mw:
+        out[:B, hdr + mw:].zero_()
     return out
 
 
@@ -52,26 +78,89 @@ def unpack_records(records, map_words: int):
     return meta.contiguous(), maps.contiguous()
 
 
-def gather_records(local_records, group=None, out=None):
-    """all_gather_into_tensor of every rank's [B, W] records -> [world*B, W] (rank-major)."""
+def _is_gloo(group) -> bool:
+    import torch.distributed as dist
+    return dist.get_backend(group) == "gloo"
+
+
+def agree_max(value: int, group=None, device=None) -> int:
+    """The maximum of an integer over all ranks (one tiny all_reduce; host value out)."""
+    import torch
+    import torch.distributed as dist
+    dev = "cpu" if (device is None or _is_gloo(group)) else device
+    t = torch.tensor([int(value)], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
+
+
+def gather_records(local_records, group=None, out=None, rows: Optional[int] = None):
+    """all_gather_into_tensor of every rank's records -> [world * rows, W] (rank-major).
+
+    `rows` (default: this rank's row count) is the per-rank row count of the collective;
+    a shorter local shard is zero-padded to it, so uneven shards still make one
+    equal-sized collective (drop the padding with `valid_rows`)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
+    n, width = local_records.shape
+    rows = n if rows is None else int(rows)
+    if n > rows:
+        raise ValueError(f"local shard of {n} rows exceeds the per-rank row count {rows}")
+    src = local_records
+    if n < rows or not src.is_contiguous():
+        src = torch.zeros((rows, width), dtype=local_records.dtype, device=local_records.device)
+        src[:n].copy_(local_records)
     if out is None:
-        out = torch.empty((world * local_records.shape[0], local_records.shape[1]), dtype=local_records.dtype,
-                          device=local_records.device)
-    if dist.get_backend(group) == "gloo":
+        out = torch.empty((world * rows, width), dtype=local_records.dtype, device=local_records.device)
+    if _is_gloo(group):
         parts = list(out.chunk(world, dim=0))
-        dist.all_gather(parts, local_records.contiguous(), group=group)
+        dist.all_gather(parts, src, group=group)
         if parts[0].data_ptr() != out.data_ptr():   # chunk() views: already in place
             torch.cat(parts, 0, out=out)
     else:
-        dist.all_gather_into_tensor(out, local_records.contiguous(), group=group)
+        dist.all_gather_into_tensor(out, src, group=group)
     return out
 
 
+class _SideStream:
+    """Runs an exchange on a side stream that waits only for the point after encode, so
+    decode's kernels keep the launch stream busy meanwhile (no-op on CPU tensors)."""
+
+    def __init__(self, device):
+        import torch
+        dev = torch.device(device)
+        self.device = dev
+        self.stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+        self.event = torch.cuda.Event() if self.stream is not None else None
+        self._marked = False
+
+    def mark(self):
+        import torch
+        if self.stream is not None:
+            self.event.record(torch.cuda.current_stream(self.device))
+            self._marked = True
+
+    def enter(self):
+        import contextlib
+
+        import torch
+        if self.stream is None:
+            return contextlib.nullcontext()
+        if self._marked:
+            self.stream.wait_event(self.event)
+            self._marked = False
+        else:
+            self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        return torch.cuda.stream(self.stream)
+
+    def join(self):
+        import torch
+        if self.stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+
+
 class RecordExchange:
-    """The record all-gather of one batch, overlapped with that batch's decode.
+    """The LSB record all-gather of one batch, overlapped with that batch's decode.
 
     The records depend only on what encode wrote (meta + packed maps), so they are packed
     and gathered on a side stream while decode's kernels run on the launch stream:
@@ -80,43 +169,131 @@ class RecordExchange:
     backend such as gloo does not hold back decode's launches either), and ``join()`` (the
     current stream waits for the gather, so the next encode cannot overwrite meta/maps under
     the pack).  On RCCL the collective runs on its own stream ordered after the side stream.
-    CPU tensors (gloo tests) run synchronously."""
+    CPU tensors (gloo tests) run synchronously.
 
-    def __init__(self, batch: int, map_words: int, world: int, device, group=None):
+    ``n_total`` (default batch * world) is the job's slice count; with uneven shards every
+    rank pads to ceil(n_total / world) rows.  The map width is agreed as the job-wide
+    maximum at construction (one all_reduce), since payload lengths -- and so the map
+    words -- may differ per rank."""
+
+    def __init__(self, batch: int, map_words: int, world: int, device, group=None, n_total: Optional[int] = None):
         import torch
         self.group = group
-        words = record_words(map_words)
-        self.record = torch.zeros((batch, words), dtype=torch.int64, device=device)
-        self.gathered = torch.empty((world * batch, words), dtype=torch.int64, device=device)
-        dev = torch.device(device)
-        self.stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
-        self.event = torch.cuda.Event() if self.stream is not None else None
-        self._marked = False
+        self.world = int(world)
+        self.n_total = int(n_total) if n_total is not None else int(batch) * self.world
+        self.rows = shard_rows(self.n_total, self.world)
+        if batch > self.rows:
+            raise ValueError("batch exceeds the per-rank row count of n_total")
+        self.batch = int(batch)
+        self.map_words = agree_max(map_words, group, device) if self.world > 1 else int(map_words)
+        words = record_words(self.map_words)
+        self.record = torch.zeros((self.rows, words), dtype=torch.int64, device=device)
+        self.padded = torch.empty((self.world * self.rows, words), dtype=torch.int64, device=device)
+        self.even = self.rows * self.world == self.n_total
+        self.index = None if self.even else torch.tensor(valid_rows(self.n_total, self.world), device=device)
+        self._side = _SideStream(device)
+
+    @property
+    def gathered(self):
+        """[n_total, words] records in global slice order (a view when shards are even)."""
+        return self.padded if self.even else self.padded.index_select(0, self.index)
+
+    def own_rows(self, rank: int):
+        """This rank's rows of the gathered (padded) buffer."""
+        return self.padded[rank * self.rows: rank * self.rows + self.batch]
 
     def mark(self):
         """Record the point after encode on the current stream (no-op on CPU)."""
-        import torch
-        if self.stream is not None:
-            self.event.record(torch.cuda.current_stream(self.gathered.device))
-            self._marked = True
+        self._side.mark()
 
     def start(self, meta, maps):
-        import torch
-        if self.stream is None:
+        with self._side.enter():
             pack_records(meta, maps, out=self.record)
-            gather_records(self.record, self.group, out=self.gathered)
-            return
-        if self._marked:
-            self.stream.wait_event(self.event)
-            self._marked = False
-        else:
-            self.stream.wait_stream(torch.cuda.current_stream(meta.device))
-        with torch.cuda.stream(self.stream):
-            pack_records(meta, maps, out=self.record)
-            gather_records(self.record, self.group, out=self.gathered)
+            gather_records(self.record, self.group, out=self.padded, rows=self.rows)
 
     def join(self):
-        import torch
-        if self.stream is not None:
-            torch.cuda.current_stream(self.gathered.device).wait_stream(self.stream)
+        self._side.join()
         return self.gathered
+
+
+PEE_META_WORDS = (_lib.PEE_META_BYTES + 7) // 8
+PEE_END_FIELD = 3          # int32 index of codec_pee_meta.end
+
+
+class PeeRecordExchange:
+    """The MED-PEE side information of every slice to every rank (north star: "an RCCL
+    all-gather of per-slice location maps").
+
+    Phase 1 gathers the fixed 64-byte codec_pee_meta records (T, L, end, maxval, status,
+    capacity ...).  Their `end` fields bound every location map (candidates 0..end), so
+    phase 2 gathers each slice's first ceil((end_max + 1) / 64) map words, end_max taken
+    over the whole job from the gathered metas -- the same number on every rank, hence one
+    equal-sized collective, with no extra agreement round.  The host reads that one
+    integer (a sync of the side stream only: decode's kernels were queued before
+    ``start`` and keep running).  Uneven shards are padded as in RecordExchange."""
+
+    def __init__(self, batch: int, world: int, device, group=None, n_total: Optional[int] = None):
+        import torch
+        self.group = group
+        self.world = int(world)
+        self.n_total = int(n_total) if n_total is not None else int(batch) * self.world
+        self.rows = shard_rows(self.n_total, self.world)
+        if batch > self.rows:
+            raise ValueError("batch exceeds the per-rank row count of n_total")
+        self.batch = int(batch)
+        self.device = torch.device(device)
+        self.meta_rec = torch.zeros((self.rows, PEE_META_WORDS), dtype=torch.int64, device=device)
+        self.meta_padded = torch.empty((self.world * self.rows, PEE_META_WORDS), dtype=torch.int64, device=device)
+        self.even = self.rows * self.world == self.n_total
+        self.index = None if self.even else torch.tensor(valid_rows(self.n_total, self.world), device=device)
+        self._lm_flat = None
+        self._lm_out_flat = None
+        self.lm_words = 0
+        self._side = _SideStream(device)
+
+    def _buffers(self, lmw: int):
+        import torch
+        need = self.rows * lmw
+        if self._lm_flat is None or self._lm_flat.numel() < need:
+            self._lm_flat = torch.zeros(need, dtype=torch.int64, device=self.device)
+            self._lm_out_flat = torch.empty(self.world * need, dtype=torch.int64, device=self.device)
+        rec = self._lm_flat[:need].view(self.rows, lmw)
+        out = self._lm_out_flat[: self.world * need].view(self.world * self.rows, lmw)
+        return rec, out
+
+    def mark(self):
+        self._side.mark()
+
+    def start(self, meta, lm):
+        """meta: uint8 [B, PEE_META_BYTES]; lm: int64 [B, lm_words] (PeeCodec outputs)."""
+        import torch
+        B = meta.shape[0]
+        with self._side.enter():
+            self.meta_rec[:B].view(torch.uint8)[:, : _lib.PEE_META_BYTES].copy_(meta)
+            if B < self.rows:
+                self.meta_rec[B:].zero_()
+            gather_records(self.meta_rec, self.group, out=self.meta_padded, rows=self.rows)
+            end_max = int(self.meta_padded.view(torch.int32)[:, PEE_END_FIELD].max().item())
+            lmw = min(max(1, (end_max + 1 + 63) // 64), int(lm.shape[1]))
+            rec, out = self._buffers(lmw)
+            rec[:B].copy_(lm[:, :lmw])
+            if B < self.rows:
+                rec[B:].zero_()
+            gather_records(rec, self.group, out=out, rows=self.rows)
+            self.lm_words = lmw
+            self._lm_padded = out
+
+    def own_rows(self, rank: int):
+        """(meta, lm) rows of this rank in the gathered (padded) buffers."""
+        a = rank * self.rows
+        return self.meta_padded[a: a + self.batch], self._lm_padded[a: a + self.batch]
+
+    def join(self):
+        """(meta uint8 [n_total, PEE_META_BYTES], lm int64 [n_total, lm_words]) in global
+        slice order; a slice's full map is its row zero-extended to the codec's lm_words."""
+        import torch
+        self._side.join()
+        meta, lm = self.meta_padded, self._lm_padded
+        if not self.even:
+            meta, lm = meta.index_select(0, self.index), lm.index_select(0, self.index)
+        return meta.view(torch.uint8)[:, : _lib.PEE_META_BYTES], lm

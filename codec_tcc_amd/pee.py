@@ -51,7 +51,8 @@ class PeeCodec:
         ws = _lib.load().codec_pee_workspace_bytes(C.byref(P))
         if ws == 0:
             _lib.check(-1, "codec_pee_workspace_bytes")
-        self.workspace = torch.empty(int(ws), dtype=torch.uint8, device=self.device)
+        # zeroed once: the cumulative look-back diagnostics live in it (codec_pee_diag_offset)
+        self.workspace = torch.zeros(int(ws), dtype=torch.uint8, device=self.device)
 
     def _params(self, payload_words: int) -> _lib.PeeParams:
         return _lib.PeeParams(B=self.B, H=self.H, W=self.W, bytes=self.bytes, T=self.T, maxval=self.maxval,
@@ -66,7 +67,11 @@ class PeeCodec:
         return (torch.from_numpy(packed).to(self.device), lengths,
                 torch.tensor(lengths, dtype=torch.int32, device=self.device))
 
-    def embed(self, covers, payloads, *, stego=None, lm=None, meta=None, packed=None) -> PeeEncoded:
+    def embed(self, covers, payloads, *, stego=None, lm=None, meta=None, packed=None, check: bool = True) -> PeeEncoded:
+        """cover -> stego + location map + per-slice meta.  check=True (default) reads the
+        per-slice status back (one sync) and raises RuntimeError if an in-place look-back
+        gave up (CODEC_PEE_ELOOKBACK: the slice is not a valid stego); check=False keeps
+        the call asynchronous (benchmarks) -- inspect enc.records() afterwards."""
         torch = _torch()
         if tuple(covers.shape) != (self.B, self.H, self.W) or _elem_bytes(covers) != self.bytes:
             raise ValueError("covers do not match the codec's shape/dtype")
@@ -82,7 +87,10 @@ class PeeCodec:
                                                lens_t.data_ptr(), meta.data_ptr(), lm.data_ptr(),
                                                self.workspace.data_ptr(), self.workspace.numel(), _stream()),
                    "codec_pee_embed")
-        return PeeEncoded(stego=stego, lm=lm, meta=meta, lengths=list(lengths), payload_words=int(words.shape[1]))
+        enc = PeeEncoded(stego=stego, lm=lm, meta=meta, lengths=list(lengths), payload_words=int(words.shape[1]))
+        if check:
+            _raise_lookback(enc.records())
+        return enc
 
     def extract(self, stego, meta, lm, *, payload_words: int, cover=None, payload=None):
         torch = _torch()
@@ -96,23 +104,43 @@ class PeeCodec:
                                                  self.workspace.numel(), _stream()), "codec_pee_extract")
         return payload, cover
 
+    def lookback_failed(self, payload_words: int = 1) -> bool:
+        """True when the last in-place extract's look-back gave up (its payload is invalid)."""
+        off = int(_lib.load().codec_pee_extract_flag_offset(C.byref(self._params(payload_words))))
+        return bool(off) and int(self.workspace[off:off + 4].view(_torch().int32).item()) != 0
+
+    def diagnostics(self, payload_words: int = 1) -> dict:
+        """Cumulative look-back counters since construction (codec_pee_diag_offset)."""
+        off = int(_lib.load().codec_pee_diag_offset(C.byref(self._params(payload_words))))
+        v = self.workspace[off:off + 16].view(_torch().int32).cpu().tolist()
+        return {"embed_fallback_chunks": v[0], "extract_fallback_chunks": v[1],
+                "embed_unrecovered_chunks": v[2], "extract_unrecovered_chunks": v[3]}
+
+    def repaired(self, payload_words: int = 1) -> int:
+        """Chunks whose look-back fell back to counting predecessors from pixels (exact)."""
+        d = self.diagnostics(payload_words)
+        return d["embed_fallback_chunks"] + d["extract_fallback_chunks"]
+
     def decode(self, enc: PeeEncoded):
         """(list of 0/1 bit vectors, restored cover tensor); raises if a slice overflowed."""
         recs = enc.records()
-        lost = [i for i, r in enumerate(recs) if r.status == _lib.CODEC_PEE_ELOOKBACK]
-        if lost:
-            raise RuntimeError(f"codec_pee_embed: cursor look-back timed out in slices {lost} "
-                               "(out-of-order workgroup dispatch); re-run with CODEC_PEE_ONEPASS=0")
+        _raise_lookback(recs)
         bad = [i for i, r in enumerate(recs) if r.status != 0]
         if bad:
             raise ValueError(f"payload exceeds PEE capacity in slices {bad} (T={self.T})")
         words, cover = self.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words)
         host = words.cpu().numpy()
-        off = int(_lib.load().codec_pee_extract_flag_offset(C.byref(self._params(enc.payload_words))))
-        if off and int(self.workspace[off:off + 4].view(_torch().int32).item()) != 0:
-            raise RuntimeError("codec_pee_extract: cursor look-back timed out (out-of-order workgroup "
-                               "dispatch); re-run with CODEC_PEE_ONEPASS=0")
+        if self.lookback_failed(enc.payload_words):
+            raise RuntimeError("codec_pee_extract: in-place cursor look-back timed out; the recovered "
+                               "payload is invalid (the restored cover is exact)")
         return [framing.unpack_bits(host[i], enc.lengths[i]) for i in range(self.B)], cover
+
+
+def _raise_lookback(recs):
+    lost = [i for i, r in enumerate(recs) if r.status == _lib.CODEC_PEE_ELOOKBACK]
+    if lost:
+        raise RuntimeError(f"codec_pee_embed: in-place cursor look-back timed out in slices {lost}; "
+                           "their pixels are not a valid stego")
 
 
 def lm_bits(enc: PeeEncoded, b: int) -> np.ndarray:

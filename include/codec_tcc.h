@@ -218,15 +218,26 @@ typedef struct codec_pee_meta {
  * e.g. on overflow or on the two-pass path). */
 #define CODEC_PEE_PARTIAL 1
 /* meta.status values: 0 ok, 1 payload exceeds capacity (truncated, still reversible),
- * CODEC_PEE_ELOOKBACK: the single-pass cursor look-back gave up waiting for a predecessor
- * chunk (bounded spin instead of a GPU hang; requires out-of-order workgroup dispatch). */
+ * CODEC_PEE_ELOOKBACK: an IN-PLACE single-pass embed's cursor look-back gave up waiting for
+ * a predecessor chunk (bounded spin instead of a GPU hang; the slice's pixels are not a
+ * valid stego -- the Python layer raises).  Sticky: nothing lowers it within the call.
+ * Out of place a look-back that waits too long computes the missing predecessor counts
+ * from the (read-only) cover itself, so the result stays exact and this never appears. */
 #define CODEC_PEE_ELOOKBACK 2
 
+/* Zero-initialise the workspace once before its first use (the diagnostic counters live
+ * in it; everything else is cleared by the calls themselves). */
 size_t codec_pee_workspace_bytes(const codec_pee_params* P);
-/* Byte offset in the workspace of a uint32 flag that codec_pee_extract's single pass sets
- * (non-zero) when a chunk's cursor look-back gave up (CODEC_PEE_ELOOKBACK on the decode
- * side); cleared at the start of every codec_pee_extract.  0 on bad parameters. */
+/* Byte offset in the workspace of a uint32 flag that codec_pee_extract's IN-PLACE single
+ * pass sets (non-zero) when a chunk's cursor look-back gave up (the recovered payload of
+ * that call is not valid); cleared at the start of every codec_pee_extract.  0 on bad
+ * parameters. */
 size_t codec_pee_extract_flag_offset(const codec_pee_params* P);
+/* Byte offset in the workspace of 4 cumulative uint32 counters (since the workspace was
+ * zeroed): [0] embed / [1] extract chunks whose look-back timed out and recovered by
+ * counting the missing predecessors from pixels (exact results), [2] embed / [3] extract
+ * in-place chunks whose look-back timed out unrecovered.  0 on bad parameters. */
+size_t codec_pee_diag_offset(const codec_pee_params* P);
 /* cover -> stego (full copy + expansion/shifting of candidates 0..end), lm, meta.
  * lengths[B] (device int32) = payload bits per slice.
  * stego == cover is allowed (in place): only the items up to `end` are read and

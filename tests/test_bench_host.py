@@ -10,14 +10,37 @@ sys.path.insert(0, REPO)
 import bench  # noqa: E402
 
 
+def _args(**kw):
+    import argparse
+    a = dict(size=64, kind="ct12", payload_chars=8, pee_T=2, cpu_seconds=0.05, cpu_ref_seconds=0.05, cpu_pool=2)
+    a.update(kw)
+    return argparse.Namespace(**a)
+
+
 def test_cpu_baseline_small():
-    r = bench.cpu_baseline(64, "ct12", 8, 0.05)
+    r = bench.cpu_baseline(_args())
     assert r["kind"] == "port" and r["cores"] == 1 and r["value"] > 0 and r["unit"] == "Mpixels/s"
+    assert "pee_cpu" in r["sample"] and r["reference_path"]["value"] > 0
+    assert "reference_path" not in bench.cpu_baseline(_args(cpu_ref_seconds=0))
 
 
 def test_cpu_baseline_pool_small():
-    r = bench.cpu_baseline_pool(64, "ct12", 8, 2, 1)
-    assert r["cores"] == 2 and r["value"] > 0 and "pool" in r["sample"]
+    for which in ("pee", "lsb"):
+        r = bench.cpu_baseline_pool(_args(), which, per_worker=1)
+        assert r["cores"] == 2 and r["value"] > 0 and "pool" in r["sample"] and which in r["sample"]
+
+
+def test_payload_equal_masks_lengths():
+    import numpy as np
+    import torch
+    want = torch.from_numpy(np.array([[0b1011, 0], [-1, -1]], dtype=np.int64))
+    got = want.clone()
+    assert bench.payload_equal(got, want, [4, 128])
+    got[0, 0] = 0b0011                       # a recovered bit differs
+    assert not bench.payload_equal(got, want, [4, 128])
+    got[0, 0] = 0b1011 | (1 << 9)            # a bit set past the slice's length
+    assert not bench.payload_equal(got, want, [4, 128])
+    assert bench.payload_equal(want, torch.from_numpy(np.array([[0b1011 | (1 << 9), 0], [-1, -1]])), [4, 128])
 
 
 def test_pmc_traffic_lookup(tmp_path, monkeypatch):

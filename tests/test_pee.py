@@ -279,3 +279,70 @@ def test_gpu_extract_lookback_flag_clear(onepass, monkeypatch):
     for i in range(3):
         np.testing.assert_array_equal(np.asarray(bits[i]), payloads[i])
     np.testing.assert_array_equal(cover.cpu().numpy(), covers)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("slots", ["flat", "lanes"])
+def test_gpu_lookback_fallback_out_of_place(slots, monkeypatch):
+    """A chunk that never publishes its look-back word (CODEC_PEE_DEBUG_SKIP, slice 0,
+    chunk 1): out of place its successors time out, count it from the read-only pixels
+    themselves, and every output still equals the oracle bit for bit."""
+    torch = pytest.importorskip("torch")
+    from codec_tcc_amd import framing
+    from codec_tcc_amd.pee import PeeCodec, lm_bits
+    monkeypatch.setenv("CODEC_PEE_ONEPASS", "1")
+    monkeypatch.setenv("CODEC_PEE_DEBUG_SKIP", "2")
+    monkeypatch.setenv("CODEC_PEE_LB_SPINS", "256")
+    if slots == "lanes":
+        monkeypatch.setenv("CODEC_PEE_FLAT_MAXB", "0")
+    bsz, h, w, T = 3, 256, 256, 2          # 4 chunks per slice; `end` in the last one
+    covers = np.stack([synth.ct12(h, w, 500 + i) for i in range(bsz)])
+    payloads = [_bits(P.capacity(c, T) - 3, 60 + i) for i, c in enumerate(covers)]
+    codec = PeeCodec(bsz, h, w, T=T)
+    enc = codec.embed(torch.from_numpy(covers).cuda(), payloads)
+    recs = enc.records()
+    stego = enc.stego.cpu().numpy()
+    for i in range(bsz):
+        st, side = P.pee_embed(covers[i], payloads[i], T)
+        assert recs[i].status == 0 and recs[i].end == side["end"] and side["end"] >= 3 * 1024 * 4
+        np.testing.assert_array_equal(stego[i], st)
+        np.testing.assert_array_equal(lm_bits(enc, i), side["lm"])
+    assert codec.diagnostics()["embed_fallback_chunks"] >= 1
+    bits, cover = codec.decode(enc)
+    for i in range(bsz):
+        np.testing.assert_array_equal(np.asarray(bits[i]), payloads[i])
+    np.testing.assert_array_equal(cover.cpu().numpy(), covers)
+    d = codec.diagnostics()
+    assert d["extract_fallback_chunks"] >= 1 and d["embed_unrecovered_chunks"] == 0 == d["extract_unrecovered_chunks"]
+
+
+@pytest.mark.gpu
+def test_gpu_lookback_timeout_in_place_raises(monkeypatch):
+    """In place a predecessor may be rewriting its pixels, so there is no fallback: the
+    slice gets the sticky status CODEC_PEE_ELOOKBACK and embed raises; an in-place extract
+    whose look-back times out sets the decode-side flag (the restored cover is still exact)."""
+    torch = pytest.importorskip("torch")
+    from codec_tcc_amd import _lib
+    from codec_tcc_amd.pee import PeeCodec
+    monkeypatch.setenv("CODEC_PEE_ONEPASS", "1")
+    monkeypatch.setenv("CODEC_PEE_LB_SPINS", "256")
+    bsz, h, w, T = 2, 256, 256, 2
+    covers = np.stack([synth.ct12(h, w, 520 + i) for i in range(bsz)])
+    payloads = [_bits(P.capacity(c, T) - 3, 80 + i) for i, c in enumerate(covers)]
+    codec = PeeCodec(bsz, h, w, T=T)
+    work = torch.from_numpy(covers).cuda()
+    monkeypatch.setenv("CODEC_PEE_DEBUG_SKIP", "2")
+    with pytest.raises(RuntimeError, match="look-back"):
+        codec.embed(work, payloads, stego=work)
+    work = torch.from_numpy(covers).cuda()
+    enc = codec.embed(work, payloads, stego=work, check=False)
+    assert enc.records()[0].status == _lib.CODEC_PEE_ELOOKBACK and enc.records()[1].status == 0
+    monkeypatch.delenv("CODEC_PEE_DEBUG_SKIP")
+    work = torch.from_numpy(covers).cuda()
+    enc = codec.embed(work, payloads, stego=work)                      # a valid in-place stego
+    assert not codec.lookback_failed(enc.payload_words)
+    monkeypatch.setenv("CODEC_PEE_DEBUG_SKIP", "2")
+    codec.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words, cover=enc.stego)
+    assert codec.lookback_failed(enc.payload_words)
+    assert codec.diagnostics()["extract_unrecovered_chunks"] >= 1
+    np.testing.assert_array_equal(enc.stego.cpu().numpy(), covers)
