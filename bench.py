@@ -255,7 +255,7 @@ def _roof(kernel, by, t_ms, traffic=None):
 
 # ------------------------------------------------------------------ MED-PEE (headline)
 def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=False, exchange=False,
-              steps=None, kind=None):
+              steps=None, kind=None, T=None):
     """MED-PEE embed + extract over one resident batch (1 KB payload per slice).
     Out of place (default): k_pee_embed1 (one pass: copy + look-back cursor + embed) and
     k_pee_extract1 (one pass: copy + look-back cursor + recover).  In place: the same
@@ -267,7 +267,8 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
     from codec_tcc_amd.pee import PeeCodec, PeeEncoded
     steps = args.steps if steps is None else steps
     kind = args.kind if kind is None else kind
-    codec = PeeCodec(B, H, W, dtype="uint16", T=args.pee_T, device=dev)
+    T = args.pee_T if T is None else T
+    codec = PeeCodec(B, H, W, dtype="uint16", T=T, device=dev)
     pay = [synth.payload(args.payload_chars, 99 + rank * B + i) for i in range(B)]
     packed = codec.pack_payloads(pay)
     work = covers.clone() if inplace else None
@@ -304,7 +305,7 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
     pay_ok = payload_equal(outw, packed[0], nbits)
     flags_ok = all(r.status in (0, 1) for r in recs) and not codec.lookback_failed(pw)
     res = {"value": round(B * H * W * world * steps / el / 1e6, 1), "unit": "Mpixels/s",
-           "ms_per_step": round(el / steps * 1e3, 4), "T": args.pee_T,
+           "ms_per_step": round(el / steps * 1e3, 4), "T": T,
            "roundtrip_ok": cover_ok and pay_ok and flags_ok and all(r.status == 0 for r in recs),
            "cover_ok": cover_ok, "payload_ok": pay_ok, "lookback_ok": flags_ok,
            "end_candidates_mean": float(np.mean([r.end + 1 for r in recs])),
@@ -312,6 +313,8 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
            # roundtrip_ok then reads False): uniform-noise slices at T=2
            "overflow_slices": int(sum(1 for r in recs if r.status == 1)),
            "repaired_slices": codec.repaired(pw)}
+    if T == "auto":
+        res["T_chosen"] = {str(t): int(sum(1 for r in recs if r.T == t)) for t in sorted({r.T for r in recs})}
     if xch is not None:
         om, ol = xch.own_rows(rank)
         res["exchange_ok"] = bool(torch.equal(om.contiguous().view(torch.uint8)[:, : _lib.PEE_META_BYTES], meta)) and \
@@ -455,8 +458,9 @@ def bench_c3(args, torch, dist, world, dev, rank):
     reference's LSB step in `lsb`."""
     B, H, W = 256, 512, 512
     covers = make_covers(torch, args.kind, B, H, W, dev, seed=1000 + rank * B)
-    res = {"workload": f"{args.kind} 512x512 uint16 x 256 slices (C3)"}
-    res.update(bench_pee(args, torch, dist, 1, rank, dev, covers, B, H, W, steps=4 * args.steps))
+    res = {"workload": f"{args.kind} 512x512 uint16 x 256 slices (C3), MED-PEE with capacity control "
+                       f"(T = 'auto': a {args.payload_chars}-char payload needs T ~ 4-5 on a 512^2 ct12 slice)"}
+    res.update(bench_pee(args, torch, dist, 1, rank, dev, covers, B, H, W, steps=4 * args.steps, T="auto"))
     lsb = bench_lsb(args, torch, dist, 1, rank, dev, covers, B, H, W, steps=4 * args.steps, seed0=5000)
     lsb.pop("_stego", None)
     res["lsb"] = lsb

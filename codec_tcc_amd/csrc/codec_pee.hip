@@ -120,8 +120,8 @@ struct Quad {
 // HBM; the wave's shuffle reduction writes the tile count directly (no LDS, no barrier).
 template <typename T, bool NT>
 __global__ __launch_bounds__(256) void k_pee_scan(const T* __restrict__ cover, T* __restrict__ stego, int H, int W,
-                                                  int Tthr, int maxval, uint32_t* __restrict__ tile_cnt_all,
-                                                  int ntiles_max, int B) {
+                                                  int T0, int maxval, uint32_t* __restrict__ tile_cnt_all,
+                                                  int ntiles_max, int B, const int32_t* __restrict__ tps) {
     typedef typename Vec8<T>::type V;
     const size_t npx = (size_t)H * W;
     const int CR = W / 8, hc = H / 2;
@@ -132,6 +132,7 @@ __global__ __launch_bounds__(256) void k_pee_scan(const T* __restrict__ cover, T
     const uint32_t wstride = gridDim.x * 4u;
     for (uint32_t g = blockIdx.x * 4u + (threadIdx.x >> 6); g < total; g += wstride) {
         const uint32_t b = g / ntiles, t = g - b * ntiles;
+        const int Tthr = tps ? tps[b] : T0;   // per-slice threshold (capacity control) or one for all
         const T* src = cover + b * npx;
         T* dst = stego + b * npx;
         V v0[4], v1[4];
@@ -181,11 +182,12 @@ __global__ __launch_bounds__(256) void k_pee_scan(const T* __restrict__ cover, T
 
 // ---- scan for any shape: counts only (the copy is a separate stream copy)
 template <typename T>
-__global__ __launch_bounds__(256) void k_pee_count(const T* __restrict__ img, int H, int W, int Tthr, int maxval,
+__global__ __launch_bounds__(256) void k_pee_count(const T* __restrict__ img, int H, int W, int T0, int maxval,
                                                    int tiles_per_wg, uint32_t* __restrict__ tile_cnt_all,
-                                                   int ntiles_max) {
+                                                   int ntiles_max, const int32_t* __restrict__ tps) {
     __shared__ uint32_t sh[8];
     const int b = blockIdx.y;
+    const int Tthr = tps ? tps[b] : T0;
     const T* src = img + (size_t)b * H * W;
     const int wc = W / 2, nc = (H / 2) * wc;
     const int ntiles = (nc + PEE_TILE - 1) / PEE_TILE;
@@ -211,16 +213,18 @@ __global__ __launch_bounds__(256) void k_pee_count(const T* __restrict__ img, in
 
 // ---- per slice: exclusive tile offsets, capacity, tile holding bit L-1, exact `end`
 template <typename T>
-__global__ __launch_bounds__(256) void k_pee_locate(const T* __restrict__ img, int H, int W, int Tthr, int maxval,
+__global__ __launch_bounds__(256) void k_pee_locate(const T* __restrict__ img, int H, int W, int T0, int maxval,
                                                     const int32_t* __restrict__ lengths,
                                                     const uint32_t* __restrict__ tile_cnt_all,
                                                     uint32_t* __restrict__ tile_off_all, int ntiles_max,
-                                                    codec_pee_meta* __restrict__ meta_all) {
+                                                    codec_pee_meta* __restrict__ meta_all,
+                                                    const int32_t* __restrict__ tps) {
     __shared__ uint32_t sh[8];
     __shared__ int s_tile;
     __shared__ uint32_t s_base;
     __shared__ int s_end;
     const int b = blockIdx.x;
+    const int Tthr = tps ? tps[b] : T0;
     const int wc = W / 2, nc = (H / 2) * wc;
     const int ntiles = (nc + PEE_TILE - 1) / PEE_TILE;
     const uint32_t* cnt = tile_cnt_all + (size_t)b * ntiles_max;
@@ -352,6 +356,72 @@ __global__ __launch_bounds__(256) void k_pee_embed(const T* __restrict__ cover, 
         if (threadIdx.x == 0 && nun) atomicAdd(&M->lm_count, (int)nun);
         __syncthreads();
     }
+}
+
+// ---- capacity control.  The expansion safety test (p + 2e >= 0, p + 2e + 1 <= maxval)
+// does not depend on T, so one pass that histograms the prediction errors e in
+// [-tmax, tmax) of the candidates whose expansion would be safe gives every capacity
+// exactly: capacity(T) = sum of the bins e in [-T, T).  grid (regions, B), LDS bins per
+// workgroup, flushed with one global atomic per non-zero bin.
+#define PEE_TMAX_MAX 64
+template <typename T, bool VEC>
+__global__ __launch_bounds__(256) void k_pee_ehist(const T* __restrict__ img, int H, int W, int maxval, int tmax,
+                                                   int per_wg, uint32_t* __restrict__ hist_all) {
+    typedef typename Vec8<T>::type V;
+    __shared__ uint32_t bins[2 * PEE_TMAX_MAX];
+    const int b = blockIdx.y;
+    const T* src = img + (size_t)b * H * W;
+    for (int i = threadIdx.x; i < 2 * tmax; i += 256) bins[i] = 0;
+    __syncthreads();
+    const int wc = W / 2;
+    auto add = [&](int x, int a, int bb, int cc) {
+        const int p = med3(a, bb, cc), e = x - p;
+        if (e >= -tmax && e < tmax && p + 2 * e >= 0 && p + 2 * e + 1 <= maxval) atomicAdd(&bins[e + tmax], 1u);
+    };
+    if constexpr (VEC) {
+        const int CR = W / 8;
+        const int items = (H / 2) * CR;
+        const int i0 = blockIdx.x * per_wg, i1 = min(items, i0 + per_wg);
+        for (int it = i0 + threadIdx.x; it < i1; it += 256) {
+            const int r = it / CR, c = it - r * CR;
+            const size_t o0 = (size_t)(2 * r) * W + (size_t)c * 8;
+            const V v0 = *reinterpret_cast<const V*>(src + o0);
+            const V v1 = *reinterpret_cast<const V*>(src + o0 + W);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                add((int)get_px(v1, 2 * q + 1), (int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1), (int)get_px(v0, 2 * q));
+        }
+    } else {
+        const int nc = (H / 2) * wc;
+        const int k0 = blockIdx.x * per_wg, k1 = min(nc, k0 + per_wg);
+        for (int k = k0 + threadIdx.x; k < k1; k += 256) {
+            int x, a, bb, cc;
+            pee_load(src, W, wc, k, &x, &a, &bb, &cc);
+            add(x, a, bb, cc);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * tmax; i += 256)
+        if (bins[i]) atomicAdd(&hist_all[(size_t)b * 2 * tmax + i], bins[i]);
+}
+
+// capacities at T = 1..tmax from the error histogram, and the smallest T whose capacity
+// holds the slice's payload (tmax if none does)
+__global__ __launch_bounds__(256) void k_pee_select(const uint32_t* __restrict__ hist_all, int tmax, int B,
+                                                    const int32_t* __restrict__ lengths, int32_t* __restrict__ caps,
+                                                    int32_t* __restrict__ t_out) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= B) return;
+    const uint32_t* h = hist_all + (size_t)b * 2 * tmax;
+    const long long L = lengths ? (long long)max(0, lengths[b]) : 0;
+    long long run = 0;
+    int tsel = 0;
+    for (int t = 1; t <= tmax; ++t) {
+        run += (long long)h[tmax - t] + h[tmax + t - 1];
+        if (caps) caps[(size_t)b * tmax + t - 1] = (int32_t)run;
+        if (!tsel && run >= L) tsel = t;
+    }
+    if (t_out) t_out[b] = tsel ? tsel : tmax;
 }
 
 // ---- decode-side cursor counts, wave per tile (W % 8 == 0): a tile's 256 items are 4 per
@@ -991,12 +1061,12 @@ __host__ __device__ __forceinline__ uint32_t pee_total_slots(int B, int nchunks,
 #define PEE_SKIP 0xFFFFFFFFu
 #define PEE_STOP 0xFFFFFFFEu
 template <typename T, bool NT, bool INPLACE>
-__global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover, T* stego, int H, int W, int Tthr,
+__global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover, T* stego, int H, int W, int T0,
                                                     int maxval, const int32_t* __restrict__ lengths,
                                                     const u64* __restrict__ payload_all, int pw, int nchunks, int B,
                                                     u64* status_all, uint32_t* ctl, codec_pee_meta* meta_all,
                                                     u64* __restrict__ lm_all, int lmw, int mode, uint32_t spin_max,
-                                                    int dbg_skip, uint32_t* diag) {
+                                                    int dbg_skip, uint32_t* diag, const int32_t* __restrict__ tps) {
     typedef typename Vec8<T>::type V;
     __shared__ u64 sh64[8];
     __shared__ uint32_t sh[8];
@@ -1016,6 +1086,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
         uint32_t* tick = ctl + 32 + 32 * (size_t)b;
         u64* st = status_all + (size_t)b * nchunks;
         const uint32_t L = (uint32_t)max(0, lengths[b]);
+        const int Tthr = tps ? tps[b] : T0;   // per-slice threshold (capacity control) or one for all
         codec_pee_meta* M = meta_all + b;
         const T* src = cover + b * npx;
         T* dst = stego + b * npx;
@@ -1399,7 +1470,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
 
 // ====================================================================== host side
 struct PeeWs {
-    size_t cnt, off, st, ctl, diag, total;
+    size_t cnt, off, st, ctl, diag, hist, total;
     int ntiles_max, nchunks;
 };
 
@@ -1417,7 +1488,9 @@ static PeeWs pee_ws(const codec_pee_params* P) {
     L.ctl = L.st + (size_t)P->B * L.nchunks * 8;   // status words and ctl are cleared together
     // diag: 4 cumulative uint32 counters (codec_pee_diag_offset), outside the per-call memset
     L.diag = align_up(L.ctl + PEE_CTL_WORDS(P->B) * 4, 16);
-    L.total = align_up(L.diag + 16, 256);
+    // capacity-control error histogram (codec_pee_capacity; cleared by that call)
+    L.hist = align_up(L.diag + 16, 256);
+    L.total = align_up(L.hist + (size_t)P->B * 2 * PEE_TMAX_MAX * 4, 256);
     return L;
 }
 
@@ -1454,6 +1527,40 @@ size_t codec_pee_extract_flag_offset(const codec_pee_params* P) {
     return pee_ws(P).ctl + 4;   // ctl[1]: set when an extract chunk's look-back gave up
 }
 
+int codec_pee_capacity(const codec_pee_params* P, const void* cover, int32_t tmax, const int32_t* lengths,
+                       int32_t* caps, int32_t* t_out, void* workspace, size_t workspace_bytes, void* stream) {
+    int rc = pee_check(P);
+    if (rc) return rc;
+    if (!cover || !workspace) return set_err(CODEC_EINVAL, "codec_pee_capacity: NULL pointer argument");
+    if (tmax < 1 || tmax > PEE_TMAX_MAX) return set_err(CODEC_EINVAL, "tmax must be in 1..64");
+    if (t_out && !lengths) return set_err(CODEC_EINVAL, "codec_pee_capacity: t_out needs lengths");
+    const PeeWs L = pee_ws(P);
+    if (workspace_bytes < L.total) return set_err(CODEC_EINVAL, "workspace too small");
+    hipStream_t st = as_stream(stream);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.hist);
+    HIP_TRY(hipMemsetAsync(hist, 0, (size_t)P->B * 2 * tmax * 4, st));
+    const size_t va = P->bytes == 2 ? 16 : 8;
+    const bool vec = (P->W % 8) == 0 && ((uintptr_t)cover % va) == 0;
+    const long long units = vec ? (long long)(P->H / 2) * (P->W / 8) : (long long)(P->H / 2) * (P->W / 2);
+    ProfScope prof(st, CODEC_K_PEE_CAPACITY);
+    if (units > 0) {
+        const long long per = knob("CODEC_PEE_EHIST_PER_WG", 4096);
+        dim3 grid((unsigned)((units + per - 1) / per), (unsigned)P->B);
+#define PEH(TT, VV) hipLaunchKernelGGL((k_pee_ehist<TT, VV>), grid, dim3(256), 0, st, static_cast<const TT*>(cover), P->H, \
+                                       P->W, P->maxval, (int)tmax, (int)per, hist)
+        if (P->bytes == 2) { if (vec) PEH(uint16_t, true); else PEH(uint16_t, false); }
+        else { if (vec) PEH(uint8_t, true); else PEH(uint8_t, false); }
+#undef PEH
+        LAUNCH_CHECK("k_pee_ehist");
+    }
+    if (caps || t_out) {
+        hipLaunchKernelGGL(k_pee_select, dim3((unsigned)((P->B + 255) / 256)), dim3(256), 0, st, hist, (int)tmax, P->B,
+                           lengths, caps, t_out);
+        LAUNCH_CHECK("k_pee_select");
+    }
+    return 0;
+}
+
 size_t codec_pee_diag_offset(const codec_pee_params* P) {
     if (pee_check(P)) return 0;
     return pee_ws(P).diag;
@@ -1462,6 +1569,12 @@ size_t codec_pee_diag_offset(const codec_pee_params* P) {
 int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, const uint64_t* payload,
                     const int32_t* lengths, codec_pee_meta* meta, uint64_t* lm, void* workspace,
                     size_t workspace_bytes, void* stream) {
+    return codec_pee_embed_ts(P, cover, stego, payload, lengths, nullptr, meta, lm, workspace, workspace_bytes, stream);
+}
+
+int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego, const uint64_t* payload,
+                       const int32_t* lengths, const int32_t* tps, codec_pee_meta* meta, uint64_t* lm, void* workspace,
+                       size_t workspace_bytes, void* stream) {
     int rc = pee_check(P);
     if (rc) return rc;
     if (!cover || !stego || !payload || !lengths || !meta || !lm || !workspace)
@@ -1524,7 +1637,7 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
 #define PE1(TT, NTV, IP) hipLaunchKernelGGL((k_pee_embed1<TT, NTV, IP>), dim3((unsigned)g), dim3(256), 0, st, \
             static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, \
             reinterpret_cast<const u64*>(payload), P->payload_words, L.nchunks, P->B, stw, ctl, meta, \
-            reinterpret_cast<u64*>(lm), P->lm_words, mode, spin_max, dbg_skip, diag)
+            reinterpret_cast<u64*>(lm), P->lm_words, mode, spin_max, dbg_skip, diag, tps)
         if (P->bytes == 2) {
             if (inplace) { if (nt) PE1(uint16_t, true, true); else PE1(uint16_t, false, true); }
             else { if (nt) PE1(uint16_t, true, false); else PE1(uint16_t, false, false); }
@@ -1552,7 +1665,7 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
             long long gw = knob("CODEC_PEE_SCAN_GS_WGS", 32768);   // tools/tune_pee.py
             if (gw > (tot + 3) / 4) gw = (tot + 3) / 4;
             if (gw < 1) gw = 1;
-#define PSCAN(TT, NTV) hipLaunchKernelGGL((k_pee_scan<TT, NTV>), dim3((unsigned)gw), dim3(256), 0, st, static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, cnt, L.ntiles_max, P->B)
+#define PSCAN(TT, NTV) hipLaunchKernelGGL((k_pee_scan<TT, NTV>), dim3((unsigned)gw), dim3(256), 0, st, static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, cnt, L.ntiles_max, P->B, tps)
             if (P->bytes == 2) { if (nt) PSCAN(uint16_t, true); else PSCAN(uint16_t, false); }
             else { if (nt) PSCAN(uint8_t, true); else PSCAN(uint8_t, false); }
 #undef PSCAN
@@ -1561,10 +1674,10 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
             if (!inplace) HIP_TRY(hipMemcpyAsync(stego, cover, (size_t)npx * P->B * P->bytes, hipMemcpyDeviceToDevice, st));
             if (P->bytes == 2)
                 hipLaunchKernelGGL(k_pee_count<uint16_t>, grid, dim3(256), 0, st, static_cast<const uint16_t*>(cover),
-                                   P->H, P->W, P->T, P->maxval, per, cnt, L.ntiles_max);
+                                   P->H, P->W, P->T, P->maxval, per, cnt, L.ntiles_max, tps);
             else
                 hipLaunchKernelGGL(k_pee_count<uint8_t>, grid, dim3(256), 0, st, static_cast<const uint8_t*>(cover),
-                                   P->H, P->W, P->T, P->maxval, per, cnt, L.ntiles_max);
+                                   P->H, P->W, P->T, P->maxval, per, cnt, L.ntiles_max, tps);
             LAUNCH_CHECK("k_pee_count");
         }
     }
@@ -1572,10 +1685,10 @@ int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, c
         ProfScope prof(st, CODEC_K_PEE_LOCATE);
         if (P->bytes == 2)
             hipLaunchKernelGGL(k_pee_locate<uint16_t>, dim3(P->B), dim3(256), 0, st, static_cast<const uint16_t*>(cover),
-                               P->H, P->W, P->T, P->maxval, lengths, cnt, off, L.ntiles_max, meta);
+                               P->H, P->W, P->T, P->maxval, lengths, cnt, off, L.ntiles_max, meta, tps);
         else
             hipLaunchKernelGGL(k_pee_locate<uint8_t>, dim3(P->B), dim3(256), 0, st, static_cast<const uint8_t*>(cover),
-                               P->H, P->W, P->T, P->maxval, lengths, cnt, off, L.ntiles_max, meta);
+                               P->H, P->W, P->T, P->maxval, lengths, cnt, off, L.ntiles_max, meta, tps);
         LAUNCH_CHECK("k_pee_locate");
     }
     {

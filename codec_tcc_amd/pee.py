@@ -33,8 +33,11 @@ class PeeEncoded:
 
 
 class PeeCodec:
-    def __init__(self, batch: int, height: int, width: int, dtype="uint16", *, T: int = 2,
+    def __init__(self, batch: int, height: int, width: int, dtype="uint16", *, T=2, tmax: int = 16,
                  maxval: Optional[int] = None, device=None):
+        """T: the expansion threshold for every slice, or "auto" -- capacity control: each
+        slice gets the smallest T <= tmax whose capacity holds its payload
+        (codec_pee_capacity, one extra read-only pass; meta.T records the choice)."""
         _require_gpu()
         torch = _torch()
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -43,7 +46,13 @@ class PeeCodec:
             raise ValueError("A imagem deve ser uint8 ou uint16.")
         vmax = 65535 if nbytes == 2 else 255
         self.B, self.H, self.W, self.bytes = int(batch), int(height), int(width), nbytes
-        self.T = int(T)
+        self.auto = isinstance(T, str)
+        if self.auto and T != "auto":
+            raise ValueError("T must be an integer >= 1 or 'auto'")
+        self.T = 1 if self.auto else int(T)
+        if not 1 <= int(tmax) <= 64:
+            raise ValueError("tmax must be in 1..64")
+        self.tmax = int(tmax)
         self.maxval = vmax if maxval is None else int(maxval)
         self.nc = (self.H // 2) * (self.W // 2)
         self.lm_words = max(1, (self.nc + 63) // 64)
@@ -53,6 +62,7 @@ class PeeCodec:
             _lib.check(-1, "codec_pee_workspace_bytes")
         # zeroed once: the cumulative look-back diagnostics live in it (codec_pee_diag_offset)
         self.workspace = torch.zeros(int(ws), dtype=torch.uint8, device=self.device)
+        self.t_slices = torch.empty(self.B, dtype=torch.int32, device=self.device) if self.auto else None
 
     def _params(self, payload_words: int) -> _lib.PeeParams:
         return _lib.PeeParams(B=self.B, H=self.H, W=self.W, bytes=self.bytes, T=self.T, maxval=self.maxval,
@@ -66,6 +76,16 @@ class PeeCodec:
         packed, lengths = framing.pack_bits(bits)
         return (torch.from_numpy(packed).to(self.device), lengths,
                 torch.tensor(lengths, dtype=torch.int32, device=self.device))
+
+    def capacity(self, covers, tmax: Optional[int] = None):
+        """int32 [B, tmax] device tensor: exact capacity of each slice at T = 1..tmax."""
+        torch = _torch()
+        tmax = self.tmax if tmax is None else int(tmax)
+        caps = torch.empty((self.B, tmax), dtype=torch.int32, device=self.device)
+        _lib.check(_lib.load().codec_pee_capacity(C.byref(self._params(1)), covers.data_ptr(), tmax, None,
+                                                  caps.data_ptr(), None, self.workspace.data_ptr(),
+                                                  self.workspace.numel(), _stream()), "codec_pee_capacity")
+        return caps
 
     def embed(self, covers, payloads, *, stego=None, lm=None, meta=None, packed=None, check: bool = True) -> PeeEncoded:
         """cover -> stego + location map + per-slice meta.  check=True (default) reads the
@@ -83,9 +103,16 @@ class PeeCodec:
         if meta is None:
             meta = torch.empty((self.B, _lib.PEE_META_BYTES), dtype=torch.uint8, device=self.device)
         P = self._params(words.shape[1])
-        _lib.check(_lib.load().codec_pee_embed(C.byref(P), covers.data_ptr(), stego.data_ptr(), words.data_ptr(),
-                                               lens_t.data_ptr(), meta.data_ptr(), lm.data_ptr(),
-                                               self.workspace.data_ptr(), self.workspace.numel(), _stream()),
+        lib = _lib.load()
+        tps = None
+        if self.auto:   # capacity control: per-slice T from one read-only pass, on the device
+            _lib.check(lib.codec_pee_capacity(C.byref(P), covers.data_ptr(), self.tmax, lens_t.data_ptr(), None,
+                                              self.t_slices.data_ptr(), self.workspace.data_ptr(),
+                                              self.workspace.numel(), _stream()), "codec_pee_capacity")
+            tps = self.t_slices.data_ptr()
+        _lib.check(lib.codec_pee_embed_ts(C.byref(P), covers.data_ptr(), stego.data_ptr(), words.data_ptr(),
+                                          lens_t.data_ptr(), tps, meta.data_ptr(), lm.data_ptr(),
+                                          self.workspace.data_ptr(), self.workspace.numel(), _stream()),
                    "codec_pee_embed")
         enc = PeeEncoded(stego=stego, lm=lm, meta=meta, lengths=list(lengths), payload_words=int(words.shape[1]))
         if check:
@@ -127,7 +154,8 @@ class PeeCodec:
         _raise_lookback(recs)
         bad = [i for i, r in enumerate(recs) if r.status != 0]
         if bad:
-            raise ValueError(f"payload exceeds PEE capacity in slices {bad} (T={self.T})")
+            raise ValueError(f"payload exceeds PEE capacity in slices {bad} "
+                             f"(T={'auto, tmax=%d' % self.tmax if self.auto else self.T})")
         words, cover = self.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words)
         host = words.cpu().numpy()
         if self.lookback_failed(enc.payload_words):

@@ -247,6 +247,19 @@ size_t codec_pee_diag_offset(const codec_pee_params* P);
 int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, const uint64_t* payload,
                     const int32_t* lengths, codec_pee_meta* meta, uint64_t* lm, void* workspace,
                     size_t workspace_bytes, void* stream);
+/* codec_pee_embed with a per-slice threshold: T_per_slice[B] (device int32, >= 1) replaces
+ * P->T for slice b (meta.T records it; extract reads it from meta).  NULL = P->T for all.
+ * Pair with codec_pee_capacity's t_out for capacity control. */
+int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego, const uint64_t* payload,
+                       const int32_t* lengths, const int32_t* T_per_slice, codec_pee_meta* meta, uint64_t* lm,
+                       void* workspace, size_t workspace_bytes, void* stream);
+/* Capacity control (one read-only pass over cover; P->T is ignored, 1 <= tmax <= 64):
+ * caps[B][tmax] = exact capacity of slice b at T = 1..tmax (expandable candidates whose
+ * expansion stays in [0, maxval]), t_out[B] = the smallest T <= tmax whose capacity holds
+ * lengths[b] bits (tmax if none does: the embed then truncates, status 1).  caps or t_out
+ * may be NULL (t_out needs lengths).  Uses the PEE workspace. */
+int codec_pee_capacity(const codec_pee_params* P, const void* cover, int32_t tmax, const int32_t* lengths,
+                       int32_t* caps, int32_t* t_out, void* workspace, size_t workspace_bytes, void* stream);
 /* stego -> exact payload bits + restored cover.  cover_out == stego is allowed (in
  * place: only the items up to `end` are read and written). */
 int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_pee_meta* meta,
@@ -289,6 +302,7 @@ int codec_quality_moments(int32_t B, int32_t H, int32_t W, int32_t bytes, const 
 #define CODEC_K_SCAN_ROWS_READ 20
 #define CODEC_K_QUALITY 21
 #define CODEC_K_DECIDE_EMBED 22
+#define CODEC_K_PEE_CAPACITY 23
 int codec_profile_begin(int32_t capacity);
 /* after the stream has been synchronised: fills ms[i], tag[i] for the recorded pairs and
  * returns their count (closes the window and frees the events). */

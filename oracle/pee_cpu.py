@@ -119,6 +119,26 @@ def pee_extract(stego: np.ndarray, side: Dict) -> Tuple[np.ndarray, np.ndarray]:
     return bits, cover
 
 
+def capacity_curve(cover: np.ndarray, tmax: int, maxval: int | None = None) -> np.ndarray:
+    """Capacities at T = 1..tmax.  The expansion safety test does not depend on T, so the
+    curve is a cumulative count of prediction errors e in [-T, T) over the candidates whose
+    expansion stays in [0, maxval] (this is what codec_pee_capacity computes)."""
+    maxval = int(np.iinfo(cover.dtype).max) if maxval is None else int(maxval)
+    x, a, b, c = _grids(cover)
+    p = med(a, b, c)
+    e = (x - p).ravel()
+    p = p.ravel()
+    ok = (p + 2 * e >= 0) & (p + 2 * e + 1 <= maxval)
+    return np.array([int((ok & (e >= -T) & (e < T)).sum()) for T in range(1, tmax + 1)], dtype=np.int64)
+
+
+def select_T(cover: np.ndarray, L: int, tmax: int = 16, maxval: int | None = None) -> int:
+    """The smallest T <= tmax whose capacity holds L bits (tmax if none does)."""
+    curve = capacity_curve(cover, tmax, maxval)
+    hit = np.flatnonzero(curve >= L)
+    return int(hit[0]) + 1 if hit.size else tmax
+
+
 def capacity(cover: np.ndarray, T: int = 2, maxval: int | None = None) -> int:
     maxval = int(np.iinfo(cover.dtype).max) if maxval is None else int(maxval)
     x, a, b, c = _grids(cover)

@@ -346,3 +346,55 @@ def test_gpu_lookback_timeout_in_place_raises(monkeypatch):
     assert codec.lookback_failed(enc.payload_words)
     assert codec.diagnostics()["extract_unrecovered_chunks"] >= 1
     np.testing.assert_array_equal(enc.stego.cpu().numpy(), covers)
+
+
+@pytest.mark.parametrize("kind,h,w,maxval", [("ct12", 64, 64, None), ("ct12", 37, 53, 4095), ("u8", 40, 24, None),
+                                             ("u16", 32, 32, None)])
+def test_oracle_capacity_curve(kind, h, w, maxval):
+    img = synth.GENERATORS[kind](h, w, 13)
+    curve = P.capacity_curve(img, 12, maxval)
+    assert list(curve) == [P.capacity(img, T, maxval) for T in range(1, 13)]
+    assert all(np.diff(curve) >= 0)
+    L = int(curve[5])
+    assert P.select_T(img, L, 12, maxval) == int(np.flatnonzero(curve >= L)[0]) + 1
+    assert P.select_T(img, int(curve[-1]) + 1, 12, maxval) == 12
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inplace", [False, True])
+@pytest.mark.parametrize("kind,h,w,bsz", [("ct12", 512, 512, 5), ("ct12", 37, 53, 3), ("u8", 96, 64, 2),
+                                          ("ct12", 256, 256, 40)])
+def test_gpu_capacity_control(kind, h, w, bsz, inplace, pee_path):
+    """T="auto": the device capacity curve equals the oracle's, each slice gets the smallest
+    T whose capacity holds its payload, and stego / map / payload / cover equal the oracle's
+    embed at that T (a payload beyond tmax's capacity truncates, status 1)."""
+    torch = pytest.importorskip("torch")
+    from codec_tcc_amd import framing
+    from codec_tcc_amd.pee import PeeCodec, lm_bits
+    tmax = 8
+    covers = np.stack([synth.GENERATORS[kind](h, w, 140 + i) for i in range(bsz)])
+    curves = [P.capacity_curve(c, tmax) for c in covers]
+    lens = [int(cv[(3 * i) % tmax]) - (i % 3) for i, cv in enumerate(curves)]
+    lens[0] = int(curves[0][-1]) + 50                       # beyond tmax's capacity: truncated
+    payloads = [_bits(max(0, n), 200 + i) for i, n in enumerate(lens)]
+    codec = PeeCodec(bsz, h, w, dtype=str(covers.dtype), T="auto", tmax=tmax)
+    dev = torch.from_numpy(covers).cuda()
+    caps = codec.capacity(dev).cpu().numpy()
+    np.testing.assert_array_equal(caps, np.stack(curves))
+    enc = codec.embed(dev, payloads, stego=dev if inplace else None)
+    recs = enc.records()
+    stego = enc.stego.cpu().numpy()
+    for i in range(bsz):
+        T = P.select_T(covers[i], len(payloads[i]), tmax)
+        assert recs[i].T == T, i
+        st, side = P.pee_embed(covers[i], payloads[i], T, truncate=True)
+        assert recs[i].status == side["status"] and recs[i].end == side["end"]
+        np.testing.assert_array_equal(stego[i], st)
+        np.testing.assert_array_equal(lm_bits(enc, i), side["lm"])
+    words, cover = codec.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words,
+                                 cover=enc.stego if inplace else None)
+    host = words.cpu().numpy()
+    for i in range(bsz):
+        n = min(len(payloads[i]), int(curves[i][-1]))
+        np.testing.assert_array_equal(framing.unpack_bits(host[i], n), payloads[i][:n])
+    np.testing.assert_array_equal(cover.cpu().numpy(), covers)
