@@ -27,7 +27,7 @@ codec.py:588).  The reference's progress print()s are not reproduced.
 from __future__ import annotations
 
 import ctypes as C
-from typing import List, Sequence
+from typing import List, Optional, Sequence
 
 import numpy as np
 
@@ -363,13 +363,14 @@ def decode_message(stego_planes, bitmaps, metadata) -> str:
 
 
 def decode_positional(stego_array, bitmaps, metadata, search_block_size: int = 16,
-                      align_across_planes: bool = False):
+                      align_across_planes: bool = False, start_offset: Optional[int] = None):
     """Exact recovery from the reference's outputs.
 
     The dense bitmaps mark flipped LSBs only, so the cover is `stego ^ bitmaps`; the start
     offset is re-derived on the restored plane 0 exactly as the embedder derived it
-    (codec.py:431-453) and the windows are read back in segment_indices order.
-    Returns (message_bits as a '0'/'1' string, restored cover)."""
+    (codec.py:431-453) and the windows are read back in segment_indices order -- unless
+    start_offset is given (a version-2 container stores the real one), which is then used
+    as is.  Returns (message_bits as a '0'/'1' string, restored cover)."""
     _require_gpu()
     img = np.asarray(stego_array)
     if img.dtype not in (np.uint8, np.uint16) or img.ndim != 2:
@@ -394,7 +395,8 @@ def decode_positional(stego_array, bitmaps, metadata, search_block_size: int = 1
                                                cover.data_ptr(), _stream()), "codec_restore_dense")
     total = sum(sizes)
     codec = Codec(1, h, w, dtype=str(img.dtype), beta=0.0, block=int(search_block_size),
-                  align=bool(align_across_planes), mode="hybrid", fixed_s=s)
+                  align=bool(align_across_planes), mode="hybrid", fixed_s=s,
+                  fixed_offset=-1 if start_offset is None else int(start_offset))
     pl = make_payloads([np.zeros(max(total, 0), np.uint8)], dev)
     meta = codec.plan(cover, pl)
     m = meta_records(meta)[0]

@@ -13,6 +13,15 @@ negative sizes) and stores the real offset:
 
     header v2 = >BBBBIIi (version=2, codec_id, s, align, width, height, start_offset)
                 + s*>i segments_lengths + s*>B segment_indices + >I bitmaps_blob_size
+                [+ >H search_block_size]   (optional; 0 / absent = unknown)
+
+MED-PEE files (this build's scheme; the reference has no PEE format) use
+the same magic and framing with version 16:
+
+    header pee = >BBBB (version=16, codec_id, bytes per pixel, reserved)
+                 + >II (width, height) + >iiiii (T, L = embedded bits, end, maxval, status)
+                 + >I lm_blob_size
+    body       = zlib(location-map bits of candidates 0..end, LSB-first) | compressed stego
 
 Stego payload codecs: the reference's ids (png 1, j2k 2, jls 3, jxl 4) are kept; id 0
 ("raw", unknown to the reference) stores the stego pixels little-endian, uncompressed.
@@ -22,19 +31,21 @@ from __future__ import annotations
 import os
 import struct
 import zlib
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
 MAGIC = b"STGC"
+PEE_VERSION = 16
 CODEC_IDS = {"png": 1, "j2k": 2, "jls": 3, "jxl": 4}     # codec.py:616
 CODEC_NAMES = {1: "png", 2: "j2k", 3: "jls", 4: "jxl"}   # codec.py:693
 
 
 def create_header(codec: str, s: int, segments_lengths: Sequence[int], segments_indices: Sequence[int],
                   bitmaps_blob_size: int, width: int, height: int, start_offset: int,
-                  align_across_planes: bool, version: int = 1) -> bytes:
-    """codec.py:601-656 (version 1, identical bytes; raises struct.error where it does)."""
+                  align_across_planes: bool, version: int = 1, search_block_size: Optional[int] = None) -> bytes:
+    """codec.py:601-656 (version 1, identical bytes; raises struct.error where it does).
+    Version 2 may also record the block size of the start-offset search."""
     cid = CODEC_IDS.get(codec.lower(), 0)
     flag = 1 if align_across_planes else 0
     if version == 1:
@@ -43,8 +54,11 @@ def create_header(codec: str, s: int, segments_lengths: Sequence[int], segments_
         fmt = ">BBBBIIi" + f"{s}i" + f"{s}B" + "I"
     else:
         raise ValueError(f"unknown container version {version}")
-    return struct.pack(fmt, version, cid, s, flag, width, height, start_offset,
-                       *list(segments_lengths), *list(segments_indices), bitmaps_blob_size)
+    hdr = struct.pack(fmt, version, cid, s, flag, width, height, start_offset,
+                      *list(segments_lengths), *list(segments_indices), bitmaps_blob_size)
+    if version == 2 and search_block_size is not None:
+        hdr += struct.pack(">H", int(search_block_size))
+    return hdr
 
 
 def create_binary_file(filename: str, header_bytes: bytes, stego_compressed: bytes, bitmaps_bytes: bytes) -> int:
@@ -64,6 +78,8 @@ def parse_bin_bytes(data: bytes) -> Tuple[Dict, bytes, bytes]:
     (hlen,) = struct.unpack(">I", data[4:8])
     hdr = data[8:8 + hlen]
     version = hdr[0]
+    if version == PEE_VERSION:
+        raise ValueError("a MED-PEE container (version 16): use parse_pee_bytes / decode_bin_pee")
     base = ">BBBBHHH" if version == 1 else ">BBBBIIi"
     nb = struct.calcsize(base)
     version, cid, s, flag, width, height, start = struct.unpack(base, hdr[:nb])
@@ -72,10 +88,13 @@ def parse_bin_bytes(data: bytes) -> Tuple[Dict, bytes, bytes]:
     lens = list(struct.unpack(lf, hdr[nb:nb + nl]))
     idx = list(struct.unpack(f">{s}B", hdr[nb + nl:nb + nl + s]))
     (blob_size,) = struct.unpack(">I", hdr[nb + nl + s:nb + nl + s + 4])
+    rest = hdr[nb + nl + s + 4:]
     body = data[8 + hlen:]
     md = {"version": version, "codec": CODEC_NAMES.get(cid, "unknown"), "s": s, "align_flag": flag,
           "width": width, "height": height, "start_offset": start, "segments_lengths": lens,
           "segments_indices": idx}
+    if version == 2 and len(rest) >= 2:
+        md["search_block_size"] = struct.unpack(">H", rest[:2])[0] or None
     return md, body[:blob_size], body[blob_size:]
 
 
@@ -106,3 +125,40 @@ def decode_stego_raw(data: bytes, height: int, width: int) -> np.ndarray:
         raise ValueError("raw stego payload does not match the header's width x height")
     return np.frombuffer(data, dtype="<u2" if itemsize == 2 else np.uint8).reshape(height, width).astype(
         np.uint16 if itemsize == 2 else np.uint8)
+
+
+# ------------------------------------------------------------------ MED-PEE container
+_PEE_FMT = ">BBBBIIiiiiiI"
+
+
+def create_pee_header(codec: str, bytes_per_px: int, width: int, height: int, T: int, L: int, end: int,
+                      maxval: int, status: int, lm_blob_size: int) -> bytes:
+    return struct.pack(_PEE_FMT, PEE_VERSION, CODEC_IDS.get(codec.lower(), 0), int(bytes_per_px), 0, width, height,
+                       int(T), int(L), int(end), int(maxval), int(status), int(lm_blob_size))
+
+
+def lm_blob(lm_bits: np.ndarray) -> bytes:
+    """zlib of the location-map bits (candidates 0..end), packed LSB-first."""
+    return zlib.compress(np.packbits(np.asarray(lm_bits, dtype=np.uint8), bitorder="little").tobytes())
+
+
+def lm_from_blob(blob: bytes, end: int) -> np.ndarray:
+    raw = np.frombuffer(zlib.decompress(blob), dtype=np.uint8)
+    return np.unpackbits(raw, bitorder="little")[: end + 1].astype(bool)
+
+
+def parse_pee_bytes(data: bytes) -> Tuple[Dict, bytes, bytes]:
+    """A version-16 STGC file -> (side information, lm_blob, stego bytes)."""
+    if data[:4] != MAGIC:
+        raise ValueError("Arquivo inválido ou com assinatura incorreta.")   # codec.py:698
+    (hlen,) = struct.unpack(">I", data[4:8])
+    hdr = data[8:8 + hlen]
+    if not hdr or hdr[0] != PEE_VERSION:
+        raise ValueError("not a MED-PEE container (version 16)")
+    (_v, cid, bpp, _r, width, height, T, L, end, maxval, status, blob_size) = struct.unpack(
+        _PEE_FMT, hdr[:struct.calcsize(_PEE_FMT)])
+    body = data[8 + hlen:]
+    md = {"version": PEE_VERSION, "codec": CODEC_NAMES.get(cid, "raw" if cid == 0 else "unknown"),
+          "bytes": bpp, "width": width, "height": height, "T": T, "L": L, "end": end, "maxval": maxval,
+          "status": status}
+    return md, body[:blob_size], body[blob_size:]

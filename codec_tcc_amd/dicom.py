@@ -1,19 +1,24 @@
-"""Minimal DICOM reader / writer for uncompressed little-endian files.
+"""Minimal DICOM reader / writer for little-endian files.
 
 pydicom is not available on this image; the path only needs the pixel matrix of
 uncompressed slices (images/pe.dcm: Explicit VR LE, 12-bit in uint16; images/torax.dcm:
 Implicit VR LE, uint8) and a Secondary-Capture writer equivalent to `create_dicom`
-(codec.py:23-106).  Encapsulated (compressed) pixel data is refused with ValueError.
+(codec.py:23-106).  The Deflated Explicit VR Little Endian transfer syntax -- the
+reference's 'png' codec (codec.py:151-162 write, :203-206 read) -- is read and written
+too: the dataset after the file-meta group is one raw deflate stream (zlib, wbits -15).
+Encapsulated (JPEG-family) pixel data is refused with ValueError.
 """
 from __future__ import annotations
 
 import struct
+import zlib
 from typing import Dict, Optional, Tuple
 
 import numpy as np
 
 EXPLICIT_LE = "1.2.840.10008.1.2.1"
 IMPLICIT_LE = "1.2.840.10008.1.2"
+DEFLATED_LE = "1.2.840.10008.1.2.1.99"                      # codec.py:157
 SECONDARY_CAPTURE = "1.2.840.10008.5.1.4.1.1.7"           # codec.py:42
 _LONG_VR = {b"OB", b"OD", b"OF", b"OL", b"OV", b"OW", b"SQ", b"UC", b"UR", b"UT", b"UN", b"SV", b"UV"}
 _UNDEF = 0xFFFFFFFF
@@ -93,10 +98,13 @@ def read_dicom(src) -> Tuple[np.ndarray, Dict]:
         tags[tag] = (vr, i + hl, ln)
         i += hl + ln
     ts = _str(buf, tags[(0x0002, 0x0010)]) if (0x0002, 0x0010) in tags else EXPLICIT_LE
-    if ts not in (EXPLICIT_LE, IMPLICIT_LE):
-        raise ValueError(f"DICOM: transfer syntax {ts} not supported (uncompressed little endian only)")
+    if ts not in (EXPLICIT_LE, IMPLICIT_LE, DEFLATED_LE):
+        raise ValueError(f"DICOM: transfer syntax {ts} not supported (uncompressed or deflated little endian only)")
+    if ts == DEFLATED_LE:   # the dataset is one raw deflate stream after the file meta
+        buf = buf[:i] + zlib.decompress(buf[i:], -15)
+    explicit = ts != IMPLICIT_LE
     ds = {}
-    _Reader(buf, ts == EXPLICIT_LE).elements(i, ts == EXPLICIT_LE, out=ds)
+    _Reader(buf, explicit).elements(i, explicit, out=ds)
     if _PIXEL not in ds:
         raise ValueError("DICOM: no pixel data")
     rows, cols = _us(buf, ds[(0x0028, 0x0010)]), _us(buf, ds[(0x0028, 0x0011)])
@@ -128,9 +136,14 @@ def _elem(g, e, vr: bytes, value: bytes) -> bytes:
 
 def create_dicom_bytes(image: np.ndarray, *, sop_instance_uid: str = "1.2.826.0.1.3680043.10.1338.1",
                        study_uid: str = "1.2.826.0.1.3680043.10.1338.2", series_uid: str = "1.2.826.0.1.3680043.10.1338.3",
-                       date: str = "20250101", time: str = "000000") -> bytes:
-    """Secondary Capture, Explicit VR LE, uncompressed -- the dataset create_dicom builds
-    (codec.py:23-106), with caller-supplied UIDs/date so the output is deterministic."""
+                       date: str = "20250101", time: str = "000000", transfer_syntax: str = EXPLICIT_LE,
+                       level: int = -1) -> bytes:
+    """Secondary Capture, Explicit VR LE -- the dataset create_dicom builds (codec.py:23-106),
+    with caller-supplied UIDs/date so the output is deterministic.  transfer_syntax
+    DEFLATED_LE deflates the dataset (the reference's 'png' codec, codec.py:151-162; zlib
+    `level`); byte parity with pydicom's writer is unpinned (pydicom is absent here)."""
+    if transfer_syntax not in (EXPLICIT_LE, DEFLATED_LE):
+        raise ValueError(f"DICOM writer: transfer syntax {transfer_syntax} not supported")
     max_val = image.max()
     bits_stored = max(1, int(np.ceil(np.log2(float(max_val) + 1.0))))     # codec.py:27-32
     if image.ndim != 2:
@@ -170,10 +183,15 @@ def create_dicom_bytes(image: np.ndarray, *, sop_instance_uid: str = "1.2.826.0.
         _elem(0x0002, 0x0001, b"OB", b"\x00\x01"),
         _elem(0x0002, 0x0002, b"UI", SECONDARY_CAPTURE.encode()),
         _elem(0x0002, 0x0003, b"UI", sop_instance_uid.encode()),
-        _elem(0x0002, 0x0010, b"UI", EXPLICIT_LE.encode()),
+        _elem(0x0002, 0x0010, b"UI", transfer_syntax.encode()),
         _elem(0x0002, 0x0012, b"UI", b"1.2.826.0.1.3680043.10.1338"),
     ])
     meta = _elem(0x0002, 0x0000, b"UL", struct.pack("<I", len(meta_body))) + meta_body
+    if transfer_syntax == DEFLATED_LE:
+        co = zlib.compressobj(level, zlib.DEFLATED, -15)
+        ds = co.compress(ds) + co.flush()
+        if len(ds) % 2:
+            ds += b"\x00"   # even length (PS3.5 A.5)
     return b"\x00" * 128 + b"DICM" + meta + ds
 
 

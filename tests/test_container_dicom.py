@@ -118,3 +118,122 @@ def test_file_pipeline_gpu(name, tmp_path):
     bits, cover = pipeline.decode_bin_exact(out)
     assert bits == R.message_to_bits(msg)
     np.testing.assert_array_equal(cover, golden_io.images()[name])
+
+
+@pytest.mark.parametrize("dt", [np.uint8, np.uint16])
+def test_deflated_dicom_roundtrip(dt):
+    """The reference's 'png' codec = a Deflated Explicit VR LE DICOM (codec.py:151-162,
+    203-206): the dataset after the file meta is one raw deflate stream.  Byte parity with
+    pydicom's writer is unpinned (pydicom is absent); the pixel round trip is exact."""
+    import zlib
+    img = (np.arange(64 * 48).reshape(64, 48) * 13 % (4096 if dt == np.uint16 else 256)).astype(dt)
+    data = dicom.create_dicom_bytes(img, transfer_syntax=dicom.DEFLATED_LE)
+    back, info = dicom.read_dicom(data)
+    assert info["transfer_syntax"] == dicom.DEFLATED_LE
+    np.testing.assert_array_equal(back, img)
+    plain = dicom.create_dicom_bytes(img)
+    i = plain.index(b"DICM") + 4
+    meta_len = 12 + struct.unpack_from("<I", plain, i + 8)[0]
+    meta_len_d = 12 + struct.unpack_from("<I", data, i + 8)[0]
+    # the body after the (group-length-framed) file meta inflates to the plain dataset
+    assert zlib.decompress(data[i + meta_len_d:], -15) == plain[i + meta_len:]
+    assert len(data) < len(plain)
+
+
+def test_container_v2_block_field(tmp_path):
+    hdr = container.create_header("raw", 2, [3, 4], [1, 0], 5, 9, 9, 77, False, version=2, search_block_size=8)
+    path = str(tmp_path / "b.bin")
+    container.create_binary_file(path, hdr, b"px", b"01234")
+    md, bm, st = container.parse_bin_file(path)
+    assert md["search_block_size"] == 8 and md["start_offset"] == 77 and bm == b"01234" and st == b"px"
+    hdr = container.create_header("raw", 2, [3, 4], [1, 0], 5, 9, 9, 77, False, version=2)
+    container.create_binary_file(path, hdr, b"px", b"01234")
+    assert "search_block_size" not in container.parse_bin_file(path)[0]
+
+
+def test_pee_container_roundtrip(tmp_path):
+    lm = np.random.default_rng(3).random(1237) < 0.1
+    blob = container.lm_blob(lm)
+    hdr = container.create_pee_header("png", 2, 512, 510, 3, 8192, 1236, 4095, 0, len(blob))
+    path = str(tmp_path / "p.bin")
+    container.create_binary_file(path, hdr, b"stego-bytes", blob)
+    md, bm, st = container.parse_pee_bytes(open(path, "rb").read())
+    assert (md["codec"], md["bytes"], md["width"], md["height"]) == ("png", 2, 512, 510)
+    assert (md["T"], md["L"], md["end"], md["maxval"], md["status"]) == (3, 8192, 1236, 4095, 0)
+    assert st == b"stego-bytes"
+    np.testing.assert_array_equal(container.lm_from_blob(bm, md["end"]), lm)
+    with pytest.raises(ValueError):
+        container.parse_bin_file(path)            # the LSB parser refuses a PEE file
+    with pytest.raises(ValueError):
+        container.parse_pee_bytes(b"STGC" + struct.pack(">I", 1) + b"\x01")
+
+
+def test_j2k_jls_raise_clearly():
+    from codec_tcc_amd import pipeline
+    for c in ("j2k", "jls"):
+        with pytest.raises(RuntimeError, match="gdcmconv"):
+            pipeline._compress(np.zeros((4, 4), np.uint16), c)
+        with pytest.raises(RuntimeError, match="gdcmconv"):
+            pipeline._decompress(b"", c, 4, 4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["pe", "torax"])
+def test_file_pipeline_png_gpu(name, tmp_path):
+    """The 'png' (deflated DICOM) stego codec through encode_file -> decode_bin /
+    decode_bin_exact: the reference's stego and message bit for bit, exact payload + cover.
+    Also version 2 (stored offset and block size, block 8)."""
+    pytest.importorskip("torch")
+    from codec_tcc_amd import pipeline
+    from oracle import ref_cpu as R
+    src = str(tmp_path / f"{name}.dcm")
+    open(src, "wb").write(_dicom_file(name))
+    msg = "Mensagem de teste para esteganografia!"
+    out = str(tmp_path / "saida.bin")
+    info = pipeline.encode_file(src, msg, out, beta=0.4, block=16, codec="png")
+    golden = CASES[f"{name}_b0.4_main"]
+    np.testing.assert_array_equal(info["stego"], golden_io.stego(golden))
+    message, stego = pipeline.decode_bin(out)
+    assert message == golden_io.decoded(golden)
+    np.testing.assert_array_equal(stego, golden_io.stego(golden))
+    bits, cover = pipeline.decode_bin_exact(out)
+    assert bits == R.message_to_bits(msg)
+    np.testing.assert_array_equal(cover, golden_io.images()[name])
+    out2 = str(tmp_path / "v2.bin")
+    img = golden_io.images()[name]
+    info2 = pipeline.encode_file(img, msg, out2, beta=0.4, block=8, codec="png", version=2)
+    exp = R.encode_slice(img, R.message_to_bits(msg), beta=0.4, sb=8)
+    assert info2["start_offset"] == exp["start_offset"]
+    np.testing.assert_array_equal(info2["stego"], exp["stego"])
+    bits2, cover2 = pipeline.decode_bin_exact(out2)            # block 8 and the offset from the header
+    assert bits2 == R.message_to_bits(msg)
+    np.testing.assert_array_equal(cover2, img)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,codec,T", [("pe", "raw", 2), ("pe", "png", "auto"), ("torax", "png", 2)])
+def test_pee_file_pipeline_gpu(name, codec, T, tmp_path):
+    """C5 with the north star's algorithm: MED-PEE on the reference's real DICOMs, maxval
+    from BitsStored (pe.dcm: 12 bits -> 4095, overflow candidates in the location map),
+    written to a version-16 STGC file and recovered exactly from the file alone."""
+    pytest.importorskip("torch")
+    from codec_tcc_amd import framing, pipeline
+    from oracle import pee_cpu as P
+    src = str(tmp_path / f"{name}.dcm")
+    open(src, "wb").write(_dicom_file(name))
+    img = golden_io.images()[name]
+    maxval = 4095 if name == "pe" else 255
+    payload = "".join(chr(32 + (i * 7) % 95) for i in range(600))
+    bits = framing.to_bits(payload)
+    out = str(tmp_path / "pee.bin")
+    info = pipeline.encode_file_pee(src, payload, out, T=T, codec=codec)
+    assert info["maxval"] == maxval and info["status"] == 0
+    Texp = P.select_T(img, bits.size, 16, maxval) if T == "auto" else T
+    st, side = P.pee_embed(img, bits, Texp, maxval=maxval)
+    assert info["T"] == Texp and info["end"] == side["end"]
+    np.testing.assert_array_equal(info["stego"], st)
+    got, cover = pipeline.decode_bin_pee(out)
+    np.testing.assert_array_equal(got, bits)
+    np.testing.assert_array_equal(cover, img)
+    if name == "pe":
+        assert info["lm_count"] > 0 or side["lm"].sum() == 0
