@@ -1468,9 +1468,397 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
     }
 }
 
+// ====================================================================== slice-serial single pass
+// For batches that fill the chip (B >= the CU count and a near multiple of it): one
+// 1024-thread workgroup per slice streams that slice's chunks (1024 items = 4096
+// candidates = 32 KB of uint16) in order.  The running count of expandable candidates is
+// a register of the workgroup -- no look-back, no status words, no ticket, nothing to
+// memset -- and D chunks of pixels are in flight per workgroup (a register ring refilled
+// right after each chunk).  The payload words of a wave's rank range are wave-uniform
+// loads (scalar cache, lgkmcnt), so waiting for them never drains the vector-load ring.
+// A static LDS pad keeps exactly one workgroup per CU: one contiguous region streamed per
+// CU is the fastest order this chip copies in (DESIGN §3, 6.2 TB/s).  In place a slice
+// stops after the chunk holding `end`; out of place the chunks past `end` are copied and
+// only counted (exact capacity).
+//
+// Why the code is shaped the way it is: hipcc counts vmcnt precisely only through
+// straight-line vector memory code.  Every vector load and store of a chunk is therefore
+// unconditional -- loads of lanes/chunks past the end read a clamped valid address,
+// stores that must not land are redirected to a per-lane sink in the workspace -- and the
+// only branches left in the ring loop contain no vector memory instruction.  Barriers are
+// LDS-only (raw s_barrier): __syncthreads()'s fence waits vmcnt(0).
+#define SS_THREADS 1024
+#define SS_PAD_WORDS (21 * 1024)     // 84 KB of the CU's 160 KB: a second workgroup does not fit
+#define SS_PAY_WORDS (SS_PAD_WORDS / 2 - 1)   // the embed keeps payloads of up to 10 751 words in that pad
+#define SS_SINK_BYTES (SS_THREADS * 48)   // per lane: two 16-B pixel vectors + one 8-B word (+pad)
+
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <typename T, bool NT>
+__device__ __forceinline__ void ss_load(const T* src, int W, int CR, uint32_t items, int k,
+                                        typename Vec8<T>::type& x0, typename Vec8<T>::type& x1) {
+    typedef typename Vec8<T>::type V;
+    const uint32_t it = min((uint32_t)k * SS_THREADS + threadIdx.x, items - 1u);
+    const uint32_t r = it / (uint32_t)CR, cc = it - r * (uint32_t)CR;
+    const size_t o0 = (size_t)(2 * r) * W + (size_t)cc * 8;
+    x0 = ldv<NT>(reinterpret_cast<const V*>(src + o0));
+    x1 = ldv<NT>(reinterpret_cast<const V*>(src + o0 + W));
+}
+
+// exclusive scan of n over the 1024 threads with ONE barrier (wave totals double-buffered
+// by parity: a wave cannot rewrite wtot[par] before every wave has passed the next barrier)
+__device__ __forceinline__ void ss_scan(uint32_t n, uint32_t (*wtot)[16], int par, uint32_t* excl, uint32_t* tot,
+                                        uint32_t* wbase) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan(n);
+    if (lane == 63) wtot[par][wv] = inc;
+    lds_barrier();
+    uint32_t wb = 0, t = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+        const uint32_t v = wtot[par][w];
+        t += v;
+        wb += w < wv ? v : 0u;
+    }
+    *excl = wb + inc - n;
+    *tot = t;
+    *wbase = wb;
+}
+
+template <typename T, bool NT, bool INPLACE, int D, bool PAY_LDS>
+__global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict__ cover, T* stego, int H, int W, int T0,
+                                                             int maxval, const int32_t* __restrict__ lengths,
+                                                             const int32_t* __restrict__ tps,
+                                                             const u64* __restrict__ payload_all, int pw,
+                                                             codec_pee_meta* __restrict__ meta_all,
+                                                             u64* __restrict__ lm_all, int lmw, char* __restrict__ sink) {
+    typedef typename Vec8<T>::type V;
+    __shared__ uint32_t ss_pad[SS_PAD_WORDS];
+    __shared__ uint32_t wtot[2][16];
+    __shared__ uint32_t red[2][16];
+    __shared__ int s_end;
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int CR = W / 8;
+    const uint32_t items = (uint32_t)(H / 2) * (uint32_t)CR;
+    const int nchunks = (int)((items + SS_THREADS - 1) / SS_THREADS);
+    const int nc = (H / 2) * (W / 2);
+    const int ntiles = (nc + PEE_TILE - 1) / PEE_TILE;
+    const uint32_t L = (uint32_t)max(0, lengths[b]);
+    const int Tthr = tps ? tps[b] : T0;
+    const size_t npx = (size_t)H * W;
+    const T* src = cover + b * npx;
+    T* dst = stego + b * npx;
+    const u64* payload = payload_all + (size_t)b * pw;
+    u64* lm = lm_all + (size_t)b * lmw;
+    V* sink_v = reinterpret_cast<V*>(sink + (size_t)tid * 48);
+    u64* sink_w = reinterpret_cast<u64*>(sink + (size_t)tid * 48 + 32);
+    u64* pay = reinterpret_cast<u64*>(ss_pad);   // PAY_LDS: the slice's payload words
+    if (tid == 0) {
+        s_end = -1;
+        ss_pad[SS_PAD_WORDS - 1] = 0u;   // the occupancy pad stays allocated
+    }
+    V r0[D], r1[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) ss_load<T, NT>(src, W, CR, items, min(d, nchunks - 1), r0[d], r1[d]);
+    if (PAY_LDS) {   // the payload in LDS once: no dependent global round trip per chunk
+        const int nw = min(pw, (int)((L + 63u) >> 6));
+        for (int w = tid; w < nw; w += SS_THREADS) pay[w] = payload[w];
+        lds_barrier();
+    }
+    uint32_t running = 0, rest = 0, unsafe_n = 0;
+    int par = 0, last = -1;
+    bool live = L > 0;   // uniform: the chunk holding bit L-1 is still to come
+
+    // one chunk, processed in the ring registers, then the ring slot is refilled
+    auto chunk = [&](int d, int k) {
+        V& v0 = r0[d];
+        V& v1 = r1[d];
+        const uint32_t it = (uint32_t)k * SS_THREADS + tid;
+        const bool ok = it < items;
+        const uint32_t rr = it / (uint32_t)CR, cc = it - rr * (uint32_t)CR;
+        const size_t o0 = (size_t)(2 * rr) * W + (size_t)cc * 8;
+        // classification on every lane: the first use of the ring registers is unconditional
+        uint32_t esm = 0, safem = 0, rightm = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const PeeCand pc = pee_classify((int)get_px(v1, 2 * q + 1), (int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1),
+                                            (int)get_px(v0, 2 * q), Tthr, maxval);
+            safem |= pc.safe ? 1u << q : 0u;
+            rightm |= pc.right ? 1u << q : 0u;
+            esm |= (pc.expand && pc.safe) ? 1u << q : 0u;
+        }
+        if (!ok) esm = 0u;
+        const uint32_t n = (uint32_t)__popc(esm);
+        u64 wm = 0;
+        bool touched = false;
+        if (live) {   // uniform; no vector memory instruction inside
+            last = k;
+            uint32_t ex, tot, wb;
+            ss_scan(n, wtot, par, &ex, &tot, &wb);
+            par ^= 1;
+            // the wave's ranks lie in [running + wb, running + wb + 256): five payload words
+            // (from LDS, or wave-uniform scalar loads for payloads too long for it)
+            const uint32_t w0 = __builtin_amdgcn_readfirstlane((running + wb) >> 6);
+            u64 pwd[5];
+            if (!PAY_LDS) {
+#pragma unroll
+                for (int i = 0; i < 5; ++i) pwd[i] = (w0 + (uint32_t)i < (uint32_t)pw) ? payload[w0 + i] : 0ull;
+            }
+            uint32_t r = running + ex, nib = 0;
+            if (ok) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (r >= L) break;                    // past `end` (ranks only grow)
+                    const uint32_t bit = 1u << q;
+                    touched = true;
+                    if (!(safem & bit)) { nib |= bit; ++unsafe_n; continue; }
+                    const int x = (int)get_px(v1, 2 * q + 1);
+                    int nv;
+                    if (esm & bit) {
+                        const int p = med3((int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1), (int)get_px(v0, 2 * q));
+                        const uint32_t wi = (r >> 6) - w0;                 // 0..4
+                        const u64 wd = PAY_LDS ? pay[r >> 6]
+                                               : (wi == 0 ? pwd[0] : wi == 1 ? pwd[1] : wi == 2 ? pwd[2] : wi == 3 ? pwd[3] : pwd[4]);
+                        nv = p + 2 * (x - p) + (int)((wd >> (r & 63u)) & 1ull);
+                        if (r == L - 1) s_end = (int)(4 * it) + q;
+                        ++r;
+                    } else {
+                        nv = (rightm & bit) ? x + Tthr : x - Tthr;
+                    }
+                    set_px(v1, 2 * q + 1, (uint32_t)nv);
+                }
+            }
+            // location-map word (4 it) / 64 = 16 lanes x 4 candidate bits, OR-ed over the 16
+            wm = (u64)nib << (4 * (lane & 15));
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) wm |= __shfl_xor(wm, o, 64);
+            running += tot;
+            if (running >= L) live = false;
+        } else {
+            rest += n;   // past `end` (out of place): counted for the exact capacity only
+        }
+        // stores, unconditional (the 16 lanes of a map word store the same value)
+        const uint32_t wix = (4 * it) >> 6;
+        *(ok && (int)wix < lmw ? lm + wix : sink_w) = wm;
+        if (INPLACE) {
+            stv<NT>(ok && touched ? reinterpret_cast<V*>(dst + o0 + W) : sink_v, v1);
+        } else {
+            stv<NT>(ok ? reinterpret_cast<V*>(dst + o0) : sink_v, v0);
+            stv<NT>(ok ? reinterpret_cast<V*>(dst + o0 + W) : sink_v + 1, v1);
+        }
+        ss_load<T, NT>(src, W, CR, items, min(k + D, nchunks - 1), v0, v1);
+    };
+
+    const int nfull = nchunks / D * D;
+    for (int k0 = 0; k0 < nfull; k0 += D) {   // full groups: no guard around any chunk
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            if (INPLACE && !live) break;         // leaves the loop (no join back into it)
+            chunk(d, k0 + d);
+        }
+        if (INPLACE && !live) break;
+    }
+    if (!INPLACE || live) {
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+            if (nfull + d < nchunks && (!INPLACE || live)) chunk(d, nfull + d);
+    }
+    // lm_count and the capacity past `end`: one block reduction
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        unsafe_n += __shfl_xor(unsafe_n, o, 64);
+        rest += __shfl_xor(rest, o, 64);
+    }
+    if (lane == 0) { red[0][wv] = unsafe_n; red[1][wv] = rest; }
+    lds_barrier();
+    if (tid == 0) {
+        uint32_t un = 0, re = 0;
+        for (int w = 0; w < 16; ++w) { un += red[0][w]; re += red[1][w]; }
+        codec_pee_meta* M = meta_all + b;
+        const uint32_t cap = running + re;
+        M->T = Tthr; M->maxval = maxval; M->L = (int)L; M->nc = nc; M->ntiles = ntiles; M->h = H; M->w = W;
+        M->lm_count = (int)un;
+        M->capacity = (int)cap;
+        // in place the count stops with the chunk holding `end`: a lower bound unless it was the last
+        M->flags = (INPLACE && last < nchunks - 1) ? CODEC_PEE_PARTIAL : 0;
+        M->reserved[0] = M->reserved[1] = M->reserved[2] = 0;
+        if (L == 0) { M->end = -1; M->tile_end = -1; M->status = 0; }
+        else if (running < L) { M->end = nc - 1; M->tile_end = ntiles - 1; M->status = 1; }   // truncated
+        else { M->end = s_end; M->tile_end = s_end / PEE_TILE; M->status = 0; }
+    }
+}
+
+template <typename T, bool NT, bool INPLACE, int D>
+__global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restrict__ stego, T* cover, int H, int W,
+                                                               const codec_pee_meta* __restrict__ meta_all,
+                                                               const u64* __restrict__ lm_all, int lmw,
+                                                               u64* __restrict__ payload_all, int pw,
+                                                               uint32_t* __restrict__ lb_flag, char* __restrict__ sink) {
+    typedef typename Vec8<T>::type V;
+    __shared__ uint32_t ss_pad[SS_PAD_WORDS];
+    __shared__ uint32_t wtot[2][16];
+    __shared__ u64 pbuf[2][SS_THREADS * 4 / 64 + 2];
+    __shared__ u64 s_carry[2];
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int CR = W / 8;
+    const uint32_t items = (uint32_t)(H / 2) * (uint32_t)CR;
+    const int nchunks = (int)((items + SS_THREADS - 1) / SS_THREADS);
+    const codec_pee_meta* M = meta_all + b;
+    const int end = M->end, Tthr = M->T;
+    const int cend = end >= 0 ? (end >> 2) / SS_THREADS : -1;
+    const int nproc = INPLACE ? cend + 1 : nchunks;
+    const int klast = max(nproc, 1) - 1;
+    const size_t npx = (size_t)H * W;
+    const T* src = stego + b * npx;
+    T* dst = cover + b * npx;
+    const u64* lm = lm_all + (size_t)b * lmw;
+    u64* payload = payload_all + (size_t)b * pw;
+    V* sink_v = reinterpret_cast<V*>(sink + (size_t)tid * 48);
+    u64* sink_w = reinterpret_cast<u64*>(sink + (size_t)tid * 48 + 32);
+    if (tid == 0) {
+        s_carry[0] = s_carry[1] = 0ull;
+        ss_pad[SS_PAD_WORDS - 1] = 0u;
+        if (b == 0) *lb_flag = 0u;   // codec_pee_extract_flag_offset: no look-back here, never set
+    }
+    if (tid < SS_THREADS * 4 / 64 + 2) pbuf[0][tid] = pbuf[1][tid] = 0ull;
+    V r0[D], r1[D];
+    u64 rl[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        ss_load<T, NT>(src, W, CR, items, min(d, klast), r0[d], r1[d]);
+        rl[d] = lm[(4 * min((uint32_t)min(d, klast) * SS_THREADS + tid, items - 1u)) >> 6];
+    }
+    uint32_t running = 0;
+    int par = 0;
+    // The payload words of chunk j are written during chunk j+1, after its scan barrier (one
+    // barrier per chunk): pending = chunk j's word range.  Chunk j's first word continues the
+    // previous partial word (s_carry[(j-1)&1]); a partial last word goes to s_carry[j&1].
+    bool pend = false;
+    uint32_t p_lo = 0, p_hi = 0;
+    int p_par = 0;
+
+    // words of the pending chunk for thread tid: (value, absolute index, store it?)
+    auto emit = [&](u64* wout, uint32_t* wabs, bool* wstore) {
+        const int nw = (int)(((p_lo & 63u) + (p_hi - p_lo) + 63u) >> 6);
+        if (tid < nw) {
+            const uint32_t a = (p_lo >> 6) + (uint32_t)tid;
+            const u64 wv = pbuf[p_par][tid] | (tid == 0 ? s_carry[p_par ^ 1] : 0ull);
+            if ((a + 1u) * 64u <= p_hi) { *wout = wv; *wabs = a; *wstore = (int)a < pw; }
+            else s_carry[p_par] = wv;
+        }
+        if (tid == 0 && (p_hi & 63u) == 0u) s_carry[p_par] = 0ull;
+    };
+
+    auto chunk = [&](int d, int k) {
+        V& v0 = r0[d];
+        V& v1 = r1[d];
+        const u64 lw = rl[d];
+        const uint32_t it = (uint32_t)k * SS_THREADS + tid;
+        const bool ok = it < items;
+        const uint32_t rr = it / (uint32_t)CR, cc = it - rr * (uint32_t)CR;
+        const size_t o0 = (size_t)(2 * rr) * W + (size_t)cc * 8;
+        // classification on every lane (unconditional first use of the ring registers)
+        uint32_t actm = 0, innm = 0;
+        const u64 l4 = lw >> ((4 * it) & 63u);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int kq = (int)(4 * it) + q;
+            const bool act = ok && k <= cend && kq <= end && !((l4 >> q) & 1ull);
+            const int p = med3((int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1), (int)get_px(v0, 2 * q));
+            const int e2 = (int)get_px(v1, 2 * q + 1) - p;
+            actm |= act ? 1u << q : 0u;
+            innm |= (act && e2 >= -2 * Tthr && e2 < 2 * Tthr) ? 1u << q : 0u;
+        }
+        u64 wout = 0;
+        bool wstore = false;
+        uint32_t wabs = 0;
+        if (k <= cend) {   // uniform; no vector memory instruction inside
+            const uint32_t n = (uint32_t)__popc(innm);
+            // pbuf[par] was last read (and re-zeroed below) by these same threads two chunks ago
+            uint32_t ex, tot, wb;
+            ss_scan(n, wtot, par, &ex, &tot, &wb);
+            if (pend) emit(&wout, &wabs, &wstore);          // the previous chunk's words
+            if (tid < SS_THREADS * 4 / 64 + 2 && pend) pbuf[p_par][tid] = 0ull;
+            const uint32_t w0 = running >> 6;
+            uint32_t r = running + ex;
+            u64 word = 0;
+            int wi = -1;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (!((actm >> q) & 1u)) continue;
+                const int x = (int)get_px(v1, 2 * q + 1);
+                const int p = med3((int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1), (int)get_px(v0, 2 * q));
+                const int e2 = x - p;
+                int nx;
+                if ((innm >> q) & 1u) {
+                    if (e2 & 1) {
+                        if (wi != (int)(r >> 6)) {
+                            if (wi >= 0) atomicOr(&pbuf[par][wi - (int)w0], word);
+                            wi = (int)(r >> 6);
+                            word = 0;
+                        }
+                        word |= 1ull << (r & 63u);
+                    }
+                    ++r;
+                    nx = p + (e2 >> 1);
+                } else {
+                    nx = e2 >= 2 * Tthr ? x - Tthr : x + Tthr;
+                }
+                set_px(v1, 2 * q + 1, (uint32_t)nx);
+            }
+            if (wi >= 0 && word) atomicOr(&pbuf[par][wi - (int)w0], word);
+            pend = true;
+            p_lo = running;
+            p_hi = running + tot;
+            p_par = par;
+            par ^= 1;
+            running += tot;
+        }
+        // stores, unconditional (redirected to the sink when they must not land)
+        *(wstore ? payload + wabs : sink_w) = wout;
+        if (INPLACE) {
+            stv<NT>(ok && actm ? reinterpret_cast<V*>(dst + o0 + W) : sink_v, v1);
+        } else {
+            stv<NT>(ok ? reinterpret_cast<V*>(dst + o0) : sink_v, v0);
+            stv<NT>(ok ? reinterpret_cast<V*>(dst + o0 + W) : sink_v + 1, v1);
+        }
+        const int kn = min(k + D, klast);
+        ss_load<T, NT>(src, W, CR, items, kn, v0, v1);
+        rl[d] = lm[(4 * min((uint32_t)kn * SS_THREADS + tid, items - 1u)) >> 6];
+    };
+
+    const int nfull = nproc / D * D;
+    for (int k0 = 0; k0 < nfull; k0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) chunk(d, k0 + d);
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+        if (nfull + d < nproc) chunk(d, nfull + d);
+    // the last chunk's words, its partial last word, then zeros to the end of the payload row
+    lds_barrier();
+    if (pend) {
+        u64 wout = 0;
+        bool wstore = false;
+        uint32_t wabs = 0;
+        emit(&wout, &wabs, &wstore);
+        if (wstore) payload[wabs] = wout;
+        lds_barrier();
+        if (tid == 0 && (running & 63u) && (int)(running >> 6) < pw) payload[running >> 6] = s_carry[p_par];
+    }
+    const uint32_t full = (running + 63u) >> 6;
+    for (uint32_t w = full + tid; w < (uint32_t)pw; w += SS_THREADS) payload[w] = 0ull;
+}
+
 // ====================================================================== host side
 struct PeeWs {
-    size_t cnt, off, st, ctl, diag, hist, total;
+    size_t cnt, off, st, ctl, diag, hist, sink, total;
     int ntiles_max, nchunks;
 };
 
@@ -1490,8 +1878,41 @@ static PeeWs pee_ws(const codec_pee_params* P) {
     L.diag = align_up(L.ctl + PEE_CTL_WORDS(P->B) * 4, 16);
     // capacity-control error histogram (codec_pee_capacity; cleared by that call)
     L.hist = align_up(L.diag + 16, 256);
-    L.total = align_up(L.hist + (size_t)P->B * 2 * PEE_TMAX_MAX * 4, 256);
+    // slice-serial kernels: per-lane sink for stores that must not land (contents unused)
+    L.sink = align_up(L.hist + (size_t)P->B * 2 * PEE_TMAX_MAX * 4, 256);
+    L.total = align_up(L.sink + SS_SINK_BYTES, 256);
     return L;
+}
+
+// slice-serial dispatch: the batch fills whole rounds of one workgroup per CU
+static int device_cu_count() {
+    static int cached[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cached[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cached[dev] = n;
+    }
+    return cached[dev];
+}
+
+// Measured at B = 256 (profiles/r02/ss_vs_lookback.json): in place the slice-serial pass
+// wins at every size (2048^2 embed 0.145 -> 0.111 ms, extract 0.115 -> 0.109); out of place
+// it streams at ~4.9 TB/s per chip, which beats the look-back pass on small slices
+// (512^2: embed 0.066 -> 0.059, extract 0.077 -> 0.069) but not on 2048^2 ones (look-back
+// 0.71-0.73 ms vs 0.88), so out of place it is used up to CODEC_PEE_SS_OOP_MAXCH chunks.
+static bool pee_use_slice_serial(const codec_pee_params* P, bool inplace) {
+    const long long k = knob("CODEC_PEE_SS", -1);
+    if (k == 0) return false;
+    if (k == 1) return true;
+    const long long ncu = device_cu_count();
+    if (P->B < ncu) return false;
+    const long long rounds = (P->B + ncu - 1) / ncu;
+    if ((double)P->B / (double)(rounds * ncu) < 0.85) return false;   // the last round nearly full
+    if (inplace) return true;
+    const long long items = (long long)(P->H / 2) * (P->W / 8);
+    return (items + SS_THREADS - 1) / SS_THREADS <= knob("CODEC_PEE_SS_OOP_MAXCH", 64);
 }
 
 static int pee_check(const codec_pee_params* P) {
@@ -1616,6 +2037,28 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
     // look-back progressing, as in the lane order; 256 tickets on one line cost 8 us at B=1).
     const long long onepass = knob("CODEC_PEE_ONEPASS", -1);
     const bool flat = !inplace && P->B < 32 && P->B <= knob("CODEC_PEE_FLAT_MAXB", 7);
+    if (vec && items > 0 && onepass != 0 && pee_use_slice_serial(P, inplace)) {
+        // slice-serial single pass: one workgroup per slice, no look-back, no memsets
+        ProfScope prof(st, CODEC_K_PEE_EMBED1);
+        const bool pay_lds = P->payload_words <= SS_PAY_WORDS && knob("CODEC_PEE_SS_PAYLDS", 1) != 0;
+#define PES1(TT, NTV, IP, PL) hipLaunchKernelGGL((k_pee_embed_ss<TT, NTV, IP, 4, PL>), dim3((unsigned)P->B), dim3(SS_THREADS), 0, st, \
+            static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, tps, \
+            reinterpret_cast<const u64*>(payload), P->payload_words, meta, reinterpret_cast<u64*>(lm), P->lm_words, \
+            static_cast<char*>(workspace) + L.sink)
+#define PES(TT, NTV, IP) do { if (pay_lds) PES1(TT, NTV, IP, true); else PES1(TT, NTV, IP, false); } while (0)
+        if (P->bytes == 2) {
+            if (inplace) { if (nt) PES(uint16_t, true, true); else PES(uint16_t, false, true); }
+            else { if (nt) PES(uint16_t, true, false); else PES(uint16_t, false, false); }
+        } else {
+            if (inplace) { if (nt) PES(uint8_t, true, true); else PES(uint8_t, false, true); }
+            else { if (nt) PES(uint8_t, true, false); else PES(uint8_t, false, false); }
+        }
+#undef PES
+#undef PES1
+        LAUNCH_CHECK("k_pee_embed_ss");
+        if ((P->H & 1) && !inplace) HIP_TRY(pee_copy_last_rows(P, cover, stego, st));
+        return 0;
+    }
     if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && onepass != 0) {
         u64* stw = reinterpret_cast<u64*>(static_cast<char*>(workspace) + L.st);
         uint32_t* ctl = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.ctl);
@@ -1733,10 +2176,29 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
     const bool nt = knob("CODEC_NT", 1) != 0;
     const size_t va = P->bytes == 2 ? 16 : 8;
     const bool vec = (P->W % 8) == 0 && ((uintptr_t)stego % va) == 0 && ((uintptr_t)cover_out % va) == 0;
-    HIP_TRY(hipMemsetAsync(payload_out, 0, (size_t)P->B * P->payload_words * 8, st));
     const long long items = (long long)(P->H / 2) * (P->W / 8);
     const bool inplace = stego == cover_out;
     const long long onepass = knob("CODEC_PEE_ONEPASS", -1);   // as in codec_pee_embed
+    if (vec && items > 0 && onepass != 0 && pee_use_slice_serial(P, inplace)) {
+        // slice-serial: writes every payload word itself (no memset) and never sets the flag
+        uint32_t* ctl = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.ctl);
+        ProfScope prof(st, CODEC_K_PEE_EXTRACT1);
+#define PXS(TT, NTV, IP) hipLaunchKernelGGL((k_pee_extract_ss<TT, NTV, IP, 4>), dim3((unsigned)P->B), dim3(SS_THREADS), 0, st, \
+            static_cast<const TT*>(stego), static_cast<TT*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm), \
+            P->lm_words, reinterpret_cast<u64*>(payload_out), P->payload_words, ctl + 1, static_cast<char*>(workspace) + L.sink)
+        if (P->bytes == 2) {
+            if (inplace) { if (nt) PXS(uint16_t, true, true); else PXS(uint16_t, false, true); }
+            else { if (nt) PXS(uint16_t, true, false); else PXS(uint16_t, false, false); }
+        } else {
+            if (inplace) { if (nt) PXS(uint8_t, true, true); else PXS(uint8_t, false, true); }
+            else { if (nt) PXS(uint8_t, true, false); else PXS(uint8_t, false, false); }
+        }
+#undef PXS
+        LAUNCH_CHECK("k_pee_extract_ss");
+        if ((P->H & 1) && !inplace) HIP_TRY(pee_copy_last_rows(P, stego, cover_out, st));
+        return 0;
+    }
+    HIP_TRY(hipMemsetAsync(payload_out, 0, (size_t)P->B * P->payload_words * 8, st));
     const bool flat = !inplace && P->B < 32 && P->B <= knob("CODEC_PEE_FLAT_MAXB", 7);
     if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && onepass != 0) {
         u64* stw = reinterpret_cast<u64*>(static_cast<char*>(workspace) + L.st);

@@ -93,8 +93,11 @@ def test_c3_lsb_256x512():
     _lsb_batch_check(covers, msgs, sample=range(0, B, 16))
 
 
-def test_c3_pee_256x512():
+@pytest.mark.parametrize("ss", ["auto", "0"])
+def test_c3_pee_256x512(ss, monkeypatch):
     """1 KB per 512^2 ct12 slice needs T ~ 4-5 (T = 2 holds ~4.4 kbit): capacity control."""
+    if ss != "auto":
+        monkeypatch.setenv("CODEC_PEE_SS", ss)
     _pee_batch_check(_batch(256, 512, 512, seed=2000), sample=range(3, 256, 16), T="auto")
 
 
@@ -115,5 +118,10 @@ def test_headline_lsb_256x2048_with_kats():
     _lsb_batch_check(covers, msgs, sample=(0, 85, 170, 255), kats=kats)
 
 
-def test_headline_pee_256x2048():
+@pytest.mark.parametrize("ss", ["auto", "0"])
+def test_headline_pee_256x2048(ss, monkeypatch):
+    """Default launch at this shape: the slice-serial single pass (one workgroup per slice);
+    "0": the look-back single pass (chunk-parallel) on the same batch."""
+    if ss != "auto":
+        monkeypatch.setenv("CODEC_PEE_SS", ss)
     _pee_batch_check(_batch(256, 2048, 2048, seed=11), sample=(0, 101, 255))

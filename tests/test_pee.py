@@ -71,7 +71,10 @@ PATHS = {"auto": {}, "onepass": {"CODEC_PEE_ONEPASS": "1"}, "twopass": {"CODEC_P
          # decode-side tile counts: workgroup-per-tile (block sums) instead of wave-per-tile,
          # and wave-per-tile with one workgroup per slice (every wave strides over tiles)
          "twopass_block_tiles": {"CODEC_PEE_ONEPASS": "0", "CODEC_PEE_WAVE_TILES": "0", "CODEC_PEE_EMBED_V": "0"},
-         "twopass_wave_tiles_1wg": {"CODEC_PEE_ONEPASS": "0", "CODEC_PEE_DCOUNT_W_WGS": "1"}}
+         "twopass_wave_tiles_1wg": {"CODEC_PEE_ONEPASS": "0", "CODEC_PEE_DCOUNT_W_WGS": "1"},
+         # slice-serial single pass (the default for batches of >= one slice per CU), forced
+         # on these small batches
+         "slice_serial": {"CODEC_PEE_SS": "1"}}
 
 
 @pytest.fixture(params=sorted(PATHS))
