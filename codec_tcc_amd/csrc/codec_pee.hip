@@ -21,21 +21,26 @@ struct PeeCand {
     bool expand, right, safe;
 };
 
+// LOCO-I MED predictor (oracle/pee_cpu.py med): min(a,b) if c >= max(a,b), max(a,b) if
+// c <= min(a,b), else a+b-c -- which is exactly median(a, b, a+b-c) (each case puts a+b-c on
+// the far side of the returned value), one v_med3_i32 after an add and a subtract
 __device__ __forceinline__ int med3(int a, int b, int c) {
-    const int lo = min(a, b), hi = max(a, b);
-    return c >= hi ? lo : (c <= lo ? hi : a + b - c);
+    return max(min(a, b), min(max(a, b), a + b - c));
 }
 
+// branch-free classification: -T <= e < T as one unsigned compare; the expansion target
+// y = p + 2e (+ bit) must stay in [0, maxval], i.e. (unsigned)y < maxval
 __device__ __forceinline__ PeeCand pee_classify(int x, int a, int b, int c, int T, int maxval) {
     PeeCand r;
     r.x = x;
     r.p = med3(a, b, c);
     const int e = x - r.p;
-    r.expand = (e >= -T) && (e < T);
+    r.expand = (unsigned)(e + T) < (unsigned)(2 * T);
     r.right = e >= T;
-    if (r.expand) r.safe = (r.p + 2 * e >= 0) && (r.p + 2 * e + 1 <= maxval);
-    else if (r.right) r.safe = x + T <= maxval;
-    else r.safe = x - T >= 0;
+    const int y = r.p + 2 * e;
+    // non-short-circuit (&, |): a ?: chain here was compiled into divergent branches
+    const bool ok_e = (unsigned)y < (unsigned)maxval, ok_r = x <= maxval - T, ok_l = x >= T;
+    r.safe = (r.expand & ok_e) | (!r.expand & r.right & ok_r) | (!r.expand & !r.right & ok_l);
     return r;
 }
 
@@ -1488,6 +1493,21 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
 // only branches left in the ring loop contain no vector memory instruction.  Barriers are
 // LDS-only (raw s_barrier): __syncthreads()'s fence waits vmcnt(0).
 #define SS_THREADS 1024
+// diagnostic build only (tools/ss_trace.py, -DPEE_SS_TRACE): workgroup 0, wave 0 stamps the
+// chunk phases into LDS (no vector memory in the loop) and writes them out at the end
+#ifdef PEE_SS_TRACE
+#define SS_TRACE_N 2048
+__device__ unsigned long long g_ss_trace[SS_TRACE_N];
+// slot i of wave w: ss_trace[w * 128 + i] (chunks < 32 traced)
+#define SS_STAMP(i)                                                                           \
+    do {                                                                                      \
+        unsigned long long t_;                                                                \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
+        if ((threadIdx.x & 63) == 0 && (i) < 128) ss_trace[(threadIdx.x >> 6) * 128 + (i)] = t_; \
+    } while (0)
+#else
+#define SS_STAMP(i) do { } while (0)
+#endif
 #define SS_PAD_WORDS (21 * 1024)     // 84 KB of the CU's 160 KB: a second workgroup does not fit
 #define SS_PAY_WORDS (SS_PAD_WORDS / 2 - 1)   // the embed keeps payloads of up to 10 751 words in that pad
 #define SS_SINK_BYTES (SS_THREADS * 48)   // per lane: two 16-B pixel vectors + one 8-B word (+pad)
@@ -1498,13 +1518,72 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("" ::: "memory");
 }
 
+// wave-level primitives without LDS round trips (each __shfl is a ds_bpermute, ~100 cycles):
+// OR over the 16 lanes of a DPP row, and an exclusive scan of 0..7 per lane from three ballots
+__device__ __forceinline__ uint32_t row_or16(uint32_t v) {
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);   // row_half_mirror
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);   // row_mirror
+    return v;
+}
+__device__ __forceinline__ u64 row_or16_64(u64 v) {
+    return (u64)row_or16((uint32_t)v) | ((u64)row_or16((uint32_t)(v >> 32)) << 32);
+}
+__device__ __forceinline__ uint32_t mbcnt64(u64 m) {   // set bits of m below this lane
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+// n in 0..7 per lane -> exclusive prefix within the wave, and the wave's total
+__device__ __forceinline__ uint32_t wave_excl_small(uint32_t n, uint32_t* total) {
+    const u64 b0 = __ballot(n & 1u), b1 = __ballot(n & 2u), b2 = __ballot(n & 4u);
+    *total = (uint32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
+    return mbcnt64(b0) + 2u * mbcnt64(b1) + 4u * mbcnt64(b2);
+}
+
+// exclusive scan of n (0..7) over the 1024 threads with ONE barrier and no shuffles: ballot
+// scans inside the waves, wave totals through LDS (double-buffered by parity: a wave cannot
+// rewrite wtot[par] before every wave has passed the next barrier)
+__device__ __forceinline__ void ss_scan_small(uint32_t n, uint32_t (*wtot)[16], int par, uint32_t* excl, uint32_t* tot,
+                                              uint32_t* wbase) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t wt;
+    const uint32_t ex = wave_excl_small(n, &wt);
+    if (lane == 0) wtot[par][wv] = wt;
+    lds_barrier();
+    uint32_t wb = 0, t = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+        const uint32_t v = wtot[par][w];
+        t += v;
+        wb += w < wv ? v : 0u;
+    }
+    *excl = wb + ex;
+    *tot = t;
+    *wbase = wb;
+}
+
+// item -> element offset of its 8-pixel column chunk in the top row of its row pair, advanced
+// chunk by chunk without divisions: item + 1024 moves (row pair, column chunk) by
+// (1024 / CR, 1024 % CR) with at most one carry.  Lanes/chunks past the end load a clamped
+// valid address (data unused): straight-line loads let hipcc count vmcnt exactly.
+struct SsCursor {
+    uint32_t rr, cc;
+    __device__ __forceinline__ void init(uint32_t it, uint32_t CR) {
+        rr = it / CR;
+        cc = it - rr * CR;
+    }
+    __device__ __forceinline__ void step(uint32_t dq, uint32_t dr, uint32_t CR) {
+        cc += dr;
+        rr += dq;
+        if (cc >= CR) { cc -= CR; ++rr; }
+    }
+    __device__ __forceinline__ uint32_t off(uint32_t W) const { return 2u * rr * W + 8u * cc; }
+};
+
 template <typename T, bool NT>
-__device__ __forceinline__ void ss_load(const T* src, int W, int CR, uint32_t items, int k,
-                                        typename Vec8<T>::type& x0, typename Vec8<T>::type& x1) {
+__device__ __forceinline__ void ss_load_at(const T* src, uint32_t W, uint32_t o0, typename Vec8<T>::type& x0,
+                                           typename Vec8<T>::type& x1) {
     typedef typename Vec8<T>::type V;
-    const uint32_t it = min((uint32_t)k * SS_THREADS + threadIdx.x, items - 1u);
-    const uint32_t r = it / (uint32_t)CR, cc = it - r * (uint32_t)CR;
-    const size_t o0 = (size_t)(2 * r) * W + (size_t)cc * 8;
     x0 = ldv<NT>(reinterpret_cast<const V*>(src + o0));
     x1 = ldv<NT>(reinterpret_cast<const V*>(src + o0 + W));
 }
@@ -1541,6 +1620,9 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
     __shared__ uint32_t wtot[2][16];
     __shared__ uint32_t red[2][16];
     __shared__ int s_end;
+#ifdef PEE_SS_TRACE
+    __shared__ unsigned long long ss_trace[SS_TRACE_N];
+#endif
     const int b = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int CR = W / 8;
@@ -1563,8 +1645,24 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
         ss_pad[SS_PAD_WORDS - 1] = 0u;   // the occupancy pad stays allocated
     }
     V r0[D], r1[D];
+    // cursors of this lane's item in the current chunk and in the chunk D ahead (the refill)
+    const uint32_t dq = SS_THREADS / (uint32_t)CR, dr = SS_THREADS % (uint32_t)CR;
+    uint32_t off_last;
+    {
+        SsCursor l;
+        l.init(items - 1u, (uint32_t)CR);
+        off_last = l.off((uint32_t)W);
+    }
+    SsCursor cur, ahead;
+    cur.init((uint32_t)tid, (uint32_t)CR);
+    ahead = cur;
+    uint32_t it_a = (uint32_t)tid;
 #pragma unroll
-    for (int d = 0; d < D; ++d) ss_load<T, NT>(src, W, CR, items, min(d, nchunks - 1), r0[d], r1[d]);
+    for (int d = 0; d < D; ++d) {
+        ss_load_at<T, NT>(src, (uint32_t)W, it_a < items ? ahead.off((uint32_t)W) : off_last, r0[d], r1[d]);
+        ahead.step(dq, dr, (uint32_t)CR);
+        it_a += SS_THREADS;
+    }
     if (PAY_LDS) {   // the payload in LDS once: no dependent global round trip per chunk
         const int nw = min(pw, (int)((L + 63u) >> 6));
         for (int w = tid; w < nw; w += SS_THREADS) pay[w] = payload[w];
@@ -1580,63 +1678,72 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
         V& v1 = r1[d];
         const uint32_t it = (uint32_t)k * SS_THREADS + tid;
         const bool ok = it < items;
-        const uint32_t rr = it / (uint32_t)CR, cc = it - rr * (uint32_t)CR;
-        const size_t o0 = (size_t)(2 * rr) * W + (size_t)cc * 8;
+        const uint32_t o0 = cur.off((uint32_t)W);
+        SS_STAMP(4 * k);
         // classification on every lane: the first use of the ring registers is unconditional
         uint32_t esm = 0, safem = 0, rightm = 0;
+        int pq[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const PeeCand pc = pee_classify((int)get_px(v1, 2 * q + 1), (int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1),
                                             (int)get_px(v0, 2 * q), Tthr, maxval);
+            pq[q] = pc.p;
             safem |= pc.safe ? 1u << q : 0u;
             rightm |= pc.right ? 1u << q : 0u;
             esm |= (pc.expand && pc.safe) ? 1u << q : 0u;
         }
         if (!ok) esm = 0u;
         const uint32_t n = (uint32_t)__popc(esm);
+        SS_STAMP(4 * k + 1);
         u64 wm = 0;
         bool touched = false;
         if (live) {   // uniform; no vector memory instruction inside
             last = k;
             uint32_t ex, tot, wb;
-            ss_scan(n, wtot, par, &ex, &tot, &wb);
+            ss_scan_small(n, wtot, par, &ex, &tot, &wb);
+            SS_STAMP(4 * k + 2);
             par ^= 1;
-            // the wave's ranks lie in [running + wb, running + wb + 256): five payload words
-            // (from LDS, or wave-uniform scalar loads for payloads too long for it)
-            const uint32_t w0 = __builtin_amdgcn_readfirstlane((running + wb) >> 6);
-            u64 pwd[5];
-            if (!PAY_LDS) {
+            // this lane's expandable candidates take ranks [rs, rs + n): their payload bits
+            // are one <= 4-bit field of at most two consecutive payload words
+            const uint32_t rs = running + ex;
+            u64 field;
+            if (PAY_LDS) {
+                const uint32_t w = min(rs >> 6, (uint32_t)SS_PAY_WORDS - 2u), sh = rs & 63u;
+                const u64 lo = pay[w], hi = pay[w + 1];
+                field = (lo >> sh) | ((hi << ((64u - sh) & 63u)) & (sh ? ~0ull : 0ull));
+            } else {
+                // wave-uniform scalar loads: the wave's ranks lie in [running + wb, +256)
+                const uint32_t w0 = __builtin_amdgcn_readfirstlane((running + wb) >> 6);
+                u64 pwd[6];
 #pragma unroll
-                for (int i = 0; i < 5; ++i) pwd[i] = (w0 + (uint32_t)i < (uint32_t)pw) ? payload[w0 + i] : 0ull;
+                for (int i = 0; i < 6; ++i) pwd[i] = (w0 + (uint32_t)i < (uint32_t)pw) ? payload[w0 + i] : 0ull;
+                const uint32_t wi = (rs >> 6) - w0, sh = rs & 63u;       // 0..4
+                const u64 lo = wi == 0 ? pwd[0] : wi == 1 ? pwd[1] : wi == 2 ? pwd[2] : wi == 3 ? pwd[3] : pwd[4];
+                const u64 hi = wi == 0 ? pwd[1] : wi == 1 ? pwd[2] : wi == 2 ? pwd[3] : wi == 3 ? pwd[4] : pwd[5];
+                field = sh ? (lo >> sh) | (hi << (64u - sh)) : lo;
             }
-            uint32_t r = running + ex, nib = 0;
-            if (ok) {
+            uint32_t nib = 0;
+            int eidx = -1;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    if (r >= L) break;                    // past `end` (ranks only grow)
-                    const uint32_t bit = 1u << q;
-                    touched = true;
-                    if (!(safem & bit)) { nib |= bit; ++unsafe_n; continue; }
-                    const int x = (int)get_px(v1, 2 * q + 1);
-                    int nv;
-                    if (esm & bit) {
-                        const int p = med3((int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1), (int)get_px(v0, 2 * q));
-                        const uint32_t wi = (r >> 6) - w0;                 // 0..4
-                        const u64 wd = PAY_LDS ? pay[r >> 6]
-                                               : (wi == 0 ? pwd[0] : wi == 1 ? pwd[1] : wi == 2 ? pwd[2] : wi == 3 ? pwd[3] : pwd[4]);
-                        nv = p + 2 * (x - p) + (int)((wd >> (r & 63u)) & 1ull);
-                        if (r == L - 1) s_end = (int)(4 * it) + q;
-                        ++r;
-                    } else {
-                        nv = (rightm & bit) ? x + Tthr : x - Tthr;
-                    }
-                    set_px(v1, 2 * q + 1, (uint32_t)nv);
-                }
+            for (int q = 0; q < 4; ++q) {   // branch-free: candidate q is processed iff rank rs+pre < L
+                const uint32_t bit = 1u << q;
+                const uint32_t pre = (uint32_t)__popc(esm & (bit - 1u));
+                const bool proc = ok & (rs + pre < L);
+                const int x = (int)get_px(v1, 2 * q + 1);
+                const int p = pq[q];
+                const int nv_e = p + 2 * (x - p) + (int)((field >> pre) & 1ull);
+                const int nv_s = (rightm & bit) ? x + Tthr : x - Tthr;
+                const bool safe = (safem & bit) != 0, expd = (esm & bit) != 0;
+                const int nv = !proc || !safe ? x : (expd ? nv_e : nv_s);
+                set_px(v1, 2 * q + 1, (uint32_t)nv);
+                nib |= (proc & !safe) ? bit : 0u;
+                touched |= proc;
+                eidx = (proc & expd & (rs + pre == L - 1)) ? (int)(4 * it) + q : eidx;
             }
-            // location-map word (4 it) / 64 = 16 lanes x 4 candidate bits, OR-ed over the 16
-            wm = (u64)nib << (4 * (lane & 15));
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) wm |= __shfl_xor(wm, o, 64);
+            if (eidx >= 0) s_end = eidx;                   // one lane of the slice, once
+            unsafe_n += (uint32_t)__popc(nib);
+            // location-map word (4 it) / 64 = 16 lanes x 4 candidate bits, OR-ed over the DPP row
+            wm = row_or16_64((u64)nib << (4 * (lane & 15)));
             running += tot;
             if (running >= L) live = false;
         } else {
@@ -1651,7 +1758,11 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
             stv<NT>(ok ? reinterpret_cast<V*>(dst + o0) : sink_v, v0);
             stv<NT>(ok ? reinterpret_cast<V*>(dst + o0 + W) : sink_v + 1, v1);
         }
-        ss_load<T, NT>(src, W, CR, items, min(k + D, nchunks - 1), v0, v1);
+        ss_load_at<T, NT>(src, (uint32_t)W, it_a < items ? ahead.off((uint32_t)W) : off_last, v0, v1);
+        cur.step(dq, dr, (uint32_t)CR);
+        ahead.step(dq, dr, (uint32_t)CR);
+        it_a += SS_THREADS;
+        SS_STAMP(4 * k + 3);
     };
 
     const int nfull = nchunks / D * D;
@@ -1676,6 +1787,10 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
     }
     if (lane == 0) { red[0][wv] = unsafe_n; red[1][wv] = rest; }
     lds_barrier();
+#ifdef PEE_SS_TRACE
+    if (b == 0)
+        for (int i = tid; i < SS_TRACE_N; i += SS_THREADS) g_ss_trace[i] = (i & 127) < 4 * (last + 1) ? ss_trace[i] : 0ull;
+#endif
     if (tid == 0) {
         uint32_t un = 0, re = 0;
         for (int w = 0; w < 16; ++w) { un += red[0][w]; re += red[1][w]; }
@@ -1729,10 +1844,26 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
     if (tid < SS_THREADS * 4 / 64 + 2) pbuf[0][tid] = pbuf[1][tid] = 0ull;
     V r0[D], r1[D];
     u64 rl[D];
+    const uint32_t dq = SS_THREADS / (uint32_t)CR, dr = SS_THREADS % (uint32_t)CR;
+    // the ring never loads past chunk klast (in place: the chunk holding `end`)
+    const uint32_t items_l = min(items, (uint32_t)(klast + 1) * SS_THREADS);
+    uint32_t off_last;
+    {
+        SsCursor l;
+        l.init(items_l - 1u, (uint32_t)CR);
+        off_last = l.off((uint32_t)W);
+    }
+    SsCursor cur, ahead;
+    cur.init((uint32_t)tid, (uint32_t)CR);
+    ahead = cur;
+    uint32_t it_a = (uint32_t)tid;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-        ss_load<T, NT>(src, W, CR, items, min(d, klast), r0[d], r1[d]);
-        rl[d] = lm[(4 * min((uint32_t)min(d, klast) * SS_THREADS + tid, items - 1u)) >> 6];
+        const bool in = it_a < items_l;
+        ss_load_at<T, NT>(src, (uint32_t)W, in ? ahead.off((uint32_t)W) : off_last, r0[d], r1[d]);
+        rl[d] = lm[(4 * (in ? it_a : items_l - 1u)) >> 6];
+        ahead.step(dq, dr, (uint32_t)CR);
+        it_a += SS_THREADS;
     }
     uint32_t running = 0;
     int par = 0;
@@ -1761,19 +1892,20 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
         const u64 lw = rl[d];
         const uint32_t it = (uint32_t)k * SS_THREADS + tid;
         const bool ok = it < items;
-        const uint32_t rr = it / (uint32_t)CR, cc = it - rr * (uint32_t)CR;
-        const size_t o0 = (size_t)(2 * rr) * W + (size_t)cc * 8;
+        const uint32_t o0 = cur.off((uint32_t)W);
         // classification on every lane (unconditional first use of the ring registers)
         uint32_t actm = 0, innm = 0;
+        int pq[4];
         const u64 l4 = lw >> ((4 * it) & 63u);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int kq = (int)(4 * it) + q;
-            const bool act = ok && k <= cend && kq <= end && !((l4 >> q) & 1ull);
+            const bool act = ok & (k <= cend) & (kq <= end) & !((l4 >> q) & 1ull);   // & : no branches
             const int p = med3((int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1), (int)get_px(v0, 2 * q));
             const int e2 = (int)get_px(v1, 2 * q + 1) - p;
+            pq[q] = p;
             actm |= act ? 1u << q : 0u;
-            innm |= (act && e2 >= -2 * Tthr && e2 < 2 * Tthr) ? 1u << q : 0u;
+            innm |= (act & ((unsigned)(e2 + 2 * Tthr) < (unsigned)(4 * Tthr))) ? 1u << q : 0u;
         }
         u64 wout = 0;
         bool wstore = false;
@@ -1782,37 +1914,30 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
             const uint32_t n = (uint32_t)__popc(innm);
             // pbuf[par] was last read (and re-zeroed below) by these same threads two chunks ago
             uint32_t ex, tot, wb;
-            ss_scan(n, wtot, par, &ex, &tot, &wb);
+            ss_scan_small(n, wtot, par, &ex, &tot, &wb);
             if (pend) emit(&wout, &wabs, &wstore);          // the previous chunk's words
             if (tid < SS_THREADS * 4 / 64 + 2 && pend) pbuf[p_par][tid] = 0ull;
-            const uint32_t w0 = running >> 6;
-            uint32_t r = running + ex;
-            u64 word = 0;
-            int wi = -1;
+            // this lane's inner candidates take ranks [rs, rs + n): their bits form one <= 4-bit
+            // field, OR-ed into at most two words of the chunk's LDS buffer
+            const uint32_t rs = running + ex;
+            u64 field = 0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (!((actm >> q) & 1u)) continue;
+            for (int q = 0; q < 4; ++q) {   // branch-free
+                const uint32_t bit = 1u << q;
                 const int x = (int)get_px(v1, 2 * q + 1);
-                const int p = med3((int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1), (int)get_px(v0, 2 * q));
+                const int p = pq[q];
                 const int e2 = x - p;
-                int nx;
-                if ((innm >> q) & 1u) {
-                    if (e2 & 1) {
-                        if (wi != (int)(r >> 6)) {
-                            if (wi >= 0) atomicOr(&pbuf[par][wi - (int)w0], word);
-                            wi = (int)(r >> 6);
-                            word = 0;
-                        }
-                        word |= 1ull << (r & 63u);
-                    }
-                    ++r;
-                    nx = p + (e2 >> 1);
-                } else {
-                    nx = e2 >= 2 * Tthr ? x - Tthr : x + Tthr;
-                }
+                const bool act = (actm & bit) != 0, inner = (innm & bit) != 0;
+                field |= (u64)((uint32_t)inner & (uint32_t)e2 & 1u) << __popc(innm & (bit - 1u));
+                const int v_in = p + (e2 >> 1), v_sh = x + ((e2 >= 2 * Tthr) ? -Tthr : Tthr);
+                const int nx = act ? (inner ? v_in : v_sh) : x;
                 set_px(v1, 2 * q + 1, (uint32_t)nx);
             }
-            if (wi >= 0 && word) atomicOr(&pbuf[par][wi - (int)w0], word);
+            if (field) {
+                const uint32_t o = rs - (running & ~63u), wi = o >> 6, sh = o & 63u;
+                atomicOr(&pbuf[par][wi], field << sh);
+                if (sh && (field >> (64u - sh))) atomicOr(&pbuf[par][wi + 1], field >> (64u - sh));
+            }
             pend = true;
             p_lo = running;
             p_hi = running + tot;
@@ -1828,9 +1953,14 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
             stv<NT>(ok ? reinterpret_cast<V*>(dst + o0) : sink_v, v0);
             stv<NT>(ok ? reinterpret_cast<V*>(dst + o0 + W) : sink_v + 1, v1);
         }
-        const int kn = min(k + D, klast);
-        ss_load<T, NT>(src, W, CR, items, kn, v0, v1);
-        rl[d] = lm[(4 * min((uint32_t)kn * SS_THREADS + tid, items - 1u)) >> 6];
+        {   // refill (branch-free; past chunk klast the last item's address, data unused)
+            const bool in = it_a < items_l;
+            ss_load_at<T, NT>(src, (uint32_t)W, in ? ahead.off((uint32_t)W) : off_last, v0, v1);
+            rl[d] = lm[(4 * (in ? it_a : items_l - 1u)) >> 6];
+            cur.step(dq, dr, (uint32_t)CR);
+            ahead.step(dq, dr, (uint32_t)CR);
+            it_a += SS_THREADS;
+        }
     };
 
     const int nfull = nproc / D * D;
@@ -1947,6 +2077,13 @@ size_t codec_pee_extract_flag_offset(const codec_pee_params* P) {
     if (pee_check(P)) return 0;
     return pee_ws(P).ctl + 4;   // ctl[1]: set when an extract chunk's look-back gave up
 }
+
+#ifdef PEE_SS_TRACE
+int codec_debug_ss_trace(unsigned long long* out, int n) {   // diagnostic build only
+    if (n > SS_TRACE_N) n = SS_TRACE_N;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ss_trace), (size_t)n * 8) == hipSuccess ? n : -1;
+}
+#endif
 
 int codec_pee_capacity(const codec_pee_params* P, const void* cover, int32_t tmax, const int32_t* lengths,
                        int32_t* caps, int32_t* t_out, void* workspace, size_t workspace_bytes, void* stream) {
