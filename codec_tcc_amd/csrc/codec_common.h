@@ -123,6 +123,55 @@ __device__ u64 block_excl_scan64(u64 x, u64* sh, u64* total) {
     return r;
 }
 
+// A barrier for LDS traffic only.  __syncthreads()'s workgroup fence makes hipcc wait
+// vmcnt(0) first, i.e. for every outstanding global load AND store of the wave; kernels whose
+// workgroups exchange data only through LDS use this instead, so stores drain and loads stay
+// in flight across the barrier (cdna_hip_programming.md: raw s_barrier + lgkmcnt(0)).  The
+// asm "memory" clobbers stop the compiler moving LDS accesses across it.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// block_excl_scan64 / block_sum_u32 with LDS-only barriers (see lds_barrier)
+template <int NT>
+__device__ u64 block_excl_scan64_lds(u64 x, u64* sh, u64* total) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    u64 inc = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const u64 y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) sh[wv] = inc;
+    lds_barrier();
+    u64 base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+        const u64 v = sh[w];
+        tot += v;
+        base += w < wv ? v : 0ull;
+    }
+    *total = tot;
+    lds_barrier();   // sh is reused by the caller's next scan
+    return base + inc - x;
+}
+
+template <int NT>
+__device__ uint32_t block_sum_u32_lds(uint32_t x, uint32_t* sh) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+    if (lane == 0) sh[wv] = x;
+    lds_barrier();
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) t += sh[w];
+    lds_barrier();
+    return t;
+}
+
 template <int NT>
 __device__ uint32_t block_sum_u32(uint32_t x, uint32_t* sh) {
     uint32_t tot;

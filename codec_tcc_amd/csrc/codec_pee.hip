@@ -1097,16 +1097,19 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
         T* dst = stego + b * npx;
         V a0[4], a1[4];
         size_t o0[4];
+        // out of place the finished flag is read BEFORE the chunk's pixels are requested, so
+        // waiting for it does not wait for them too (vmcnt counts in issue order)
+        const uint32_t dn0 = !INPLACE ? ld_agent(tick + 1) : 0u;   // every lane (one request): no branch
         // out of place: the slot's own chunk j is loaded while the ticket is in flight (the
         // ticket equals j unless workgroups were dispatched out of order)
         if (!INPLACE) pee_load_chunk<T, NT>(src, W, CR, items, j, a0, a1, o0);
         if (tid == 0) {
             uint32_t cc = PEE_SKIP;
             if (!INPLACE) {
-                // the flag load goes out with the ticket (one round trip): a flag seen set was
-                // set before this ticket was drawn, so `end` lies in an earlier chunk; a flag
-                // set meanwhile but not seen only costs this chunk the full path
-                const uint32_t dn = ld_agent(tick + 1);
+                // a flag seen set was set before this chunk started, so `end` lies in an
+                // earlier chunk; a flag set meanwhile but not seen only costs this chunk the
+                // full path
+                const uint32_t dn = dn0;
                 cc = (mode & PEE_MODE_NOTICKET) ? (uint32_t)j : atomicAdd(tick, 1u);
                 if (dn) {   // `end` already placed: this chunk is a plain copy
                     lb_store(st + cc, LB_INC | (u64)L);
@@ -1126,11 +1129,11 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
             s_v = cc;
         }
         if (tid < 4 * PEE_TILE / 32) lm32[tid] = 0;
-        __syncthreads();
+        lds_barrier();
         const uint32_t cv = s_v;
         if (INPLACE) {
             if (cv == PEE_STOP) return;
-            if (cv >= (uint32_t)nchunks) { __syncthreads(); continue; }
+            if (cv >= (uint32_t)nchunks) { lds_barrier(); continue; }
         }
         const bool copy_only = !INPLACE && (cv & 0x80000000u);
         const int c = (int)(cv & 0x7FFFFFFFu);
@@ -1148,7 +1151,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                 const int w = c * (4 * PEE_TILE / 64) + tid;
                 if (w < lmw) lm_all[(size_t)b * lmw + w] = 0;
             }
-            __syncthreads();
+            lds_barrier();
             continue;
         }
         uint32_t esm = 0, safem = 0, rightm = 0;   // bit 4u+q
@@ -1171,7 +1174,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
             }
         }
         u64 ptot;
-        const u64 pex = block_excl_scan64<256>(packed, sh64, &ptot);
+        const u64 pex = block_excl_scan64_lds<256>(packed, sh64, &ptot);
         const uint32_t agg = (uint32_t)((ptot & 0xFFFFu) + ((ptot >> 16) & 0xFFFFu) + ((ptot >> 32) & 0xFFFFu) + (ptot >> 48));
         const bool publish = !(b == 0 && c == dbg_skip);
         if (c == 0) {
@@ -1192,7 +1195,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                 }
             }
         }
-        __syncthreads();
+        lds_barrier();
         const uint32_t excl = s_excl;
         const bool last = c == nchunks - 1;
         if (tid == 0) {
@@ -1209,7 +1212,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
             }
             if (last && excl + agg < L) { M->end = nc - 1; M->tile_end = ntiles - 1; atomicMax(&M->status, 1); }
         }
-        __syncthreads();   // lm32 zeroing vs the ORs below
+        lds_barrier();   // lm32 zeroing vs the ORs below
         if (excl < L) {   // some candidate of this chunk is active
             uint32_t base = excl;
             uint32_t unsafe_n = 0;
@@ -1261,7 +1264,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                 if (nib) atomicOr(&lm32[u * 32 + (tid >> 3)], nib << (4 * (tid & 7)));
                 if (INPLACE && touched) stv<NT>(reinterpret_cast<V*>(dst + o0[u] + W), a1[u]);
             }
-            const uint32_t nun = block_sum_u32<256>(unsafe_n, sh);   // also orders the lm32 ORs
+            const uint32_t nun = block_sum_u32_lds<256>(unsafe_n, sh);   // also orders the lm32 ORs
             if (tid == 0 && nun) atomicAdd(&M->lm_count, (int)nun);
         }
         if (tid == 0) {   // `end` is in this chunk (or there is none): later chunks need no cursor
@@ -1288,7 +1291,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                 if (w < lmw) lm_all[(size_t)b * lmw + w] = (u64)lm32[2 * tid] | ((u64)lm32[2 * tid + 1] << 32);
             }
         }
-        __syncthreads();
+        lds_barrier();
     }
 }
 
@@ -1315,14 +1318,14 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
     int cmax = nchunks - 1;
     if (INPLACE) {   // chunk-major slots: nothing past the last chunk any slice needs
         if (tid == 0) s_cmax = -1;
-        __syncthreads();
+        lds_barrier();
         int cm = -1;
         for (int b = tid; b < B; b += 256) {
             const int e = meta_all[b].end;
             cm = max(cm, e >= 0 ? (e >> 2) / PEE_CHUNK : -1);
         }
         if (cm >= 0) atomicMax(&s_cmax, cm);
-        __syncthreads();
+        lds_barrier();
         cmax = s_cmax;
     }
     for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
@@ -1359,7 +1362,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
         int c = j;
         if (j <= cend && !noticket) {   // exactly cend+1 slots take tickets 0..cend
             if (tid == 0) s_v = atomicAdd(ctl + 32 + 32 * (size_t)b, 1u);
-            __syncthreads();
+            lds_barrier();
             c = (int)s_v;
             if (INPLACE || c != j) pee_load_chunk<T, NT>(src, W, CR, items, c, a0, a1, o0);
         }
@@ -1385,7 +1388,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
             }
             if (tid < PEE_CHUNK * 4 / 64 + 2) pbuf[tid] = 0;   // ordered by the scan's barriers
             u64 ptot;
-            const u64 pex = block_excl_scan64<256>(packed, sh64, &ptot);
+            const u64 pex = block_excl_scan64_lds<256>(packed, sh64, &ptot);
             const uint32_t agg = (uint32_t)((ptot & 0xFFFFu) + ((ptot >> 16) & 0xFFFFu) + ((ptot >> 32) & 0xFFFFu) + (ptot >> 48));
             u64* st = status_all + (size_t)b * nchunks;
             const bool publish = c < cend && !(b == 0 && c == dbg_skip);
@@ -1406,7 +1409,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
                     }
                 }
             }
-            __syncthreads();
+            lds_barrier();
             const uint32_t excl = s_excl;
             const int w0 = (int)(excl >> 6);
             uint32_t base = excl;
@@ -1448,7 +1451,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
             // one store per payload word instead of a global atomic per item: words wholly
             // inside [excl, excl + agg) belong to this chunk alone; the first and last may be
             // shared with the neighbouring chunks (OR-ed in); the host zeroed the payload
-            __syncthreads();
+            lds_barrier();
             const int nw = (int)(((excl & 63u) + agg + 63u) >> 6);
             if (tid < nw) {
                 const u64 wv = pbuf[tid];
@@ -1469,7 +1472,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
                 }
             }
         }
-        __syncthreads();
+        lds_barrier();
     }
 }
 
@@ -1512,11 +1515,6 @@ __device__ unsigned long long g_ss_trace[SS_TRACE_N];
 #define SS_PAY_WORDS (SS_PAD_WORDS / 2 - 1)   // the embed keeps payloads of up to 10 751 words in that pad
 #define SS_SINK_BYTES (SS_THREADS * 48)   // per lane: two 16-B pixel vectors + one 8-B word (+pad)
 
-__device__ __forceinline__ void lds_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-}
 
 // wave-level primitives without LDS round trips (each __shfl is a ds_bpermute, ~100 cycles):
 // OR over the 16 lanes of a DPP row, and an exclusive scan of 0..7 per lane from three ballots
