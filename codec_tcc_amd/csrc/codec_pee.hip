@@ -1496,17 +1496,24 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
 // only branches left in the ring loop contain no vector memory instruction.  Barriers are
 // LDS-only (raw s_barrier): __syncthreads()'s fence waits vmcnt(0).
 #define SS_THREADS 1024
+#ifndef SS_LOCKSTEP
+#define SS_LOCKSTEP 1   // copy chunks: a barrier every SS_LOCKSTEP chunks keeps the waves in step
+#endif
 // diagnostic build only (tools/ss_trace.py, -DPEE_SS_TRACE): workgroup 0, wave 0 stamps the
 // chunk phases into LDS (no vector memory in the loop) and writes them out at the end
 #ifdef PEE_SS_TRACE
 #define SS_TRACE_N 2048
 __device__ unsigned long long g_ss_trace[SS_TRACE_N];
-// slot i of wave w: ss_trace[w * 128 + i] (chunks < 32 traced)
+// slot i of wave w: ss_trace[w * 128 + i - 4 * K0] (chunks K0 .. K0+31 traced)
+#ifndef PEE_SS_TRACE_K0
+#define PEE_SS_TRACE_K0 0
+#endif
 #define SS_STAMP(i)                                                                           \
     do {                                                                                      \
         unsigned long long t_;                                                                \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
-        if ((threadIdx.x & 63) == 0 && (i) < 128) ss_trace[(threadIdx.x >> 6) * 128 + (i)] = t_; \
+        const int j_ = (i) - 4 * PEE_SS_TRACE_K0;                                             \
+        if ((threadIdx.x & 63) == 0 && j_ >= 0 && j_ < 128) ss_trace[(threadIdx.x >> 6) * 128 + j_] = t_; \
     } while (0)
 #else
 #define SS_STAMP(i) do { } while (0)
@@ -1678,24 +1685,26 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
         const bool ok = it < items;
         const uint32_t o0 = cur.off((uint32_t)W);
         SS_STAMP(4 * k);
-        // classification on every lane: the first use of the ring registers is unconditional
-        uint32_t esm = 0, safem = 0, rightm = 0;
-        int pq[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const PeeCand pc = pee_classify((int)get_px(v1, 2 * q + 1), (int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1),
-                                            (int)get_px(v0, 2 * q), Tthr, maxval);
-            pq[q] = pc.p;
-            safem |= pc.safe ? 1u << q : 0u;
-            rightm |= pc.right ? 1u << q : 0u;
-            esm |= (pc.expand && pc.safe) ? 1u << q : 0u;
-        }
-        if (!ok) esm = 0u;
-        const uint32_t n = (uint32_t)__popc(esm);
+        // the chunk's registers are waited for here, once, outside any branch (an empty asm
+        // reading them): the compiler then counts vmcnt exactly around the branches below
+        asm volatile("" ::"v"(v0.x), "v"(v1.x));
         SS_STAMP(4 * k + 1);
         u64 wm = 0;
         bool touched = false;
         if (live) {   // uniform; no vector memory instruction inside
+            uint32_t esm = 0, safem = 0, rightm = 0;
+            int pq[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const PeeCand pc = pee_classify((int)get_px(v1, 2 * q + 1), (int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1),
+                                                (int)get_px(v0, 2 * q), Tthr, maxval);
+                pq[q] = pc.p;
+                safem |= pc.safe ? 1u << q : 0u;
+                rightm |= pc.right ? 1u << q : 0u;
+                esm |= (pc.expand && pc.safe) ? 1u << q : 0u;
+            }
+            if (!ok) esm = 0u;
+            const uint32_t n = (uint32_t)__popc(esm);
             last = k;
             uint32_t ex, tot, wb;
             ss_scan_small(n, wtot, par, &ex, &tot, &wb);
@@ -1744,8 +1753,13 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
             wm = row_or16_64((u64)nib << (4 * (lane & 15)));
             running += tot;
             if (running >= L) live = false;
-        } else {
-            rest += n;   // past `end` (out of place): counted for the exact capacity only
+        } else if (SS_LOCKSTEP && (k % SS_LOCKSTEP) == SS_LOCKSTEP - 1) {
+            // past `end` (out of place) the chunk is a plain copy: not classified (capacity
+            // stays a lower bound, CODEC_PEE_PARTIAL, as on the look-back path).  Without a
+            // barrier the oldest waves (scheduled first) run ahead and finish, and the youngest
+            // stream the slice's tail alone with a quarter of the loads in flight
+            // (tools/ss_trace.py: 0.37 ms of drift by chunk 100; 0.80 -> 0.74 ms with it)
+            lds_barrier();
         }
         // stores, unconditional (the 16 lanes of a map word store the same value)
         const uint32_t wix = (4 * it) >> 6;
@@ -1787,18 +1801,18 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
     lds_barrier();
 #ifdef PEE_SS_TRACE
     if (b == 0)
-        for (int i = tid; i < SS_TRACE_N; i += SS_THREADS) g_ss_trace[i] = (i & 127) < 4 * (last + 1) ? ss_trace[i] : 0ull;
+        for (int i = tid; i < SS_TRACE_N; i += SS_THREADS) g_ss_trace[i] = ss_trace[i];
 #endif
     if (tid == 0) {
         uint32_t un = 0, re = 0;
         for (int w = 0; w < 16; ++w) { un += red[0][w]; re += red[1][w]; }
         codec_pee_meta* M = meta_all + b;
-        const uint32_t cap = running + re;
+        const uint32_t cap = running + re;   // re = 0: chunks past `end` are not counted
         M->T = Tthr; M->maxval = maxval; M->L = (int)L; M->nc = nc; M->ntiles = ntiles; M->h = H; M->w = W;
         M->lm_count = (int)un;
         M->capacity = (int)cap;
-        // in place the count stops with the chunk holding `end`: a lower bound unless it was the last
-        M->flags = (INPLACE && last < nchunks - 1) ? CODEC_PEE_PARTIAL : 0;
+        // the count stops with the chunk holding `end`: a lower bound unless it was the last
+        M->flags = last < nchunks - 1 ? CODEC_PEE_PARTIAL : 0;
         M->reserved[0] = M->reserved[1] = M->reserved[2] = 0;
         if (L == 0) { M->end = -1; M->tile_end = -1; M->status = 0; }
         else if (running < L) { M->end = nc - 1; M->tile_end = ntiles - 1; M->status = 1; }   // truncated
@@ -1891,24 +1905,26 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
         const uint32_t it = (uint32_t)k * SS_THREADS + tid;
         const bool ok = it < items;
         const uint32_t o0 = cur.off((uint32_t)W);
-        // classification on every lane (unconditional first use of the ring registers)
-        uint32_t actm = 0, innm = 0;
-        int pq[4];
-        const u64 l4 = lw >> ((4 * it) & 63u);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int kq = (int)(4 * it) + q;
-            const bool act = ok & (k <= cend) & (kq <= end) & !((l4 >> q) & 1ull);   // & : no branches
-            const int p = med3((int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1), (int)get_px(v0, 2 * q));
-            const int e2 = (int)get_px(v1, 2 * q + 1) - p;
-            pq[q] = p;
-            actm |= act ? 1u << q : 0u;
-            innm |= (act & ((unsigned)(e2 + 2 * Tthr) < (unsigned)(4 * Tthr))) ? 1u << q : 0u;
-        }
+        // the chunk's registers are waited for here, once, outside any branch (see k_pee_embed_ss)
+        asm volatile("" ::"v"(v0.x), "v"(v1.x), "v"((uint32_t)lw));
+        uint32_t actm = 0;
         u64 wout = 0;
         bool wstore = false;
         uint32_t wabs = 0;
         if (k <= cend) {   // uniform; no vector memory instruction inside
+            uint32_t innm = 0;
+            int pq[4];
+            const u64 l4 = lw >> ((4 * it) & 63u);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int kq = (int)(4 * it) + q;
+                const bool act = ok & (kq <= end) & !((l4 >> q) & 1ull);   // & : no branches
+                const int p = med3((int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1), (int)get_px(v0, 2 * q));
+                const int e2 = (int)get_px(v1, 2 * q + 1) - p;
+                pq[q] = p;
+                actm |= act ? 1u << q : 0u;
+                innm |= (act & ((unsigned)(e2 + 2 * Tthr) < (unsigned)(4 * Tthr))) ? 1u << q : 0u;
+            }
             const uint32_t n = (uint32_t)__popc(innm);
             // pbuf[par] was last read (and re-zeroed below) by these same threads two chunks ago
             uint32_t ex, tot, wb;
@@ -1942,6 +1958,8 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
             p_par = par;
             par ^= 1;
             running += tot;
+        } else if (SS_LOCKSTEP && (k % SS_LOCKSTEP) == SS_LOCKSTEP - 1) {
+            lds_barrier();   // copy chunks: keep the waves in step (see k_pee_embed_ss; 0.91 -> 0.78 ms)
         }
         // stores, unconditional (redirected to the sink when they must not land)
         *(wstore ? payload + wabs : sink_w) = wout;

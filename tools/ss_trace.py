@@ -18,7 +18,8 @@ OUT = os.path.join(REPO, "tools", "bin", "libcodec_sstrace.so")
 if sys.argv[1] == "build":
     from codec_tcc_amd import build as B
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    cmd = [B.hipcc(), *B.FLAGS, "-DPEE_SS_TRACE", f"-I{B.INC}", *B.SRCS, "-o", OUT]
+    k0 = sys.argv[2] if len(sys.argv) > 2 else "0"   # first traced chunk
+    cmd = [B.hipcc(), *B.FLAGS, "-DPEE_SS_TRACE", f"-DPEE_SS_TRACE_K0={k0}", f"-I{B.INC}", *B.SRCS, "-o", OUT]
     subprocess.run(cmd, check=True)
     print(OUT)
     sys.exit(0)
@@ -46,14 +47,19 @@ for _ in range(3):
 torch.cuda.synchronize()
 buf = (C.c_ulonglong * 2048)()
 n = fn(buf, 2048)
-t = np.array(buf[:n], dtype=np.int64).reshape(16, 128)
-k = min(32, int(np.count_nonzero(t[0]) // 4))
+t = np.array(buf[:n], dtype=np.uint64).reshape(16, 128).astype(np.float64)
+k = 32
 t = t[:, : 4 * k].reshape(16, k, 4)
+bad = (t[:, :, 2] < t[:, :, 1]) | (t[:, :, 2] > t[:, :, 3])   # no scan stamp (chunk past `end`)
+t[:, :, 2] = np.where(bad, t[:, :, 1], t[:, :, 2])
+t = t.astype(np.int64)
 t0 = t[0, 0, 0]
 print(f"{'inplace' if inplace else 'out of place'}: {k} chunks traced (workgroup 0, 16 waves), cycles since the first stamp")
 print("chunk  start(w0)  data_min  data_max  barrier_out_min  barrier_out_max  end_max  per_chunk")
 for i in range(k):
     st = t[0, i, 0] - t0
+    if not t[0, i, 0]:
+        continue
     print(f"{i:5d} {st:10d} {t[:, i, 1].min() - t0:9d} {t[:, i, 1].max() - t0:9d} {t[:, i, 2].min() - t0:15d} "
           f"{t[:, i, 2].max() - t0:15d} {t[:, i, 3].max() - t0:8d} {(t[0, i + 1, 0] - t[0, i, 0]) if i + 1 < k else 0:9d}")
 print("slowest wave to reach the data per chunk:", [int(np.argmax(t[:, i, 1])) for i in range(k)])
