@@ -101,7 +101,7 @@ KERNEL_TAGS = {1: "k_scan_fast", 2: "k_scan_generic", 3: "k_block_exact", 4: "k_
                11: "k_pee_embed", 12: "k_pee_copy", 13: "k_pee_dcount", 14: "k_pee_recover",
                15: "k_pee_embed1", 16: "k_pee_extract1", 17: "k_scan_read", 18: "k_unxor",
                19: "k_scan_rows", 20: "k_scan_rows_read", 21: "k_quality", 22: "k_decide_embed",
-               23: "k_pee_capacity"}
+               23: "k_pee_capacity", 24: "k_pee_embed_ss", 25: "k_pee_extract_ss"}
 EXPORTS = tuple(_SIGS)
 
 _lib = None

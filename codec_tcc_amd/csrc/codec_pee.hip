@@ -2192,7 +2192,7 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
     const bool flat = !inplace && P->B < 32 && P->B <= knob("CODEC_PEE_FLAT_MAXB", 7);
     if (vec && items > 0 && onepass != 0 && pee_use_slice_serial(P, inplace)) {
         // slice-serial single pass: one workgroup per slice, no look-back, no memsets
-        ProfScope prof(st, CODEC_K_PEE_EMBED1);
+        ProfScope prof(st, CODEC_K_PEE_EMBED_SS);
         const bool pay_lds = P->payload_words <= SS_PAY_WORDS && knob("CODEC_PEE_SS_PAYLDS", 1) != 0;
 #define PES1(TT, NTV, IP, PL) hipLaunchKernelGGL((k_pee_embed_ss<TT, NTV, IP, 4, PL>), dim3((unsigned)P->B), dim3(SS_THREADS), 0, st, \
             static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, tps, \
@@ -2335,7 +2335,7 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
     if (vec && items > 0 && onepass != 0 && pee_use_slice_serial(P, inplace)) {
         // slice-serial: writes every payload word itself (no memset) and never sets the flag
         uint32_t* ctl = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.ctl);
-        ProfScope prof(st, CODEC_K_PEE_EXTRACT1);
+        ProfScope prof(st, CODEC_K_PEE_EXTRACT_SS);
 #define PXS(TT, NTV, IP) hipLaunchKernelGGL((k_pee_extract_ss<TT, NTV, IP, 4>), dim3((unsigned)P->B), dim3(SS_THREADS), 0, st, \
             static_cast<const TT*>(stego), static_cast<TT*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm), \
             P->lm_words, reinterpret_cast<u64*>(payload_out), P->payload_words, ctl + 1, static_cast<char*>(workspace) + L.sink)
