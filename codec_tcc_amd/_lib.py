@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcodec_hip.so")
+# CODEC_TCC_LIB: an alternative build of the same library (A/B benchmarking, tools/ab_bench.sh)
+LIB_PATH = os.environ.get("CODEC_TCC_LIB") or os.path.join(_HERE, "libcodec_hip.so")
 
 MAX_PLANES = 16
 MODE_HYBRID = 0

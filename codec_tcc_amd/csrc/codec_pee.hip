@@ -1547,42 +1547,49 @@ __device__ __forceinline__ uint32_t wave_excl_small(uint32_t n, uint32_t* total)
 
 // exclusive scan of n (0..7) over the 1024 threads with ONE barrier and no shuffles: ballot
 // scans inside the waves, wave totals through LDS (double-buffered by parity: a wave cannot
-// rewrite wtot[par] before every wave has passed the next barrier)
+// rewrite wtot[par] before every wave has passed the next barrier).  The 16 wave totals are
+// scanned across the 16 lanes of each DPP row (4 row_shr adds) and the wave's base and the
+// block total read back with readlane into scalars: 8 VALU instead of 16 per-lane sums.
 __device__ __forceinline__ void ss_scan_small(uint32_t n, uint32_t (*wtot)[16], int par, uint32_t* excl, uint32_t* tot,
                                               uint32_t* wbase) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     uint32_t wt;
     const uint32_t ex = wave_excl_small(n, &wt);
     if (lane == 0) wtot[par][wv] = wt;
     lds_barrier();
-    uint32_t wb = 0, t = 0;
-#pragma unroll
-    for (int w = 0; w < 16; ++w) {
-        const uint32_t v = wtot[par][w];
-        t += v;
-        wb += w < wv ? v : 0u;
-    }
+    int x = (int)wtot[par][lane & 15];
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);   // row_shr:1 (lane 0 of a row reads 0)
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);   // row_shr:8
+    const uint32_t t = (uint32_t)__builtin_amdgcn_readlane(x, 15);
+    const uint32_t wb = wv ? (uint32_t)__builtin_amdgcn_readlane(x, wv - 1) : 0u;
     *excl = wb + ex;
     *tot = t;
     *wbase = wb;
 }
 
 // item -> element offset of its 8-pixel column chunk in the top row of its row pair, advanced
-// chunk by chunk without divisions: item + 1024 moves (row pair, column chunk) by
-// (1024 / CR, 1024 % CR) with at most one carry.  Lanes/chunks past the end load a clamped
-// valid address (data unused): straight-line loads let hipcc count vmcnt exactly.
+// chunk by chunk without divisions or multiplies: item + 1024 moves (row pair, column chunk)
+// by (1024 / CR, 1024 % CR) with at most one carry, i.e. the offset by a fixed step plus a
+// fixed wrap correction.  Lanes/chunks past the end load a clamped valid address (data
+// unused): straight-line loads let hipcc count vmcnt exactly.
 struct SsCursor {
-    uint32_t rr, cc;
-    __device__ __forceinline__ void init(uint32_t it, uint32_t CR) {
-        rr = it / CR;
+    uint32_t cc, o;
+    __device__ __forceinline__ void init(uint32_t it, uint32_t CR, uint32_t W) {
+        const uint32_t rr = it / CR;
         cc = it - rr * CR;
+        o = 2u * rr * W + 8u * cc;
     }
-    __device__ __forceinline__ void step(uint32_t dq, uint32_t dr, uint32_t CR) {
+    // ostep = 2 W (1024 / CR) + 8 (1024 % CR), owrap = 2 W - 8 CR (uniform)
+    __device__ __forceinline__ void step(uint32_t dr, uint32_t CR, uint32_t ostep, uint32_t owrap) {
         cc += dr;
-        rr += dq;
-        if (cc >= CR) { cc -= CR; ++rr; }
+        o += ostep;
+        const bool wrap = cc >= CR;
+        cc = wrap ? cc - CR : cc;
+        o = wrap ? o + owrap : o;
     }
-    __device__ __forceinline__ uint32_t off(uint32_t W) const { return 2u * rr * W + 8u * cc; }
 };
 
 template <typename T, bool NT>
@@ -1652,20 +1659,23 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
     V r0[D], r1[D];
     // cursors of this lane's item in the current chunk and in the chunk D ahead (the refill)
     const uint32_t dq = SS_THREADS / (uint32_t)CR, dr = SS_THREADS % (uint32_t)CR;
+    const uint32_t ostep = 2u * (uint32_t)W * dq + 8u * dr, owrap = 2u * (uint32_t)W - 8u * (uint32_t)CR;
     uint32_t off_last;
     {
         SsCursor l;
-        l.init(items - 1u, (uint32_t)CR);
-        off_last = l.off((uint32_t)W);
+        l.init(items - 1u, (uint32_t)CR, (uint32_t)W);
+        off_last = l.o;
     }
-    SsCursor cur, ahead;
-    cur.init((uint32_t)tid, (uint32_t)CR);
-    ahead = cur;
+    // ro[d]: the offset ring slot d was loaded from (= the item's store offset)
+    uint32_t ro[D];
+    SsCursor ahead;
+    ahead.init((uint32_t)tid, (uint32_t)CR, (uint32_t)W);
     uint32_t it_a = (uint32_t)tid;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-        ss_load_at<T, NT>(src, (uint32_t)W, it_a < items ? ahead.off((uint32_t)W) : off_last, r0[d], r1[d]);
-        ahead.step(dq, dr, (uint32_t)CR);
+        ro[d] = it_a < items ? ahead.o : off_last;
+        ss_load_at<T, NT>(src, (uint32_t)W, ro[d], r0[d], r1[d]);
+        ahead.step(dr, (uint32_t)CR, ostep, owrap);
         it_a += SS_THREADS;
     }
     if (PAY_LDS) {   // the payload in LDS once: no dependent global round trip per chunk
@@ -1683,25 +1693,29 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
         V& v1 = r1[d];
         const uint32_t it = (uint32_t)k * SS_THREADS + tid;
         const bool ok = it < items;
-        const uint32_t o0 = cur.off((uint32_t)W);
+        const uint32_t o0 = ro[d];
         SS_STAMP(4 * k);
         // the chunk's registers are waited for here, once, outside any branch (an empty asm
         // reading them): the compiler then counts vmcnt exactly around the branches below
         asm volatile("" ::"v"(v0.x), "v"(v1.x));
         SS_STAMP(4 * k + 1);
-        u64 wm = 0;
+        uint32_t wm = 0;
         bool touched = false;
+        const bool was_live = live;
         if (live) {   // uniform; no vector memory instruction inside
-            uint32_t esm = 0, safem = 0, rightm = 0;
+            uint32_t esm = 0, safem = 0;
             int pq[4];
+            bool eb[4], sb[4], rb[4];   // per-candidate lane masks (SGPR pairs) for the selects below
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const PeeCand pc = pee_classify((int)get_px(v1, 2 * q + 1), (int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1),
                                                 (int)get_px(v0, 2 * q), Tthr, maxval);
                 pq[q] = pc.p;
+                eb[q] = pc.expand;
+                sb[q] = pc.safe;
+                rb[q] = pc.right;
                 safem |= pc.safe ? 1u << q : 0u;
-                rightm |= pc.right ? 1u << q : 0u;
-                esm |= (pc.expand && pc.safe) ? 1u << q : 0u;
+                esm |= (pc.expand & pc.safe) ? 1u << q : 0u;
             }
             if (!ok) esm = 0u;
             const uint32_t n = (uint32_t)__popc(esm);
@@ -1711,13 +1725,16 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
             SS_STAMP(4 * k + 2);
             par ^= 1;
             // this lane's expandable candidates take ranks [rs, rs + n): their payload bits
-            // are one <= 4-bit field of at most two consecutive payload words
+            // are one <= 4-bit field of at most two consecutive 32-bit payload words; the
+            // first m of them carry bits, and candidate q is processed iff fewer than m
+            // expandable candidates precede it in the lane
             const uint32_t rs = running + ex;
-            u64 field;
+            const uint32_t m = (ok & (L > rs)) ? min(L - rs, 4u) : 0u;
+            uint32_t field;
             if (PAY_LDS) {
-                const uint32_t w = min(rs >> 6, (uint32_t)SS_PAY_WORDS - 2u), sh = rs & 63u;
-                const u64 lo = pay[w], hi = pay[w + 1];
-                field = (lo >> sh) | ((hi << ((64u - sh) & 63u)) & (sh ? ~0ull : 0ull));
+                const uint32_t* pay32 = reinterpret_cast<const uint32_t*>(pay);
+                const uint32_t w = min(rs >> 5, 2u * (uint32_t)SS_PAY_WORDS - 2u);
+                field = __builtin_amdgcn_alignbit(pay32[w + 1], pay32[w], rs & 31u);
             } else {
                 // wave-uniform scalar loads: the wave's ranks lie in [running + wb, +256)
                 const uint32_t w0 = __builtin_amdgcn_readfirstlane((running + wb) >> 6);
@@ -1727,30 +1744,34 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
                 const uint32_t wi = (rs >> 6) - w0, sh = rs & 63u;       // 0..4
                 const u64 lo = wi == 0 ? pwd[0] : wi == 1 ? pwd[1] : wi == 2 ? pwd[2] : wi == 3 ? pwd[3] : pwd[4];
                 const u64 hi = wi == 0 ? pwd[1] : wi == 1 ? pwd[2] : wi == 2 ? pwd[3] : wi == 3 ? pwd[4] : pwd[5];
-                field = sh ? (lo >> sh) | (hi << (64u - sh)) : lo;
+                field = (uint32_t)(sh ? (lo >> sh) | (hi << (64u - sh)) : lo);
             }
-            uint32_t nib = 0;
-            int eidx = -1;
+            uint32_t procm = 0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {   // branch-free: candidate q is processed iff rank rs+pre < L
+            for (int q = 0; q < 4; ++q) {   // branch-free
                 const uint32_t bit = 1u << q;
                 const uint32_t pre = (uint32_t)__popc(esm & (bit - 1u));
-                const bool proc = ok & (rs + pre < L);
+                const bool proc = pre < m;
+                procm |= proc ? bit : 0u;
                 const int x = (int)get_px(v1, 2 * q + 1);
-                const int p = pq[q];
-                const int nv_e = p + 2 * (x - p) + (int)((field >> pre) & 1ull);
-                const int nv_s = (rightm & bit) ? x + Tthr : x - Tthr;
-                const bool safe = (safem & bit) != 0, expd = (esm & bit) != 0;
-                const int nv = !proc || !safe ? x : (expd ? nv_e : nv_s);
+                const int nv_e = 2 * x - pq[q] + (int)((field >> pre) & 1u);   // p + 2e + bit
+                const int nv_s = rb[q] ? x + Tthr : x - Tthr;
+                const int nv = (proc & sb[q]) ? (eb[q] ? nv_e : nv_s) : x;
                 set_px(v1, 2 * q + 1, (uint32_t)nv);
-                nib |= (proc & !safe) ? bit : 0u;
-                touched |= proc;
-                eidx = (proc & expd & (rs + pre == L - 1)) ? (int)(4 * it) + q : eidx;
             }
-            if (eidx >= 0) s_end = eidx;                   // one lane of the slice, once
+            touched = procm != 0;
+            // the lane holding rank L-1 (1 <= L - rs <= n): `end` is its last processed
+            // expandable candidate; one lane of the slice, once
+            if (m != 0 && L - rs <= n) s_end = (int)(4 * it) + 31 - __clz(procm & esm);
+            const uint32_t nib = procm & ~safem;
             unsafe_n += (uint32_t)__popc(nib);
-            // location-map word (4 it) / 64 = 16 lanes x 4 candidate bits, OR-ed over the DPP row
-            wm = row_or16_64((u64)nib << (4 * (lane & 15)));
+            // location-map word (4 it) / 64 = 16 lanes x 4 candidate bits: each half is the
+            // OR over 8 lanes (two quad permutes + a half-row mirror), stored as a 32-bit word
+            // by lanes 0 and 8 of the DPP row
+            wm = nib << (4 * (lane & 7));
+            wm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+            wm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+            wm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0x141, 0xF, 0xF, false);   // row_half_mirror
             running += tot;
             if (running >= L) live = false;
         } else if (SS_LOCKSTEP && (k % SS_LOCKSTEP) == SS_LOCKSTEP - 1) {
@@ -1761,29 +1782,35 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
             // (tools/ss_trace.py: 0.37 ms of drift by chunk 100; 0.80 -> 0.74 ms with it)
             lds_barrier();
         }
-        // stores, unconditional (the 16 lanes of a map word store the same value)
+        // stores, unconditional (lanes 0 / 8 of a DPP row store the map word's low / high half)
         const uint32_t wix = (4 * it) >> 6;
-        *(ok && (int)wix < lmw ? lm + wix : sink_w) = wm;
+        *(ok && (!INPLACE || was_live) && (lane & 7) == 0 && (int)wix < lmw
+              ? reinterpret_cast<uint32_t*>(lm + wix) + ((lane >> 3) & 1)
+              : reinterpret_cast<uint32_t*>(sink_w)) = wm;
         if (INPLACE) {
             stv<NT>(ok && touched ? reinterpret_cast<V*>(dst + o0 + W) : sink_v, v1);
         } else {
             stv<NT>(ok ? reinterpret_cast<V*>(dst + o0) : sink_v, v0);
             stv<NT>(ok ? reinterpret_cast<V*>(dst + o0 + W) : sink_v + 1, v1);
         }
-        ss_load_at<T, NT>(src, (uint32_t)W, it_a < items ? ahead.off((uint32_t)W) : off_last, v0, v1);
-        cur.step(dq, dr, (uint32_t)CR);
-        ahead.step(dq, dr, (uint32_t)CR);
+        // in place, once `end` is reached the rest of the group refills from one clamped
+        // address (L2 hits): the group still runs to its end, see the loop below
+        ro[d] = it_a < items && (!INPLACE || live) ? ahead.o : off_last;
+        ss_load_at<T, NT>(src, (uint32_t)W, ro[d], v0, v1);
+        ahead.step(dr, (uint32_t)CR, ostep, owrap);
         it_a += SS_THREADS;
         SS_STAMP(4 * k + 3);
     };
 
+    // Full groups of D chunks, no guard around any chunk.  In place the loop is left only
+    // at the end of a group (a chunk past `end` is a no-op): an exit after any chunk is
+    // folded by the CFG structurizer into the loop latch, and hipcc's vmcnt bookkeeping then
+    // merges the exit paths into the loop header's state (vmcnt(2) instead of (14): every
+    // D-th chunk waited for the loads issued one chunk earlier).
     const int nfull = nchunks / D * D;
-    for (int k0 = 0; k0 < nfull; k0 += D) {   // full groups: no guard around any chunk
+    for (int k0 = 0; k0 < nfull; k0 += D) {
 #pragma unroll
-        for (int d = 0; d < D; ++d) {
-            if (INPLACE && !live) break;         // leaves the loop (no join back into it)
-            chunk(d, k0 + d);
-        }
+        for (int d = 0; d < D; ++d) chunk(d, k0 + d);
         if (INPLACE && !live) break;
     }
     if (!INPLACE || live) {
@@ -1857,24 +1884,26 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
     V r0[D], r1[D];
     u64 rl[D];
     const uint32_t dq = SS_THREADS / (uint32_t)CR, dr = SS_THREADS % (uint32_t)CR;
+    const uint32_t ostep = 2u * (uint32_t)W * dq + 8u * dr, owrap = 2u * (uint32_t)W - 8u * (uint32_t)CR;
     // the ring never loads past chunk klast (in place: the chunk holding `end`)
     const uint32_t items_l = min(items, (uint32_t)(klast + 1) * SS_THREADS);
     uint32_t off_last;
     {
         SsCursor l;
-        l.init(items_l - 1u, (uint32_t)CR);
-        off_last = l.off((uint32_t)W);
+        l.init(items_l - 1u, (uint32_t)CR, (uint32_t)W);
+        off_last = l.o;
     }
-    SsCursor cur, ahead;
-    cur.init((uint32_t)tid, (uint32_t)CR);
-    ahead = cur;
+    uint32_t ro[D];
+    SsCursor ahead;
+    ahead.init((uint32_t)tid, (uint32_t)CR, (uint32_t)W);
     uint32_t it_a = (uint32_t)tid;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         const bool in = it_a < items_l;
-        ss_load_at<T, NT>(src, (uint32_t)W, in ? ahead.off((uint32_t)W) : off_last, r0[d], r1[d]);
+        ro[d] = in ? ahead.o : off_last;
+        ss_load_at<T, NT>(src, (uint32_t)W, ro[d], r0[d], r1[d]);
         rl[d] = lm[(4 * (in ? it_a : items_l - 1u)) >> 6];
-        ahead.step(dq, dr, (uint32_t)CR);
+        ahead.step(dr, (uint32_t)CR, ostep, owrap);
         it_a += SS_THREADS;
     }
     uint32_t running = 0;
@@ -1904,7 +1933,7 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
         const u64 lw = rl[d];
         const uint32_t it = (uint32_t)k * SS_THREADS + tid;
         const bool ok = it < items;
-        const uint32_t o0 = cur.off((uint32_t)W);
+        const uint32_t o0 = ro[d];
         // the chunk's registers are waited for here, once, outside any branch (see k_pee_embed_ss)
         asm volatile("" ::"v"(v0.x), "v"(v1.x), "v"((uint32_t)lw));
         uint32_t actm = 0;
@@ -1914,11 +1943,11 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
         if (k <= cend) {   // uniform; no vector memory instruction inside
             uint32_t innm = 0;
             int pq[4];
-            const u64 l4 = lw >> ((4 * it) & 63u);
+            const uint32_t l4 = (uint32_t)(lw >> ((4 * it) & 63u));
+            const int rem = end - (int)(4 * it);   // candidate q of this item is at or before `end` iff q <= rem
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int kq = (int)(4 * it) + q;
-                const bool act = ok & (kq <= end) & !((l4 >> q) & 1ull);   // & : no branches
+                const bool act = ok & (q <= rem) & !((l4 >> q) & 1u);   // & : no branches
                 const int p = med3((int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1), (int)get_px(v0, 2 * q));
                 const int e2 = (int)get_px(v1, 2 * q + 1) - p;
                 pq[q] = p;
@@ -1934,7 +1963,7 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
             // this lane's inner candidates take ranks [rs, rs + n): their bits form one <= 4-bit
             // field, OR-ed into at most two words of the chunk's LDS buffer
             const uint32_t rs = running + ex;
-            u64 field = 0;
+            uint32_t field = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {   // branch-free
                 const uint32_t bit = 1u << q;
@@ -1942,15 +1971,16 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
                 const int p = pq[q];
                 const int e2 = x - p;
                 const bool act = (actm & bit) != 0, inner = (innm & bit) != 0;
-                field |= (u64)((uint32_t)inner & (uint32_t)e2 & 1u) << __popc(innm & (bit - 1u));
+                field |= ((uint32_t)inner & (uint32_t)e2 & 1u) << __popc(innm & (bit - 1u));
                 const int v_in = p + (e2 >> 1), v_sh = x + ((e2 >= 2 * Tthr) ? -Tthr : Tthr);
                 const int nx = act ? (inner ? v_in : v_sh) : x;
                 set_px(v1, 2 * q + 1, (uint32_t)nx);
             }
-            if (field) {
-                const uint32_t o = rs - (running & ~63u), wi = o >> 6, sh = o & 63u;
-                atomicOr(&pbuf[par][wi], field << sh);
-                if (sh && (field >> (64u - sh))) atomicOr(&pbuf[par][wi + 1], field >> (64u - sh));
+            if (field) {   // <= 4 bits at chunk bit o: one or two 32-bit words of the LDS buffer
+                uint32_t* pb32 = reinterpret_cast<uint32_t*>(pbuf[par]);
+                const uint32_t o = rs - (running & ~63u), wi = o >> 5, sh = o & 31u;
+                atomicOr(&pb32[wi], field << sh);
+                if (sh > 28u && (field >> (32u - sh))) atomicOr(&pb32[wi + 1], field >> (32u - sh));
             }
             pend = true;
             p_lo = running;
@@ -1971,10 +2001,10 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
         }
         {   // refill (branch-free; past chunk klast the last item's address, data unused)
             const bool in = it_a < items_l;
-            ss_load_at<T, NT>(src, (uint32_t)W, in ? ahead.off((uint32_t)W) : off_last, v0, v1);
+            ro[d] = in ? ahead.o : off_last;
+            ss_load_at<T, NT>(src, (uint32_t)W, ro[d], v0, v1);
             rl[d] = lm[(4 * (in ? it_a : items_l - 1u)) >> 6];
-            cur.step(dq, dr, (uint32_t)CR);
-            ahead.step(dq, dr, (uint32_t)CR);
+            ahead.step(dr, (uint32_t)CR, ostep, owrap);
             it_a += SS_THREADS;
         }
     };
@@ -2199,8 +2229,20 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
             reinterpret_cast<const u64*>(payload), P->payload_words, meta, reinterpret_cast<u64*>(lm), P->lm_words, \
             static_cast<char*>(workspace) + L.sink)
 #define PES(TT, NTV, IP) do { if (pay_lds) PES1(TT, NTV, IP, true); else PES1(TT, NTV, IP, false); } while (0)
+        // ring depth of the in-place embed: it does not know `end` in advance, so the D - 1
+        // chunks it has in flight past it are wasted reads; at 256 x 2048^2 the steady state
+        // is HBM-bound (~5 TB/s of reads + writes), and D = 2 keeps enough in flight:
+        // 0.0825 -> 0.0789 ms (D = 3: 0.0824; tools/ab_depth.sh).  CODEC_PEE_SS_D=4 restores 4.
+        const long long ss_d = pay_lds ? knob("CODEC_PEE_SS_D", 2) : 4;
+#define PES1D(TT, NTV, IP, DD) hipLaunchKernelGGL((k_pee_embed_ss<TT, NTV, IP, DD, true>), dim3((unsigned)P->B), dim3(SS_THREADS), 0, st, \
+            static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, tps, \
+            reinterpret_cast<const u64*>(payload), P->payload_words, meta, reinterpret_cast<u64*>(lm), P->lm_words, \
+            static_cast<char*>(workspace) + L.sink)
         if (P->bytes == 2) {
-            if (inplace) { if (nt) PES(uint16_t, true, true); else PES(uint16_t, false, true); }
+            if (inplace) {
+                if (ss_d == 2 && nt) PES1D(uint16_t, true, true, 2);
+                else if (nt) PES(uint16_t, true, true); else PES(uint16_t, false, true);
+            }
             else { if (nt) PES(uint16_t, true, false); else PES(uint16_t, false, false); }
         } else {
             if (inplace) { if (nt) PES(uint8_t, true, true); else PES(uint8_t, false, true); }
@@ -2208,6 +2250,7 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
         }
 #undef PES
 #undef PES1
+#undef PES1D
         LAUNCH_CHECK("k_pee_embed_ss");
         if ((P->H & 1) && !inplace) HIP_TRY(pee_copy_last_rows(P, cover, stego, st));
         return 0;
