@@ -1035,6 +1035,11 @@ struct ListTerm {
     __device__ __forceinline__ double operator()(int k) const { return terms[list[k]]; }
 };
 
+#ifndef DECIDE_RP
+// planes per round of the wave-parallel decision: 7 plane waves + the H(Y) wave = 2 waves
+// per SIMD (8 put three on one SIMD: 33.4 -> 32.0 us per slice, tools/decide_phases.py)
+#define DECIDE_RP 7
+#endif
 #ifdef DECIDE_TS   // diagnostic build only (tools/decide_phases.py): phase timestamps into the term scratch
 #define DTS(k) do { if (threadIdx.x == 0) reinterpret_cast<long long*>(gterms + (size_t)blockIdx.x * HistCfg<T>::kBins)[HistCfg<T>::kBins - 16 + (k)] = wall_clock64(); } while (0)
 #else
@@ -1116,6 +1121,8 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
     codec_slice_meta* M = meta_all + b;
 
     DTS(0);
+    // the scan's block key, loaded now (used by the offset argmax after the decision)
+    const u64 key0 = (t == 0 && fast_blocks && P.fixed_offset < 0 && P.mode == CODEC_MODE_HYBRID) ? gkey[b] : 0ull;
     // fused embed: the slice's payload words (<= 2 KiB) go to LDS now, read by the embed
     // loop after the decision instead of one dependent global load per bit
     constexpr int kPaySh = EMBED ? 256 : 1;
@@ -1193,15 +1200,26 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
             }
         }
     }
+    DTS(12);
     if (t < 16) pops_sh[t] = 0;
     uint32_t m;
     const uint32_t rank0 = block_excl_scan<1024>((uint32_t)__popcll(nzmask), sh, &m);
+    DTS(13);
+    {   // the 16 per-plane sums of the wave as one reduce-scatter: 8 + 4 + 2 + 1 shuffles leave
+        // lane l with plane l >> 2 summed over 16 lanes, two more finish it (17 instead of 96)
+        const int lane = t & 63;
+        uint32_t a[8], b4[4], c2[2];
+        const bool h5 = (lane >> 5) & 1, h4 = (lane >> 4) & 1, h3 = (lane >> 3) & 1, h2 = (lane >> 2) & 1;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        uint32_t x = pop[i];
+        for (int j = 0; j < 8; ++j) a[j] = (h5 ? pop[8 + j] : pop[j]) + __shfl_xor(h5 ? pop[j] : pop[8 + j], 32, 64);
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
-        if ((t & 63) == 0 && x) atomicAdd(&pops_sh[i], x);
+        for (int j = 0; j < 4; ++j) b4[j] = (h4 ? a[4 + j] : a[j]) + __shfl_xor(h4 ? a[j] : a[4 + j], 16, 64);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) c2[j] = (h3 ? b4[2 + j] : b4[j]) + __shfl_xor(h3 ? b4[j] : b4[2 + j], 8, 64);
+        uint32_t x = (h2 ? c2[1] : c2[0]) + __shfl_xor(h2 ? c2[0] : c2[1], 4, 64);
+        x += __shfl_xor(x, 2, 64);
+        x += __shfl_xor(x, 1, 64);
+        if ((lane & 3) == 0 && x) atomicAdd(&pops_sh[lane >> 2], x);
     }
     DTS(1);
     const bool lut_ok = lut_len >= npx;
@@ -1270,18 +1288,21 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
         for (int g = wv; g < ngrp; g += 16) {             // bit-plane ballots per rank group
             const int r = g * 64 + lane;
             const uint32_t v = r < (int)m ? rv[r] : 0u;
+            uint32_t lo = 0, hi = 0;                       // lane i < 16 collects plane i's ballot
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const u64 bm = __ballot((v >> i) & 1u);
-                if (lane == i) pm[g * 16 + i] = bm;
+                lo = lane == i ? (uint32_t)bm : lo;
+                hi = lane == i ? (uint32_t)(bm >> 32) : hi;
             }
+            if (lane < 16) pm[g * 16 + lane] = (u64)lo | ((u64)hi << 32);
         }
         __syncthreads();
         DTS(8);
         // planes per round: enough for the usual s (5 on 12-bit data, 7 on uniform 16-bit),
         // few enough that the round's waves are not sharing SIMDs 4 to 1 (each list build and
         // sum is VALU-issue bound); H(Y) runs on the last wave meanwhile
-        const int rp = min(wplanes, 8);
+        const int rp = min(wplanes, DECIDE_RP);
         if (wv == 15) {
             const double h = -np_sum_wave(RankTerm{tl}, (int)m);
             if (lane == 0) hy_sh = h;
@@ -1294,40 +1315,37 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
                 const uint32_t pp = pops_sh[i];
                 double hxy = 0.0;
                 if (pp != 0 && (long long)pp != npx) {
-                    // joint order from the group ballots: lane j holds group (blk + j)'s mask and
-                    // the zeros / ones before it; the group loop then only shuffles and stores
+                    // joint order from the group ballots (rank group g's bit-i mask)
                     uint16_t* L = jl + (size_t)wv * m;
                     uint32_t ones = 0;
                     for (int g = lane; g < ngrp; g += 64) ones += (uint32_t)__popcll(pm[g * 16 + i]);
 #pragma unroll
                     for (int o = 32; o >= 1; o >>= 1) ones += __shfl_xor(ones, o, 64);
                     uint32_t zbase = 0, obase = (uint32_t)m - ones;      // ones follow all zeros
+                    // one rank group per step, the whole wave on it: lane e places rank
+                    // 64 g + e at the next zero / one position (mbcnt of the group's mask), so
+                    // each step is one store of two contiguous runs.  The masks of 64 groups
+                    // sit one per lane and are broadcast with readlane (uniform, no LDS trip).
                     for (int blk = 0; blk < ngrp; blk += 64) {
-                        const int g = blk + lane;
-                        const u64 mk = g < ngrp ? pm[g * 16 + i] : 0ull;
-                        const int nr = g < ngrp ? min(64, (int)m - g * 64) : 0;   // ranks in group g
-                        const uint32_t oc = (uint32_t)__popcll(mk), zc = (uint32_t)nr - oc;
-                        uint32_t zi = zc, oi = oc;                         // inclusive scans
-#pragma unroll
-                        for (int o = 1; o < 64; o <<= 1) {
-                            const uint32_t zy = __shfl_up(zi, o, 64), oy = __shfl_up(oi, o, 64);
-                            if (lane >= o) { zi += zy; oi += oy; }
-                        }
+                        const int gl = blk + lane;
+                        const u64 mkl = gl < ngrp ? pm[gl * 16 + i] : 0ull;
+                        const int ng = min(64, ngrp - blk);
                         if (i0 == 0 && wv == 0 && blk == 0) DTS(9);
-                        // lane j places the ranks of its own group j in order (no cross-lane
-                        // traffic: a shuffle-broadcast per group costs 4 LDS permutes)
-                        uint32_t zp = zbase + zi - zc, op = obase + oi - oc;
-                        const int r0 = g * 64;
-                        for (int e = 0; e < 64; ++e) {
-                            if (e < nr) {
-                                const bool one = (mk >> e) & 1ull;
-                                L[one ? op : zp] = (uint16_t)(r0 + e);
-                                op += one ? 1u : 0u;
-                                zp += one ? 0u : 1u;
-                            }
+                        for (int gg = 0; gg < ng; ++gg) {
+                            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mkl, gg);
+                            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mkl >> 32), gg);
+                            const u64 mk = (u64)lo | ((u64)hi << 32);
+                            const int g = blk + gg;
+                            const int nr = min(64, (int)m - g * 64);        // ranks in group g
+                            const u64 valid = nr >= 64 ? ~0ull : ((1ull << nr) - 1ull);
+                            const u64 zm = ~mk & valid;
+                            const bool one = (mk >> lane) & 1ull;
+                            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)((one ? mk : zm) >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)(one ? mk : zm), 0u));
+                            if (lane < nr) L[(one ? obase : zbase) + below] = (uint16_t)(g * 64 + lane);
+                            obase += (uint32_t)__popcll(mk);
+                            zbase += (uint32_t)__popcll(zm);
                         }
-                        zbase += __shfl(zi, 63, 64);
-                        obase += __shfl(oi, 63, 64);
                     }
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
@@ -1464,7 +1482,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
             if (sc > bsc || (sc == bsc && ix < bix)) { bsc = sc; bix = ix; }
         }
         if (t == 0 && fast_blocks) {
-            const u64 key = gkey[b];
+            const u64 key = key0;
             if (key) {
                 const uint32_t score = (uint32_t)(key >> 32);
                 const int ix = (int)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFu));
@@ -1489,38 +1507,54 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
         }
     }
 
+    __shared__ SliceWin Wsh;   // the fused embed's window cache, filled by thread 0 below
+    // ... and its segments in perm order: bit j belongs to the first k with j < seg_end[k];
+    // pixel = seg_q0[k] + j (mod npx), payload bit = seg_s0[k] + j
+    __shared__ int seg_end[16], seg_p[16], seg_q0[16], seg_s0[16];
     __syncthreads();   // lay_sh
     DTS(4);
-    if (t == 0) {   // ---- windows and the slice record (thread 0)
+    if (t < 64) {   // ---- windows and the slice record (wave 0: lane j = segment j in perm order)
+    const int lane = t;
+    const int sdec = ctl_sh[1];                    // thread 0's s (the wave path decides there)
+    const int bix0 = __shfl(bix, 0, 64);
+    const double cum0 = __shfl(cum, 0, 64);
     int offset = 0;
     if (P.fixed_offset >= 0) offset = P.fixed_offset;
-    else if (P.mode == CODEC_MODE_HYBRID) offset = (bix / nbx) * sb * P.W + (bix % nbx) * sb;
+    else if (P.mode == CODEC_MODE_HYBRID) offset = (bix0 / nbx) * sb * P.W + (bix0 % nbx) * sb;
     if (offset < 0 || (long long)offset >= npx) offset = 0;   // no block scored (never for valid stats)
 
-    // ---- segment windows (codec.py:455-485 / 288-316)
+    // ---- segment windows (codec.py:455-485 / 288-316).  The layout's perm is a permutation
+    // of the planes 0..s-1, so lane j < s owns plane perm[j] and lane p in [s, 16) plane p.
     const codec_layout& L = *reinterpret_cast<const codec_layout*>(lay_sh);
-    uint32_t flags = 0;
-    int pos = offset, cat = 0;
-    for (int j = 0; j < s; ++j) {
-        const int p = L.perm[j];
-        const int len = L.len[p];
-        const int n = (int)min((long long)len, npx);
-        if (len != L.sizes[p] || n != len) flags |= CODEC_FLAG_LOSSY;
-        M->perm[j] = p;
-        M->n[p] = n;
-        M->src[p] = L.src[p];
-        M->cat[p] = cat;
-        cat += n;
-        if (P.mode == CODEC_MODE_MULTI) {
-            M->off[p] = 0;
-            M->sizes[p] = n;                                   // codec.py:315
-        } else {
-            M->off[p] = pos;
-            M->sizes[p] = L.sizes[p];                          // codec.py:425,487
-            if (!P.align) pos = (int)(((long long)pos + n) % npx);
-        }
+    const bool segl = lane < sdec;
+    const int p = segl ? L.perm[lane] : (lane & 15);
+    const int len = segl ? L.len[p] : 0;
+    const int n = segl ? (int)min((long long)len, npx) : 0;
+    const bool lossy = segl && (len != L.sizes[p] || n != len);
+    int incl = n;                                    // segments are concatenated in perm order
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
     }
-    for (int p = s; p < 16; ++p) { M->perm[p] = -1; M->n[p] = 0; M->src[p] = 0; M->cat[p] = cat; M->off[p] = 0; M->sizes[p] = 0; }
+    const int catj = incl - n;                       // == the sequential loop's `cat` before j
+    const int cat = __shfl(incl, 15, 64);            // total (s <= 16)
+    // pos advances by n mod npx per segment (hybrid, not aligned): (offset + cat_j) mod npx
+    const int off = (!segl || P.mode == CODEC_MODE_MULTI) ? 0
+                  : P.align ? offset : (int)(((long long)offset + catj) % npx);
+    const int sz = !segl ? 0 : P.mode == CODEC_MODE_MULTI ? n : L.sizes[p];   // codec.py:315 / 425,487
+    if (lane < 16) {
+        M->perm[lane] = segl ? p : -1;
+        M->n[p] = n; M->src[p] = segl ? L.src[p] : 0; M->cat[p] = catj; M->off[p] = off; M->sizes[p] = sz;
+        M->mi[lane] = mis_sh[lane];
+    }
+    if (EMBED && segl) { seg_end[lane] = catj + n; seg_p[lane] = p; seg_q0[lane] = off - catj; seg_s0[lane] = L.src[p] - catj; }
+    int maxn = n;
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) maxn = max(maxn, __shfl_xor(maxn, o, 64));
+    uint32_t flags = __ballot(lossy) ? CODEC_FLAG_LOSSY : 0u;
+    if (lane == 0) {
+    const int s = sdec;
     if ((P.mode == CODEC_MODE_MULTI && s > 1) || (P.align && s > 1) || (long long)cat > npx) flags |= CODEC_FLAG_OVERLAP;
     if (!lut_ok) flags |= CODEC_FLAG_BADLUT;
     M->s = s;
@@ -1533,21 +1567,20 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
     M->nonzero_bins = (int)m;
     M->entropy = Hy;
     M->target = target;
-    M->cum_info = cum;
+    M->cum_info = cum0;
     {   // circular hull of the windows (lets a streaming pass skip untouched chunks cheaply)
-        int maxn = 0;
-        for (int p = 0; p < s; ++p) maxn = max(maxn, M->n[p]);
         const bool shared_start = (P.mode == CODEC_MODE_MULTI) || P.align;
-        const long long len = shared_start ? maxn : cat;
+        const long long hl = shared_start ? maxn : cat;
         M->span_lo = (P.mode == CODEC_MODE_HYBRID) ? offset : 0;
-        M->span_len = (int)min(len, npx);
+        M->span_len = (int)min(hl, npx);
     }
-    for (int i = 0; i < 16; ++i) M->mi[i] = mis_sh[i];
+    if constexpr (EMBED) { Wsh.s = s; Wsh.tot = cat; Wsh.npix = (int)npx; Wsh.flags = flags; }
     DTS(5);
     }
+    }
     if constexpr (EMBED) {
-        __shared__ SliceWin W;
-        load_win(M, &W);                      // thread 0 wrote M; barrier inside
+        const SliceWin& W = Wsh;
+        __syncthreads();
         DTS(10);
         const T* cv = static_cast<const T*>(E.cover) + (size_t)b * npx;
         T* sv = static_cast<T*>(E.stego) + (size_t)b * npx;
@@ -1556,6 +1589,10 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
         // issued before any store (the stores may alias the cover, so a per-bit loop would
         // serialise one HBM round trip per bit)
         const int lim = min(W.tot, E.mw * 64);
+        // segment ends in registers (a linear search per bit instead of dependent LDS reads)
+        int ends[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) ends[k] = k < W.s ? seg_end[k] : 0x7FFFFFFF;
         for (int j0 = 0; j0 < lim; j0 += 8 * 1024) {
             int pl[8];
             long long ql[8];
@@ -1565,11 +1602,13 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
                 const int j = j0 + k * 1024 + t;
                 pl[k] = -1;
                 if (j < lim) {
-                    const int p = plane_of(W, j);
-                    const int i = j - W.cat[p];
-                    long long q = (long long)W.off[p] + i;
+                    int sg = 0;
+#pragma unroll
+                    for (int kk = 0; kk < 16; ++kk) sg += j >= ends[kk] ? 1 : 0;
+                    const int p = seg_p[sg];
+                    long long q = (long long)seg_q0[sg] + j;
                     if (q >= npx) q -= npx;
-                    const long long sbit = (long long)W.src[p] + i;
+                    const long long sbit = (long long)seg_s0[sg] + j;
                     pl[k] = p;
                     ql[k] = q;
                     mb[k] = (uint32_t)((pay_in_lds ? pay_sh[sbit >> 6] : pay[sbit >> 6]) >> (sbit & 63)) & 1u;

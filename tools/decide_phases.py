@@ -44,6 +44,9 @@ def main():
         np.median(raw[:, 8] - raw[:, 2]) * 0.01, np.median(raw[:, 9] - raw[:, 8]) * 0.01,
         np.median(w0[:, 1] - raw[:, 9]) * 0.01, np.median(w0[:, 0] - w0[:, 1]) * 0.01,
         np.median(raw[:, 3] - w0[:, 0]) * 0.01))
+    print("pass1 split: loads+pops %.2f us, block scan %.2f us, pop reductions %.2f us" % (
+        np.median(raw[:, 12] - raw[:, 0]) * 0.01, np.median(raw[:, 13] - raw[:, 12]) * 0.01,
+        np.median(raw[:, 1] - raw[:, 13]) * 0.01))
     d = np.diff(t, axis=1)
     names = ["pass1+scan", "terms", "H(Y)+MI", "offset argmax", "windows/meta"]
     med = np.median(d, axis=0)
