@@ -364,69 +364,150 @@ __global__ __launch_bounds__(256) void k_pee_embed(const T* __restrict__ cover, 
 }
 
 // ---- capacity control.  The expansion safety test (p + 2e >= 0, p + 2e + 1 <= maxval)
-// does not depend on T, so one pass that histograms the prediction errors e in
-// [-tmax, tmax) of the candidates whose expansion would be safe gives every capacity
-// exactly: capacity(T) = sum of the bins e in [-T, T).  grid (regions, B), LDS bins per
-// workgroup, flushed with one global atomic per non-zero bin.
+// does not depend on T, so one pass that histograms the prediction errors of the
+// candidates whose expansion would be safe gives every capacity exactly: with u = e for
+// e >= 0 and -e - 1 for e < 0, e lies in [-T, T) iff u < T, so capacity(T) = sum of the
+// u-bins below T.  grid (regions, B), 256 threads.  The bins are lane-private LDS
+// counters (bin u of thread t at u * 256 + t: a wave's 64 lanes always hit 64 banks), so
+// an update is a plain read-add-write instead of an LDS atomic on a handful of hot bins
+// (the errors of a smooth slice crowd around 0: 64-way same-address atomics ran at
+// ~0.5 lane-ops per cycle); equal bins of a lane's 4 candidates are merged first.  The
+// workgroup's bins are reduced and added to the slice's global bins; the slice's last
+// workgroup (a per-slice arrival counter) turns them into the capacity curve and the
+// chosen T, and clears bins and counter (the workspace is zeroed once: no memset, no
+// second launch per call).
 #define PEE_TMAX_MAX 64
-template <typename T, bool VEC>
-__global__ __launch_bounds__(256) void k_pee_ehist(const T* __restrict__ img, int H, int W, int maxval, int tmax,
-                                                   int per_wg, uint32_t* __restrict__ hist_all) {
-    typedef typename Vec8<T>::type V;
-    __shared__ uint32_t bins[2 * PEE_TMAX_MAX];
-    const int b = blockIdx.y;
-    const T* src = img + (size_t)b * H * W;
-    for (int i = threadIdx.x; i < 2 * tmax; i += 256) bins[i] = 0;
-    __syncthreads();
-    const int wc = W / 2;
-    auto add = [&](int x, int a, int bb, int cc) {
-        const int p = med3(a, bb, cc), e = x - p;
-        if (e >= -tmax && e < tmax && p + 2 * e >= 0 && p + 2 * e + 1 <= maxval) atomicAdd(&bins[e + tmax], 1u);
-    };
-    if constexpr (VEC) {
-        const int CR = W / 8;
-        const int items = (H / 2) * CR;
-        const int i0 = blockIdx.x * per_wg, i1 = min(items, i0 + per_wg);
-        for (int it = i0 + threadIdx.x; it < i1; it += 256) {
-            const int r = it / CR, c = it - r * CR;
-            const size_t o0 = (size_t)(2 * r) * W + (size_t)c * 8;
-            const V v0 = *reinterpret_cast<const V*>(src + o0);
-            const V v1 = *reinterpret_cast<const V*>(src + o0 + W);
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                add((int)get_px(v1, 2 * q + 1), (int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1), (int)get_px(v0, 2 * q));
-        }
-    } else {
-        const int nc = (H / 2) * wc;
-        const int k0 = blockIdx.x * per_wg, k1 = min(nc, k0 + per_wg);
-        for (int k = k0 + threadIdx.x; k < k1; k += 256) {
-            int x, a, bb, cc;
-            pee_load(src, W, wc, k, &x, &a, &bb, &cc);
-            add(x, a, bb, cc);
-        }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < 2 * tmax; i += 256)
-        if (bins[i]) atomicAdd(&hist_all[(size_t)b * 2 * tmax + i], bins[i]);
-}
-
-// capacities at T = 1..tmax from the error histogram, and the smallest T whose capacity
-// holds the slice's payload (tmax if none does)
-__global__ __launch_bounds__(256) void k_pee_select(const uint32_t* __restrict__ hist_all, int tmax, int B,
-                                                    const int32_t* __restrict__ lengths, int32_t* __restrict__ caps,
-                                                    int32_t* __restrict__ t_out) {
-    const int b = blockIdx.x * 256 + threadIdx.x;
-    if (b >= B) return;
-    const uint32_t* h = hist_all + (size_t)b * 2 * tmax;
-    const long long L = lengths ? (long long)max(0, lengths[b]) : 0;
+__device__ __forceinline__ void pee_select_slice(uint32_t* h, int tmax, long long L, int32_t* caps, int32_t* t_out) {
     long long run = 0;
     int tsel = 0;
     for (int t = 1; t <= tmax; ++t) {
-        run += (long long)h[tmax - t] + h[tmax + t - 1];
-        if (caps) caps[(size_t)b * tmax + t - 1] = (int32_t)run;
+        run += (long long)__hip_atomic_load(h + t - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        h[t - 1] = 0u;
+        if (caps) caps[t - 1] = (int32_t)run;
         if (!tsel && run >= L) tsel = t;
     }
-    if (t_out) t_out[b] = tsel ? tsel : tmax;
+    if (t_out) *t_out = tsel ? tsel : tmax;
+}
+
+template <typename T, bool VEC>
+__global__ __launch_bounds__(256) void k_pee_ehist(const T* __restrict__ img, int H, int W, int maxval, int tmax,
+                                                   int per_wg, uint32_t* __restrict__ hist_all,
+                                                   uint32_t* __restrict__ arrivals, const int32_t* __restrict__ lengths,
+                                                   int32_t* __restrict__ caps, int32_t* __restrict__ t_out) {
+    typedef typename Vec8<T>::type V;
+    extern __shared__ uint32_t cnt[];                 // [tmax][256]
+    __shared__ uint32_t bins[PEE_TMAX_MAX];
+    const int b = blockIdx.y, tid = threadIdx.x;
+    const T* src = img + (size_t)b * H * W;
+    for (int u = 0; u < tmax; ++u) cnt[u * 256 + tid] = 0u;
+    if (tid < tmax) bins[tid] = 0u;
+    // the 4 candidates of one item (or 1 on the scalar path): bins merged, then one
+    // independent read-add-write per distinct bin (the lane's own counters only)
+    auto add4 = [&](const int (&x)[4], const int (&a)[4], const int (&bb)[4], const int (&cc)[4], int nq) {
+        int u[4];
+        uint32_t c[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int p = med3(a[q], bb[q], cc[q]), e = x[q] - p;
+            const int uq = e >= 0 ? e : -e - 1;
+            u[q] = uq;
+            c[q] = (q < nq) & (uq < tmax) & (p + 2 * e >= 0) & (p + 2 * e + 1 <= maxval) ? 1u : 0u;
+        }
+#pragma unroll
+        for (int q = 1; q < 4; ++q)
+#pragma unroll
+            for (int r = 0; r < q; ++r) {   // branch-free merge (& instead of &&)
+                const bool same = (c[r] != 0u) & (c[q] != 0u) & (u[r] == u[q]);
+                c[r] += same ? c[q] : 0u;
+                c[q] = same ? 0u : c[q];
+            }
+        uint32_t old[4];
+        int ad[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            ad[q] = min(u[q], tmax - 1) * 256 + tid;
+            old[q] = cnt[ad[q]];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (c[q]) cnt[ad[q]] = old[q] + c[q];   // masked: a merged duplicate must not write back
+    };
+    __syncthreads();
+    if constexpr (VEC) {
+        const uint32_t CR = (uint32_t)W / 8;
+        const uint32_t items = (uint32_t)(H / 2) * CR;
+        const uint32_t i0 = (uint32_t)blockIdx.x * (uint32_t)per_wg;
+        const uint32_t i1 = min(items, i0 + (uint32_t)per_wg);
+        const uint32_t dq = 256u / CR, dr = 256u % CR;
+        uint32_t it = i0 + (uint32_t)tid;
+        uint32_t r = it / CR, c = it - r * CR;             // advanced without divisions below
+        // 4 items per thread per step, their 8 loads issued together (one item at a time
+        // left each thread waiting a full HBM round trip per item); plain loads: the embed
+        // that follows reads the same cover, and at C3 size it is still in the MALL
+        constexpr int U = 4;
+        for (; it < i1; it += 256 * U) {
+            V v0[U], v1[U];
+            bool in[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                in[k] = it + 256u * k < i1;
+                const size_t o0 = in[k] ? (size_t)(2 * r) * W + (size_t)c * 8 : 0;
+                v0[k] = *reinterpret_cast<const V*>(src + o0);
+                v1[k] = *reinterpret_cast<const V*>(src + o0 + W);
+                c += dr;
+                r += dq;
+                if (c >= CR) { c -= CR; ++r; }
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                int x[4], a[4], bb[4], cc[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    x[q] = (int)get_px(v1[k], 2 * q + 1); a[q] = (int)get_px(v1[k], 2 * q);
+                    bb[q] = (int)get_px(v0[k], 2 * q + 1); cc[q] = (int)get_px(v0[k], 2 * q);
+                }
+                add4(x, a, bb, cc, in[k] ? 4 : 0);
+            }
+        }
+    } else {
+        const int wc = W / 2;
+        const int nc = (H / 2) * wc;
+        const int k0 = blockIdx.x * per_wg, k1 = min(nc, k0 + per_wg);
+        for (int k = k0 + tid; k < k1; k += 256) {
+            int x[4] = {0, 0, 0, 0}, a[4] = {0, 0, 0, 0}, bb[4] = {0, 0, 0, 0}, cc[4] = {0, 0, 0, 0};
+            pee_load(src, W, wc, k, &x[0], &a[0], &bb[0], &cc[0]);
+            add4(x, a, bb, cc, 1);
+        }
+    }
+    __syncthreads();
+    // bin u of the workgroup: thread t sums lanes t / tmax, + 256 / tmax ... of bin t % tmax
+    const int g = 256 / tmax;
+    if (tid < g * tmax) {
+        const int u = tid % tmax;
+        uint32_t sum = 0;
+        for (int l = tid / tmax; l < 256; l += g) sum += cnt[u * 256 + l];
+        if (sum) atomicAdd(&bins[u], sum);
+    }
+    __syncthreads();
+    // No __threadfence: on gfx950 an agent-scope release writes back the XCD's L2 (measured:
+    // 30 -> 180 us for this kernel at C3).  The bins' device-scope atomics are returning ones
+    // whose results are waited for, i.e. performed at the coherence point before the
+    // barrier, and so before this workgroup's arrival atomic; the last arrival then reads
+    // the bins with device-scope atomic loads.
+    if (tid < tmax && bins[tid]) {
+        const uint32_t prev = atomicAdd(&hist_all[(size_t)b * PEE_TMAX_MAX + tid], bins[tid]);
+        asm volatile("" ::"v"(prev));   // wait for the atomic's return
+    }
+    __shared__ uint32_t ticket;
+    __syncthreads();
+    if (tid == 0) ticket = atomicAdd(&arrivals[b], 1u);
+    __syncthreads();
+    if (ticket == gridDim.x - 1u && tid == 0) {   // the slice's last workgroup
+        const long long L = lengths ? (long long)max(0, lengths[b]) : 0;
+        pee_select_slice(hist_all + (size_t)b * PEE_TMAX_MAX, tmax, L, caps ? caps + (size_t)b * tmax : nullptr,
+                         t_out ? t_out + b : nullptr);
+        arrivals[b] = 0u;
+    }
 }
 
 // ---- decode-side cursor counts, wave per tile (W % 8 == 0): a tile's 256 items are 4 per
@@ -2055,7 +2136,7 @@ static PeeWs pee_ws(const codec_pee_params* P) {
     // capacity-control error histogram (codec_pee_capacity; cleared by that call)
     L.hist = align_up(L.diag + 16, 256);
     // slice-serial kernels: per-lane sink for stores that must not land (contents unused)
-    L.sink = align_up(L.hist + (size_t)P->B * 2 * PEE_TMAX_MAX * 4, 256);
+    L.sink = align_up(L.hist + (size_t)P->B * (PEE_TMAX_MAX + 1) * 4, 256);   // + per-slice arrival counters
     L.total = align_up(L.sink + SS_SINK_BYTES, 256);
     return L;
 }
@@ -2142,25 +2223,23 @@ int codec_pee_capacity(const codec_pee_params* P, const void* cover, int32_t tma
     if (workspace_bytes < L.total) return set_err(CODEC_EINVAL, "workspace too small");
     hipStream_t st = as_stream(stream);
     uint32_t* hist = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.hist);
-    HIP_TRY(hipMemsetAsync(hist, 0, (size_t)P->B * 2 * tmax * 4, st));
+    // no memset: bins and arrival counters are zero on entry (zeroed workspace; each slice's
+    // last workgroup clears them)
     const size_t va = P->bytes == 2 ? 16 : 8;
     const bool vec = (P->W % 8) == 0 && ((uintptr_t)cover % va) == 0;
     const long long units = vec ? (long long)(P->H / 2) * (P->W / 8) : (long long)(P->H / 2) * (P->W / 2);
     ProfScope prof(st, CODEC_K_PEE_CAPACITY);
-    if (units > 0) {
+    {   // launched even when there is nothing to count: the last workgroup writes caps / t_out
         const long long per = knob("CODEC_PEE_EHIST_PER_WG", 4096);
-        dim3 grid((unsigned)((units + per - 1) / per), (unsigned)P->B);
-#define PEH(TT, VV) hipLaunchKernelGGL((k_pee_ehist<TT, VV>), grid, dim3(256), 0, st, static_cast<const TT*>(cover), P->H, \
-                                       P->W, P->maxval, (int)tmax, (int)per, hist)
+        dim3 grid((unsigned)max(1LL, (units + per - 1) / per), (unsigned)P->B);
+        const size_t lds = (size_t)tmax * 256 * 4;   // lane-private counters
+        uint32_t* arrivals = hist + (size_t)P->B * PEE_TMAX_MAX;
+#define PEH(TT, VV) hipLaunchKernelGGL((k_pee_ehist<TT, VV>), grid, dim3(256), lds, st, static_cast<const TT*>(cover), P->H, \
+                                       P->W, P->maxval, (int)tmax, (int)per, hist, arrivals, lengths, caps, t_out)
         if (P->bytes == 2) { if (vec) PEH(uint16_t, true); else PEH(uint16_t, false); }
         else { if (vec) PEH(uint8_t, true); else PEH(uint8_t, false); }
 #undef PEH
         LAUNCH_CHECK("k_pee_ehist");
-    }
-    if (caps || t_out) {
-        hipLaunchKernelGGL(k_pee_select, dim3((unsigned)((P->B + 255) / 256)), dim3(256), 0, st, hist, (int)tmax, P->B,
-                           lengths, caps, t_out);
-        LAUNCH_CHECK("k_pee_select");
     }
     return 0;
 }

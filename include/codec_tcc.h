@@ -257,7 +257,8 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
  * caps[B][tmax] = exact capacity of slice b at T = 1..tmax (expandable candidates whose
  * expansion stays in [0, maxval]), t_out[B] = the smallest T <= tmax whose capacity holds
  * lengths[b] bits (tmax if none does: the embed then truncates, status 1).  caps or t_out
- * may be NULL (t_out needs lengths).  Uses the PEE workspace. */
+ * may be NULL (t_out needs lengths).  Uses the PEE workspace, which must have been zeroed
+ * once (its error bins are cleared at the end of every call, not at the start). */
 int codec_pee_capacity(const codec_pee_params* P, const void* cover, int32_t tmax, const int32_t* lengths,
                        int32_t* caps, int32_t* t_out, void* workspace, size_t workspace_bytes, void* stream);
 /* stego -> exact payload bits + restored cover.  cover_out == stego is allowed (in
