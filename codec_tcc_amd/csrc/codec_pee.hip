@@ -1601,7 +1601,12 @@ __device__ unsigned long long g_ss_trace[SS_TRACE_N];
 #endif
 #define SS_PAD_WORDS (21 * 1024)     // 84 KB of the CU's 160 KB: a second workgroup does not fit
 #define SS_PAY_WORDS (SS_PAD_WORDS / 2 - 1)   // the embed keeps payloads of up to 10 751 words in that pad
-#define SS_SINK_BYTES (SS_THREADS * 48)   // per lane: two 16-B pixel vectors + one 8-B word (+pad)
+// sink for stores that must not land: one 64-B slot per wave (two 16-B pixel vectors and one
+// 8-B word), shared by the wave's lanes -- a store instruction whose lanes all go to the sink
+// touches one line instead of 64 (per-lane slots made the extract's mostly-sunk payload-word
+// stores scatter over 64 lines per wave and chunk)
+#define SS_SINK_SLOT(b, tid) ((size_t)((b) * (SS_THREADS / 64) + ((tid) >> 6)) * 64)
+#define SS_SINK_BYTES(B) ((size_t)(B) * (SS_THREADS / 64) * 64)
 
 
 // wave-level primitives without LDS round trips (each __shfl is a ds_bpermute, ~100 cycles):
@@ -1730,8 +1735,8 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
     T* dst = stego + b * npx;
     const u64* payload = payload_all + (size_t)b * pw;
     u64* lm = lm_all + (size_t)b * lmw;
-    V* sink_v = reinterpret_cast<V*>(sink + (size_t)tid * 48);
-    u64* sink_w = reinterpret_cast<u64*>(sink + (size_t)tid * 48 + 32);
+    V* sink_v = reinterpret_cast<V*>(sink + SS_SINK_SLOT(b, tid));
+    u64* sink_w = reinterpret_cast<u64*>(sink + SS_SINK_SLOT(b, tid) + 32);
     u64* pay = reinterpret_cast<u64*>(ss_pad);   // PAY_LDS: the slice's payload words
     if (tid == 0) {
         s_end = -1;
@@ -1954,8 +1959,8 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
     T* dst = cover + b * npx;
     const u64* lm = lm_all + (size_t)b * lmw;
     u64* payload = payload_all + (size_t)b * pw;
-    V* sink_v = reinterpret_cast<V*>(sink + (size_t)tid * 48);
-    u64* sink_w = reinterpret_cast<u64*>(sink + (size_t)tid * 48 + 32);
+    V* sink_v = reinterpret_cast<V*>(sink + SS_SINK_SLOT(b, tid));
+    u64* sink_w = reinterpret_cast<u64*>(sink + SS_SINK_SLOT(b, tid) + 32);
     if (tid == 0) {
         s_carry[0] = s_carry[1] = 0ull;
         ss_pad[SS_PAD_WORDS - 1] = 0u;
@@ -2137,7 +2142,7 @@ static PeeWs pee_ws(const codec_pee_params* P) {
     L.hist = align_up(L.diag + 16, 256);
     // slice-serial kernels: per-lane sink for stores that must not land (contents unused)
     L.sink = align_up(L.hist + (size_t)P->B * (PEE_TMAX_MAX + 1) * 4, 256);   // + per-slice arrival counters
-    L.total = align_up(L.sink + SS_SINK_BYTES, 256);
+    L.total = align_up(L.sink + SS_SINK_BYTES(P->B), 256);
     return L;
 }
 
