@@ -1003,13 +1003,27 @@ struct SliceWin {
 };
 
 __device__ __forceinline__ void load_win(const codec_slice_meta* M, SliceWin* W) {
-    if (threadIdx.x == 0) {
-        W->s = M->s; W->tot = M->total_used; W->npix = M->npix; W->flags = M->flags;
-        for (int i = 0; i < 16; ++i) {
-            W->perm[i] = M->perm[i]; W->off[i] = M->off[i]; W->n[i] = M->n[i];
-            W->cat[i] = M->cat[i]; W->src[i] = M->src[i]; W->sizes[i] = M->sizes[i];
-        }
+    const int i = threadIdx.x;   // 16 threads, one plane each (independent loads, one round trip)
+    if (i < 16) {
+        W->perm[i] = M->perm[i]; W->off[i] = M->off[i]; W->n[i] = M->n[i];
+        W->cat[i] = M->cat[i]; W->src[i] = M->src[i]; W->sizes[i] = M->sizes[i];
+        if (i == 0) { W->s = M->s; W->tot = M->total_used; W->npix = M->npix; W->flags = M->flags; }
     }
+    __syncthreads();
+}
+
+// the windows in perm order for per-bit lookups: bit j lies in segment k = #(ends <= j),
+// plane seg_p[k], pixel seg_q0[k] + j (mod npx) -- 16 register-held ends and two
+// independent LDS reads per bit instead of plane_of's dependent search
+__device__ __forceinline__ void win_segments(const SliceWin& W, int* seg_p, int* seg_q0, int (&ends)[16]) {
+    const int k = threadIdx.x;
+    if (k < 16 && k < W.s) {
+        const int p = W.perm[k];
+        seg_p[k] = p;
+        seg_q0[k] = W.off[p] - W.cat[p];
+    }
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) ends[kk] = kk < W.s ? W.cat[W.perm[kk]] + W.n[W.perm[kk]] : 0x7FFFFFFF;
     __syncthreads();
 }
 
@@ -1944,7 +1958,10 @@ __device__ __forceinline__ void gather_body(const T* __restrict__ stego, long lo
                                             const codec_slice_meta* __restrict__ meta,
                                             u64* __restrict__ out, int pw, int b) {
     __shared__ SliceWin W;
+    __shared__ int seg_p[16], seg_q0[16];
     load_win(meta + b, &W);
+    int ends[16];
+    win_segments(W, seg_p, seg_q0, ends);
     const T* sv = stego + (size_t)b * npx;
     const int t = threadIdx.x;
     for (int j0 = 0; j0 < pw * 64; j0 += 8 * NTH) {
@@ -1956,11 +1973,12 @@ __device__ __forceinline__ void gather_body(const T* __restrict__ stego, long lo
             pl[k] = -1;
             v[k] = 0;
             if (j < W.tot) {
-                const int p = plane_of(W, j);
-                const int i = j - W.cat[p];
-                long long q = (long long)W.off[p] + i;
+                int sg = 0;
+#pragma unroll
+                for (int kk = 0; kk < 16; ++kk) sg += j >= ends[kk] ? 1 : 0;
+                long long q = (long long)seg_q0[sg] + j;
                 if (q >= npx) q -= npx;
-                pl[k] = p;
+                pl[k] = seg_p[sg];
                 v[k] = sv[q];
             }
         }
