@@ -74,7 +74,11 @@ PATHS = {"auto": {}, "onepass": {"CODEC_PEE_ONEPASS": "1"}, "twopass": {"CODEC_P
          "twopass_wave_tiles_1wg": {"CODEC_PEE_ONEPASS": "0", "CODEC_PEE_DCOUNT_W_WGS": "1"},
          # slice-serial single pass (the default for batches of >= one slice per CU), forced
          # on these small batches
-         "slice_serial": {"CODEC_PEE_SS": "1"}}
+         "slice_serial": {"CODEC_PEE_SS": "1"},
+         # ... with the payload read from global memory (wave-uniform scalar loads; the
+         # default stages it in LDS) and with the 4-deep ring in place (default 2)
+         "slice_serial_gpay": {"CODEC_PEE_SS": "1", "CODEC_PEE_SS_PAYLDS": "0"},
+         "slice_serial_d4": {"CODEC_PEE_SS": "1", "CODEC_PEE_SS_D": "4"}}
 
 
 @pytest.fixture(params=sorted(PATHS))
