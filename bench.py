@@ -498,6 +498,19 @@ def bench_c3(args, torch, dist, world, dev, rank):
     return res
 
 
+def bench_c4(args, torch, dist, world, rank, dev):
+    """BASELINE config C4 at N > 1: 256 x 512^2 ct12 slices per rank (2048 slices on 8 GPUs),
+    the MED-PEE step with capacity control and the RCCL all-gather of every slice's side
+    information + location-map prefix (PeeRecordExchange, overlapped with extract)."""
+    B, H, W = 256, 512, 512
+    covers = make_covers(torch, args.kind, B, H, W, dev, seed=3000 + rank * B)
+    res = {"workload": f"{args.kind} 512x512 uint16 x {B} slices/GPU x {world} GPUs (C4), MED-PEE T='auto' + "
+                       f"all-gather of side information and location maps"}
+    res.update(bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, exchange=True,
+                         steps=4 * args.steps, T="auto"))
+    return res
+
+
 def bench_c2(args, torch, dev, rank):
     """BASELINE config C2: ONE 2048^2 slice (a latency case), the MED-PEE step (single pass
     with flat slots over all XCDs at this batch size) and the LSB step, wall clock per step
@@ -564,6 +577,7 @@ def main():
         lsb["inplace"] = bench_lsb_inplace(args, torch, dist, world, dev, covers, B, H, W)
         quality = bench_quality(args, torch, covers, stego, B, H, W) if rank == 0 else None
         del stego
+    c4 = bench_c4(args, torch, dist, world, rank, dev) if (world > 1 and args.c3) else None
     c3 = bench_c3(args, torch, dist, world, dev, rank) if (rank == 0 and args.c3) else None
     c2 = bench_c2(args, torch, dev, rank) if (rank == 0 and args.c2 and world == 1) else None
 
@@ -596,6 +610,8 @@ def main():
             out["quality"] = quality
         if c3 is not None:
             out["c3"] = c3
+        if c4 is not None:
+            out["c4"] = c4
         if c2 is not None:
             out["c2"] = c2
         if args.cpu_seconds > 0 and world == 1:
