@@ -2191,6 +2191,29 @@ static int pee_check(const codec_pee_params* P) {
     return 0;
 }
 
+// up to three 8-byte-aligned regions zeroed by one launch (the look-back paths clear their
+// status words, meta records, location map or payload rows before the pass: one dispatch
+// instead of two or three hipMemsetAsync fills, which at C2 size cost more than the work)
+struct ZeroSpans {
+    u64* p[3];
+    size_t n[3];   // 8-byte words
+};
+__global__ __launch_bounds__(256) void k_zero_spans(ZeroSpans z) {
+    const size_t stride = (size_t)gridDim.x * 256;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+        for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < z.n[r]; i += stride) z.p[r][i] = 0ull;
+}
+static hipError_t pee_zero(hipStream_t st, void* a, size_t abytes, void* b = nullptr, size_t bbytes = 0,
+                           void* c = nullptr, size_t cbytes = 0) {
+    ZeroSpans z{{static_cast<u64*>(a), static_cast<u64*>(b), static_cast<u64*>(c)}, {abytes / 8, bbytes / 8, cbytes / 8}};
+    const size_t tot = z.n[0] + z.n[1] + z.n[2];
+    if (!tot) return hipSuccess;
+    const unsigned g = (unsigned)std::min<size_t>(1024, (tot + 1023) / 1024);
+    hipLaunchKernelGGL(k_zero_spans, dim3(g), dim3(256), 0, st, z);
+    return hipGetLastError();
+}
+
 // row H-1 of every slice, src -> dst (one strided 2-D copy)
 static hipError_t pee_copy_last_rows(const codec_pee_params* P, const void* src, void* dst, hipStream_t st) {
     const size_t row = (size_t)P->W * P->bytes, pitch = (size_t)P->H * row, off = (size_t)(P->H - 1) * row;
@@ -2342,9 +2365,8 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
     if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && onepass != 0) {
         u64* stw = reinterpret_cast<u64*>(static_cast<char*>(workspace) + L.st);
         uint32_t* ctl = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.ctl);
-        HIP_TRY(hipMemsetAsync(stw, 0, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4, st));
-        HIP_TRY(hipMemsetAsync(meta, 0, (size_t)P->B * sizeof(codec_pee_meta), st));
-        if (inplace) HIP_TRY(hipMemsetAsync(lm, 0, (size_t)P->B * P->lm_words * 8, st));
+        HIP_TRY(pee_zero(st, stw, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4, meta, (size_t)P->B * sizeof(codec_pee_meta),
+                         inplace ? lm : nullptr, inplace ? (size_t)P->B * P->lm_words * 8 : 0));
         ProfScope prof(st, CODEC_K_PEE_EMBED1);
         const int mode = flat ? PEE_MODE_FLAT | (knob("CODEC_PEE_FLAT_TICKET", 0) ? 0 : PEE_MODE_NOTICKET)
                               : (knob("CODEC_PEE_1P_CHUNK_MAJOR", 1) ? PEE_MODE_CMAJOR : 0) |
@@ -2478,12 +2500,11 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
         if ((P->H & 1) && !inplace) HIP_TRY(pee_copy_last_rows(P, stego, cover_out, st));
         return 0;
     }
-    HIP_TRY(hipMemsetAsync(payload_out, 0, (size_t)P->B * P->payload_words * 8, st));
     const bool flat = !inplace && P->B < 32 && P->B <= knob("CODEC_PEE_FLAT_MAXB", 7);
     if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && onepass != 0) {
         u64* stw = reinterpret_cast<u64*>(static_cast<char*>(workspace) + L.st);
         uint32_t* ctl = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.ctl);
-        HIP_TRY(hipMemsetAsync(stw, 0, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4, st));
+        HIP_TRY(pee_zero(st, payload_out, (size_t)P->B * P->payload_words * 8, stw, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4));
         ProfScope prof(st, CODEC_K_PEE_EXTRACT1);
         const int mode = flat ? PEE_MODE_FLAT | (knob("CODEC_PEE_FLAT_TICKET", 0) ? 0 : PEE_MODE_NOTICKET)
                               : (knob("CODEC_PEE_X_CHUNK_MAJOR", knob("CODEC_PEE_1P_CHUNK_MAJOR", 1)) ? PEE_MODE_CMAJOR : 0) |
@@ -2512,6 +2533,7 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
         if ((P->H & 1) && !inplace) HIP_TRY(pee_copy_last_rows(P, stego, cover_out, st));
         return 0;
     }
+    HIP_TRY(hipMemsetAsync(payload_out, 0, (size_t)P->B * P->payload_words * 8, st));
     {   // the single pass's look-back flag (codec_pee_extract_flag_offset) stays clear here
         uint32_t* ctl = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.ctl);
         HIP_TRY(hipMemsetAsync(ctl + 1, 0, 4, st));
