@@ -356,7 +356,8 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
     emb = next((k for k in ("k_pee_embed_ss", "k_pee_embed1", "k_pee_scan") if k in kern), None)
     ext = next((k for k in ("k_pee_extract_ss", "k_pee_extract1") if k in kern), None)
     res["embed_kernel"], res["extract_kernel"] = emb, ext
-    inst = {"k_pee_embed_ss": "<unsigned short, true, %s, 4, true>" % ("true" if inplace else "false"),
+    ss_d = os.environ.get("CODEC_PEE_SS_D", "2") if inplace else "4"   # ring depth (codec_pee.hip dispatch)
+    inst = {"k_pee_embed_ss": "<unsigned short, true, %s, %s, true>" % ("true" if inplace else "false", ss_d),
             "k_pee_extract_ss": "<unsigned short, true, %s, 4>" % ("true" if inplace else "false"),
             "k_pee_embed1": "<unsigned short, true, %s>" % ("true" if inplace else "false"),
             "k_pee_extract1": "<unsigned short, true, %s>" % ("true" if inplace else "false")}
