@@ -1011,59 +1011,80 @@ struct ExtractCount {
     }
 };
 
+// One look-back round reads LB_WIN windows of 64 predecessor words at once (one memory round
+// trip instead of LB_WIN): a chunk far from the slice's first one -- e.g. the 256 chunks of a
+// lone 2048^2 slice spread over all CUs, whose predecessors have all published aggregates but
+// few inclusive prefixes yet -- sums them in one round instead of one round per 64 chunks.
+#ifndef LB_WIN
+#define LB_WIN 4
+#endif
 template <typename F>
 __device__ uint32_t lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, uint32_t spin_max, const F& count,
                                  uint32_t* done = nullptr, uint32_t sat = 0) {
     const int lane = threadIdx.x & 63;
     uint32_t excl = 0;
-    int p = c - 1;
+    int p = c - 1;            // the highest predecessor not summed yet
     uint32_t spins = 0;
     for (;;) {
-        const int idx = p - lane;
-        u64 w = idx >= 0 ? lb_load(st + idx) : LB_INC;
-        uint32_t fl = (uint32_t)(w >> 62);
-        u64 inc = __ballot(fl == 2u);
-        const u64 notready = __ballot(fl == 0u);
-        int first = inc ? (int)__builtin_ctzll(inc) : 64;                // nearest inclusive
-        u64 need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);       // lanes 0..first
-        if (notready & need) {
-            if (done && ld_agent(done)) return sat;
-            if (++spins <= spin_max) {
-                __builtin_amdgcn_s_sleep(PEE_LB_SLEEP);
-                continue;
-            }
-            if constexpr (!F::can) {
-                *timeout = true;
-                return excl;
-            } else {
-                // the missing aggregates from the pixels, one chunk per round of the wave; a
-                // chunk that published meanwhile keeps its own word (CAS from 0 only)
-                u64 m = notready & need;
-                while (m) {
-                    const int l = (int)__builtin_ctzll(m);
-                    m &= m - 1ull;
-                    const uint32_t a = count(p - l);
-                    if (lane == l) {
-                        const u64 mine = LB_AGG | (u64)a;
-                        atomicCAS(reinterpret_cast<unsigned long long*>(st + idx), 0ull, (unsigned long long)mine);
-                        w = mine;
-                        fl = 1u;
-                    }
-                }
-                *fallback = true;
-                spins = 0;
-            }
-        }
-        uint32_t v = lane <= first ? (uint32_t)w : 0u;
+        u64 wv[LB_WIN];
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-        excl += v;
-        if (first < 64) return excl;
-        // embed (done != nullptr): a partial sum that already reaches `sat` (= L) places the
-        // chunk past `end`; the caller only compares the prefix with L, and publishes it as a
-        // saturated inclusive value, as the done-flag path does
-        if (done && excl >= sat) return excl;
-        p -= 64;
+        for (int r = 0; r < LB_WIN; ++r) {
+            const int idx = p - 64 * r - lane;
+            wv[r] = idx >= 0 ? lb_load(st + idx) : LB_INC;
+        }
+        bool reload = false;
+#pragma unroll
+        for (int r = 0; r < LB_WIN; ++r) {   // the windows in order, from the loaded words
+            const int pr = p - 64 * r;       // this window's top predecessor
+            const int idx = pr - lane;
+            u64 w = wv[r];
+            uint32_t fl = (uint32_t)(w >> 62);
+            const u64 inc = __ballot(fl == 2u);
+            const u64 notready = __ballot(fl == 0u);
+            const int first = inc ? (int)__builtin_ctzll(inc) : 64;        // nearest inclusive
+            const u64 need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);  // lanes 0..first
+            if (notready & need) {
+                if (done && ld_agent(done)) return sat;
+                if (++spins <= spin_max) {
+                    __builtin_amdgcn_s_sleep(PEE_LB_SLEEP);
+                    p = pr;                  // reload from this window
+                    reload = true;
+                    break;
+                }
+                if constexpr (!F::can) {
+                    *timeout = true;
+                    return excl;
+                } else {
+                    // the missing aggregates from the pixels, one chunk per round of the wave; a
+                    // chunk that published meanwhile keeps its own word (CAS from what was read)
+                    u64 m = notready & need;
+                    while (m) {
+                        const int l = (int)__builtin_ctzll(m);
+                        m &= m - 1ull;
+                        const uint32_t a = count(pr - l);
+                        if (lane == l) {
+                            const u64 mine = LB_AGG | (u64)a;
+                            atomicCAS(reinterpret_cast<unsigned long long*>(st + idx), (unsigned long long)w,
+                                      (unsigned long long)mine);
+                            w = mine;
+                            fl = 1u;
+                        }
+                    }
+                    *fallback = true;
+                    spins = 0;
+                }
+            }
+            uint32_t v = lane <= first ? (uint32_t)w : 0u;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+            excl += v;
+            if (first < 64) return excl;
+            // embed (done != nullptr): a partial sum that already reaches `sat` (= L) places the
+            // chunk past `end`; the caller only compares the prefix with L, and publishes it as a
+            // saturated inclusive value, as the done-flag path does
+            if (done && excl >= sat) return excl;
+        }
+        if (!reload) p -= 64 * LB_WIN;
     }
 }
 
