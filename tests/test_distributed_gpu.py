@@ -1,0 +1,102 @@
+"""world_size-2 exchange test on the GPU (gloo, both ranks on cuda:0): the real kernels'
+records go through the stream-overlapped exchanges the multi-GPU bench uses -- `mark()`
+right after the embed, `start()` on the side stream while the extract runs on the launch
+stream, `join()` -- with uneven shards (5 slices = 3 + 2).  Every rank recomputes the whole
+batch locally and checks that the gathered MED-PEE side information and location-map
+prefixes equal it row for row, and the LSB records of its own rows."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _covers(n, h, w, dev):
+    from codec_tcc_amd import synth
+    return torch.from_numpy(np.stack([synth.GENERATORS["ct12"](h, w, 60 + i) for i in range(n)])).to(dev)
+
+
+def _worker(rank, world, port, n, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    ok = True
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import codec_tcc_amd as ct
+        from codec_tcc_amd import _lib, framing, synth
+        from codec_tcc_amd import distributed as D
+        from codec_tcc_amd.pee import PeeCodec
+        H = W = 256
+        allc = _covers(n, H, W, dev)
+        pays = [framing.to_bits(synth.payload(96, 500 + g)) for g in range(n)]
+        lo, hi = D.shard_range(n, world, rank)
+        B = hi - lo
+        # ---- MED-PEE: the whole batch locally (reference rows), then this rank's shard
+        full = PeeCodec(n, H, W, dtype="uint16", T=2, device=dev)
+        ref = full.embed(allc, pays)
+        codec = PeeCodec(B, H, W, dtype="uint16", T=2, device=dev)
+        enc = codec.embed(allc[lo:hi].contiguous(), pays[lo:hi], check=False)
+        xch = D.PeeRecordExchange(B, world, dev, n_total=n)
+        xch.mark()                                   # records final on the launch stream
+        xch.start(enc.meta, enc.lm)                  # side stream ...
+        words, cover = codec.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words)
+        gmeta, glm = xch.join()                      # ... joined after the extract was queued
+        torch.cuda.synchronize()
+        ok &= bool(torch.equal(cover.view(torch.int16), allc[lo:hi].view(torch.int16)))
+        ok &= tuple(gmeta.shape) == (n, _lib.PEE_META_BYTES)
+        ok &= bool(torch.equal(gmeta, ref.meta))
+        recs = ref.records()
+        for g in range(n):
+            nw = (recs[g].end + 1 + 63) // 64
+            ok &= nw <= glm.shape[1] and bool(torch.equal(glm[g, :nw], ref.lm[g, :nw]))
+        # ---- LSB records: own rows of the gathered records equal the local packing
+        lcodec = ct.Codec(B, H, W, dtype="uint16", beta=0.4, block=16, device=dev)
+        pl = ct.make_payloads([synth.payload(96, 700 + g) for g in range(lo, hi)], dev)
+        lenc = lcodec.encode(allc[lo:hi].contiguous(), pl)
+        rx = D.RecordExchange(B, pl.map_words, world, dev, n_total=n)
+        rx.mark()
+        rx.start(lenc.meta, lenc.maps)
+        w2, c2 = lcodec.decode(lenc.stego, lenc.maps, lenc.meta, payload_words=pl.payload_words,
+                               map_words=pl.map_words)
+        allrec = rx.join()
+        torch.cuda.synchronize()
+        ok &= bool(torch.equal(c2.view(torch.int16), allc[lo:hi].view(torch.int16)))
+        ok &= allrec.shape[0] == n
+        mine = D.pack_records(lenc.meta, lenc.maps, out=torch.zeros((B, allrec.shape[1]), dtype=torch.int64,
+                                                                      device=dev))
+        ok &= bool(torch.equal(rx.own_rows(rank), mine))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - reported through the queue
+        q.put((rank, False, repr(e)))
+        return
+    q.put((rank, bool(ok), ""))
+
+
+def test_exchanges_on_gpu_streams_world2():
+    import torch.multiprocessing as mp
+    world, n = 2, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=110) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+    assert all(ok for _r, ok, _e in res), res
