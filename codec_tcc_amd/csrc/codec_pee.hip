@@ -1162,6 +1162,20 @@ __host__ __device__ __forceinline__ uint32_t pee_total_slots(int B, int nchunks,
 // place) or flag the slice (in place).
 // diag[0] / diag[2]: chunks whose look-back used the pixel fallback / timed out unrecovered
 // (cumulative since the workspace was zeroed; codec_pee_diag_offset).
+// diagnostic build only (tools/lb_trace.py, -DPEE_LB_TRACE): thread 0 of every embed1
+// workgroup stamps its slot's phases into LDS; threads 0..7 write them out per slot
+#ifdef PEE_LB_TRACE
+#define LB_TRACE_SLOTS 4096
+__device__ unsigned long long g_lb_trace[LB_TRACE_SLOTS * 12];
+#define LB_STAMP(k)                                                                     \
+    do {                                                                                \
+        unsigned long long t_;                                                          \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");      \
+        if (tid == 0) lbt[k] = t_;                                                      \
+    } while (0)
+#else
+#define LB_STAMP(k) do { } while (0)
+#endif
 #define PEE_MODE_CMAJOR 1
 #define PEE_MODE_NOTICKET 2
 #define PEE_CTL_WORDS(B) (32 + 32 * (size_t)(B))
@@ -1179,6 +1193,11 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
     __shared__ uint32_t sh[8];
     __shared__ uint32_t s_v, s_excl;
     __shared__ uint32_t lm32[4 * PEE_TILE / 32];
+    __shared__ u64 s_pay[192];   // the slice's payload words when pw <= 192 (see below)
+    const bool pay_st = pw <= 192;
+#ifdef PEE_LB_TRACE
+    __shared__ unsigned long long lbt[12];
+#endif
     const int CR = W / 8;
     const uint32_t items = (uint32_t)(H / 2) * (uint32_t)CR;
     const int nc = (H / 2) * (W / 2);
@@ -1190,6 +1209,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
     for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
         int b, j;
         if (!pee_slot(v, B, nchunks, g8, &b, &j)) continue;   // uniform; no barrier passed
+        LB_STAMP(0);
         uint32_t* tick = ctl + 32 + 32 * (size_t)b;
         u64* st = status_all + (size_t)b * nchunks;
         const uint32_t L = (uint32_t)max(0, lengths[b]);
@@ -1232,6 +1252,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
         }
         if (tid < 4 * PEE_TILE / 32) lm32[tid] = 0;
         lds_barrier();
+        LB_STAMP(1);
         const uint32_t cv = s_v;
         if (INPLACE) {
             if (cv == PEE_STOP) return;
@@ -1253,7 +1274,12 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                 const int w = c * (4 * PEE_TILE / 64) + tid;
                 if (w < lmw) lm_all[(size_t)b * lmw + w] = 0;
             }
+            LB_STAMP(5);
             lds_barrier();
+#ifdef PEE_LB_TRACE
+            if (tid < 12 && v < LB_TRACE_SLOTS) g_lb_trace[v * 12 + tid] = (tid == 0 || tid == 1 || tid == 5) ? lbt[tid] : (tid == 10 ? 1ull : (unsigned long long)c);
+            lds_barrier();
+#endif
             continue;
         }
         uint32_t esm = 0, safem = 0, rightm = 0;   // bit 4u+q
@@ -1279,6 +1305,13 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
         const u64 pex = block_excl_scan64_lds<256>(packed, sh64, &ptot);
         const uint32_t agg = (uint32_t)((ptot & 0xFFFFu) + ((ptot >> 16) & 0xFFFFu) + ((ptot >> 32) & 0xFFFFu) + (ptot >> 48));
         const bool publish = !(b == 0 && c == dbg_skip);
+        LB_STAMP(2);
+        // waves 1-3 (idle during wave 0's look-back) fetch the payload words into LDS meanwhile:
+        // a dependent global round trip after the look-back is then an LDS read, and wave 0's
+        // look-back loads -- the chain every later chunk waits on -- never wait behind them
+        // (vmcnt is per wave).  Loading them in wave 0 too, before the look-back, slowed it.
+        u64 pwv = 0;
+        if (pay_st && tid >= 64) pwv = payload_all[(size_t)b * pw + min(tid - 64, pw - 1)];
         if (c == 0) {
             if (tid == 0) { if (publish) lb_store(st, LB_INC | (u64)agg); s_excl = 0; }
         } else {
@@ -1297,7 +1330,9 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                 }
             }
         }
+        if (pay_st && tid >= 64 && tid - 64 < pw) s_pay[tid - 64] = pwv;
         lds_barrier();
+        LB_STAMP(3);
         const uint32_t excl = s_excl;
         const bool last = c == nchunks - 1;
         if (tid == 0) {
@@ -1315,6 +1350,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
             if (last && excl + agg < L) { M->end = nc - 1; M->tile_end = ntiles - 1; atomicMax(&M->status, 1); }
         }
         lds_barrier();   // lm32 zeroing vs the ORs below
+        LB_STAMP(6);
         if (excl < L) {   // some candidate of this chunk is active
             uint32_t base = excl;
             uint32_t unsafe_n = 0;
@@ -1331,44 +1367,63 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                 const uint32_t n = (uint32_t)((packed >> (16 * u)) & 0xFFFFu);
                 const uint32_t w = rs[u] >> 6;
                 const bool any = n && rs[u] < L;
-                plo[u] = any ? payload[w] : 0ull;
-                phi[u] = (any && (rs[u] & 63u) + n > 64u && (int)w + 1 < pw) ? payload[w + 1] : 0ull;
+                const bool two = any && (rs[u] & 63u) + n > 64u && (int)w + 1 < pw;
+                plo[u] = any ? (pay_st ? s_pay[w] : payload[w]) : 0ull;
+                phi[u] = two ? (pay_st ? s_pay[w + 1] : payload[w + 1]) : 0ull;
             }
+            // the payload words are waited for here, once: their uses sit in the divergent
+            // candidate branches below, where hipcc otherwise waited vmcnt(0) lgkmcnt(0) --
+            // i.e. for every store this chunk had issued -- at each use (~4 us per chunk)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                asm volatile("" ::"v"((uint32_t)plo[u]), "v"((uint32_t)(plo[u] >> 32)), "v"((uint32_t)phi[u]),
+                             "v"((uint32_t)(phi[u] >> 32)));
+            // branch-free per item (a divergent candidate loop with a global store inside cost
+            // ~4 us per chunk): this item's expandable candidates take ranks [rs, rs + n), the
+            // first m = min(L - rs, 4) of them carry bits, and candidate q is processed iff
+            // fewer than m expandable candidates precede it in the item
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const uint32_t it = (uint32_t)c * PEE_CHUNK + u * 256u + tid;
-                uint32_t r = rs[u];
-                const uint32_t r64 = rs[u] & ~63u;
-                if (it >= items) continue;
-                bool touched = false;
-                uint32_t nib = 0;
+                const bool ok = it < items;
+                const uint32_t eb = (esm >> (4 * u)) & 15u, sb = (safem >> (4 * u)) & 15u, rb = (rightm >> (4 * u)) & 15u;
+                const uint32_t rsu = rs[u];
+                const uint32_t mcnt = (ok & (rsu < L)) ? min(L - rsu, 4u) : 0u;
+                const uint32_t o = rsu & 63u;
+                const u64 field = o ? ((plo[u] >> o) | (phi[u] << (64u - o))) : plo[u];
+                uint32_t procm = 0, nib = 0;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const uint32_t bit = 1u << (4 * u + q);
-                    if (r >= L) break;                     // past `end` (ranks only grow)
+                    const uint32_t bit = 1u << q;
+                    const uint32_t pre = (uint32_t)__popc(eb & (bit - 1u));
+                    const bool proc = pre < mcnt;
+                    procm |= proc ? bit : 0u;
+                    nib |= (proc & !(sb & bit)) ? bit : 0u;
                     const int x = (int)get_px(a1[u], 2 * q + 1);
-                    const int k = (int)(4 * it) + q;
-                    touched = true;
-                    if (!(safem & bit)) { nib |= 1u << q; ++unsafe_n; continue; }
-                    int nv;
-                    if (esm & bit) {
-                        const int p = med3((int)get_px(a1[u], 2 * q), (int)get_px(a0[u], 2 * q + 1), (int)get_px(a0[u], 2 * q));
-                        const uint32_t o = r - r64;        // < 64 + 4
-                        const int pb = (int)(((o < 64u ? plo[u] >> o : phi[u] >> (o - 64u))) & 1ull);
-                        nv = p + 2 * (x - p) + pb;
-                        if (r == L - 1) { M->end = k; M->tile_end = k / PEE_TILE; }   // status stays 0 (memset)
-                        ++r;
-                    } else {
-                        nv = (rightm & bit) ? x + Tthr : x - Tthr;
-                    }
+                    const int pr = med3((int)get_px(a1[u], 2 * q), (int)get_px(a0[u], 2 * q + 1), (int)get_px(a0[u], 2 * q));
+                    const int nv_e = 2 * x - pr + (int)((field >> pre) & 1ull);   // p + 2e + bit
+                    const int nv_s = (rb & bit) ? x + Tthr : x - Tthr;
+                    const int nv = (proc & ((sb & bit) != 0u)) ? ((eb & bit) ? nv_e : nv_s) : x;
                     set_px(a1[u], 2 * q + 1, (uint32_t)nv);
                 }
-                if (nib) atomicOr(&lm32[u * 32 + (tid >> 3)], nib << (4 * (tid & 7)));
-                if (INPLACE && touched) stv<NT>(reinterpret_cast<V*>(dst + o0[u] + W), a1[u]);
+                unsafe_n += (uint32_t)__popc(nib);
+                // the item holding rank L - 1 (1 <= L - rs <= n): `end` is its last processed
+                // expandable candidate (status stays 0: zeroed before the pass)
+                if (mcnt != 0u && L - rsu <= (uint32_t)__popc(eb)) {
+                    const int k = (int)(4 * it) + 31 - __clz(procm & eb);
+                    M->end = k;
+                    M->tile_end = k / PEE_TILE;
+                }
+                if (nib) __hip_atomic_fetch_or(&lm32[u * 32 + (tid >> 3)], nib << (4 * (tid & 7)), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (INPLACE && procm) stv<NT>(reinterpret_cast<V*>(dst + o0[u] + W), a1[u]);
             }
+            LB_STAMP(7);
             const uint32_t nun = block_sum_u32_lds<256>(unsafe_n, sh);   // also orders the lm32 ORs
+            LB_STAMP(8);
             if (tid == 0 && nun) atomicAdd(&M->lm_count, (int)nun);
         }
+        LB_STAMP(4);
         if (tid == 0) {   // `end` is in this chunk (or there is none): later chunks need no cursor
             const bool fin = (excl < L && excl + agg >= L) || (L == 0 && c == 0) || (last && excl + agg < L);
             if (fin) {
@@ -1393,7 +1448,12 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                 if (w < lmw) lm_all[(size_t)b * lmw + w] = (u64)lm32[2 * tid] | ((u64)lm32[2 * tid + 1] << 32);
             }
         }
+        LB_STAMP(5);
         lds_barrier();
+#ifdef PEE_LB_TRACE
+        if (tid < 12 && v < LB_TRACE_SLOTS) g_lb_trace[v * 12 + tid] = tid < 10 ? lbt[tid] : (tid == 10 ? 0ull : (unsigned long long)c);
+        lds_barrier();
+#endif
     }
 }
 
@@ -1471,11 +1531,18 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
         if (c <= cend) {
             uint32_t actm = 0, innm = 0;
             u64 packed = 0;
+            if (!noticket) {   // the map words of the ticketed chunk, all four in flight at once
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t it = min((uint32_t)c * PEE_CHUNK + u * 256u + tid, items - 1u);
+                    lwv[u] = lm[(4 * it) >> 6];
+                }
+            }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const uint32_t it = (uint32_t)c * PEE_CHUNK + u * 256u + tid;
                 if (it >= items) continue;
-                const u64 lw = (noticket ? lwv[u] : lm[(4 * it) >> 6]) >> ((4 * it) & 63);   // 4 bits, same word
+                const u64 lw = lwv[u] >> ((4 * it) & 63);   // 4 bits, same word
                 uint32_t n = 0;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -1520,35 +1587,30 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
             for (int u = 0; u < 4; ++u) {
                 uint32_t r = base + (uint32_t)((pex >> (16 * u)) & 0xFFFFu);
                 base += (uint32_t)((ptot >> (16 * u)) & 0xFFFFu);
-                if (!((actm >> (4 * u)) & 0xFu)) continue;
-                u64 word = 0;
-                int wi = -1;
+                // branch-free per item: the item's inner candidates take ranks [r, r + n), n <= 4;
+                // their bits are gathered into one nibble and OR-ed into at most two words
+                const uint32_t am = (actm >> (4 * u)) & 0xFu, im = (innm >> (4 * u)) & 0xFu;
+                uint32_t bits = 0;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const uint32_t bit = 1u << (4 * u + q);
-                    if (!(actm & bit)) continue;
+                    const uint32_t bit = 1u << q;
                     const int x = (int)get_px(a1[u], 2 * q + 1);
                     const int p = med3((int)get_px(a1[u], 2 * q), (int)get_px(a0[u], 2 * q + 1), (int)get_px(a0[u], 2 * q));
                     const int e2 = x - p;
-                    int nx;
-                    if (innm & bit) {
-                        if (e2 & 1) {
-                            if (wi != (int)(r >> 6)) {
-                                if (wi >= 0) atomicOr(&pbuf[wi - w0], word);
-                                wi = (int)(r >> 6);
-                                word = 0;
-                            }
-                            word |= 1ull << (r & 63);
-                        }
-                        ++r;
-                        nx = p + (e2 >> 1);
-                    } else {
-                        nx = e2 >= 2 * Tthr ? x - Tthr : x + Tthr;
-                    }
-                    set_px(a1[u], 2 * q + 1, (uint32_t)nx);
+                    const bool inner = (im & bit) != 0u;
+                    bits |= (inner ? (uint32_t)(e2 & 1) : 0u) << __popc(im & (bit - 1u));
+                    const int nx = inner ? p + (e2 >> 1) : (e2 >= 2 * Tthr ? x - Tthr : x + Tthr);
+                    set_px(a1[u], 2 * q + 1, (uint32_t)((am & bit) ? nx : x));
                 }
-                if (wi >= 0 && word) atomicOr(&pbuf[wi - w0], word);
-                if (INPLACE) stv<NT>(reinterpret_cast<V*>(dst + o0[u] + W), a1[u]);
+                if (bits) {
+                    const uint32_t o = r & 63u;
+                    const int wl = (int)(r >> 6) - w0;
+                    __hip_atomic_fetch_or(&pbuf[wl], (u64)bits << o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (o > 60u && (bits >> (64u - o)))
+                        __hip_atomic_fetch_or(&pbuf[wl + 1], (u64)(bits >> (64u - o)), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                if (INPLACE && am) stv<NT>(reinterpret_cast<V*>(dst + o0[u] + W), a1[u]);
             }
             // one store per payload word instead of a global atomic per item: words wholly
             // inside [excl, excl + agg) belong to this chunk alone; the first and last may be
@@ -2254,6 +2316,12 @@ size_t codec_pee_extract_flag_offset(const codec_pee_params* P) {
     return pee_ws(P).ctl + 4;   // ctl[1]: set when an extract chunk's look-back gave up
 }
 
+#ifdef PEE_LB_TRACE
+int codec_debug_lb_trace(unsigned long long* out, int n) {   // diagnostic build only
+    if (n > LB_TRACE_SLOTS * 12) n = LB_TRACE_SLOTS * 12;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lb_trace), (size_t)n * 8) == hipSuccess ? n : -1;
+}
+#endif
 #ifdef PEE_SS_TRACE
 int codec_debug_ss_trace(unsigned long long* out, int n) {   // diagnostic build only
     if (n > SS_TRACE_N) n = SS_TRACE_N;
