@@ -18,6 +18,7 @@ MODE_MULTI = 1
 FLAG_OVERLAP = 1
 FLAG_LOSSY = 2
 FLAG_BADLUT = 4
+FLAG_DECIDE_TIMEOUT = 8   # split decision: a plane workgroup never reported (status 2)
 
 I16 = C.c_int32 * MAX_PLANES
 D16 = C.c_double * MAX_PLANES

@@ -79,20 +79,14 @@ __device__ uint32_t block_excl_scan(uint32_t x, uint32_t* sh, uint32_t* total) {
     const uint32_t inc = wave_incl_scan(x);
     if (lane == 63) sh[wv] = inc;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (int w = 0; w < NT / 64; ++w) {
-            const uint32_t tmp = sh[w];
-            sh[w] = acc;
-            acc += tmp;
-        }
-        sh[NT / 64] = acc;
-    }
-    __syncthreads();
-    const uint32_t r = sh[wv] + inc - x;
-    *total = sh[NT / 64];
-    __syncthreads();
-    return r;
+    // every wave scans the NT/64 wave totals itself (no serial pass by one thread, one
+    // barrier fewer)
+    const uint32_t wt = lane < NT / 64 ? sh[lane] : 0u;
+    const uint32_t wi = wave_incl_scan(wt);
+    const uint32_t pre = wv ? (uint32_t)__shfl(wi, wv - 1, 64) : 0u;
+    *total = (uint32_t)__shfl(wi, NT / 64 - 1, 64);
+    __syncthreads();   // sh reusable
+    return pre + inc - x;
 }
 
 // 64-bit variant (several packed 16-bit counters scanned at once); sh needs NT/64+1 words

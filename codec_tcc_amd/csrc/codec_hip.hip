@@ -120,6 +120,28 @@ __device__ __forceinline__ int np_node_size(int r, int d, int j, int* start) {
     return n;
 }
 
+// one chunk tree's internal nodes from its depth-7 slot sums (slot lane in vA, slot
+// lane + 64 in vB), bottom-up in numpy's order with shuffles; the chunk sum, in every lane
+__device__ __forceinline__ double np_combine_wave(double vA, double vB, int r) {
+    const int lane = threadIdx.x & 63;
+    // level 6: node j (lane j) = slots 2j, 2j+1 (lanes 2j, 2j+1 of vA for j < 32, of vB above)
+    const int s0 = (2 * lane) & 63;
+    const double lA = __shfl(vA, s0, 64), rA = __shfl(vA, s0 + 1, 64);
+    const double lB = __shfl(vB, s0, 64), rB = __shfl(vB, s0 + 1, 64);
+    int a6;
+    const int n6 = np_node_size(r, 6, lane, &a6);
+    const double L6 = lane < 32 ? lA : lB, R6 = lane < 32 ? rA : rB;
+    double v = n6 > NP_LEAF ? L6 + R6 : L6;
+    for (int d = 5; d >= 0; --d) {
+        const double L = __shfl(v, (2 * lane) & 63, 64);
+        const double R = __shfl(v, (2 * lane + 1) & 63, 64);
+        int ad;
+        const int nd = np_node_size(r, d, lane, &ad);
+        v = nd > NP_LEAF ? L + R : L;
+    }
+    return __shfl(v, 0, 64);
+}
+
 // np.sum semantics over any m, computed by ONE wave (no block barrier), so that 16 waves
 // can sum 16 different orders at once.  Per 8192-element buffer: the chunk's depth-7 tree
 // has 128 bottom slots, two per lane (slots lane and lane+64); a slot's leaf (numpy's
@@ -137,22 +159,7 @@ __device__ __forceinline__ double np_sum_wave(const F& f, int m) {
         const int nB = np_node_size(r, 7, lane + 64, &aB);
         const double vA = nA > 0 ? np_leaf(f, cs + aA, nA) : 0.0;
         const double vB = nB > 0 ? np_leaf(f, cs + aB, nB) : 0.0;
-        // level 6: node j (lane j) = slots 2j, 2j+1 (lanes 2j, 2j+1 of vA for j < 32, of vB above)
-        const int s0 = (2 * lane) & 63;
-        const double lA = __shfl(vA, s0, 64), rA = __shfl(vA, s0 + 1, 64);
-        const double lB = __shfl(vB, s0, 64), rB = __shfl(vB, s0 + 1, 64);
-        int a6;
-        const int n6 = np_node_size(r, 6, lane, &a6);
-        const double L6 = lane < 32 ? lA : lB, R6 = lane < 32 ? rA : rB;
-        double v = n6 > NP_LEAF ? L6 + R6 : L6;
-        for (int d = 5; d >= 0; --d) {
-            const double L = __shfl(v, (2 * lane) & 63, 64);
-            const double R = __shfl(v, (2 * lane + 1) & 63, 64);
-            int ad;
-            const int nd = np_node_size(r, d, lane, &ad);
-            v = nd > NP_LEAF ? L + R : L;
-        }
-        res += __shfl(v, 0, 64);
+        res += np_combine_wave(vA, vB, r);
     }
     return res;
 }
@@ -234,6 +241,59 @@ __device__ double np_sum_block1024(const F& f, int m, double* vals /*[1024]*/) {
     }
     __syncthreads();
     return np_tree_combine1024(m, vals);
+}
+
+// np_sum_block1024's leaves, then wave 0 alone re-adds the chunk trees with shuffles (no
+// block barriers: 14 fewer than np_tree_combine1024).  The sum is valid in wave 0 only.
+template <class F>
+__device__ double np_sum_block1024_w0(const F& f, int m, double* vals /*[1024]*/) {
+    const int t = threadIdx.x;
+    {
+        const int lane = t & 63, wv = t >> 6, q = lane & 7;
+        const int nchunks_ = (m + NP_CHUNK - 1) / NP_CHUNK;
+        for (int rnd = 0; rnd < nchunks_; ++rnd) {
+            const int slot = rnd * 128 + wv * 8 + (lane >> 3);
+            const int cs = rnd * NP_CHUNK;
+            const int rr = min(NP_CHUNK, max(0, m - cs));
+            int a = 0, n = 0;
+            if (rr > 0) n = np_node_size(rr, 7, slot & 127, &a);
+            a += cs;
+            const int lim = n - (n % 8);
+            double tv[NP_LEAF / 8];
+#pragma unroll
+            for (int u = 0; u < NP_LEAF / 8; ++u) tv[u] = (8 * u < lim) ? f(a + 8 * u + q) : 0.0;
+            double acc = 0.0;
+            if (n >= 8) {
+                acc = tv[0];
+#pragma unroll
+                for (int u = 1; u < NP_LEAF / 8; ++u)
+                    if (8 * u < lim) acc += tv[u];
+            }
+            const double s2 = acc + __shfl_xor(acc, 1, 64);
+            const double s4 = s2 + __shfl_xor(s2, 2, 64);
+            const double s8 = s4 + __shfl_xor(s4, 4, 64);
+            if (q == 0) {
+                double res;
+                if (n >= 8) {
+                    res = s8;
+                    for (int i = lim; i < n; ++i) res += f(a + i);
+                } else {
+                    res = -0.0;
+                    for (int i = 0; i < n; ++i) res += f(a + i);
+                }
+                vals[slot] = n > 0 ? res : 0.0;
+            }
+        }
+    }
+    __syncthreads();
+    double res = -0.0;
+    if (t < 64) {
+        for (int cs = 0; cs < m; cs += NP_CHUNK) {
+            const int c = cs / NP_CHUNK;
+            res += np_combine_wave(vals[c * 128 + t], vals[c * 128 + 64 + t], min(NP_CHUNK, m - cs));
+        }
+    }
+    return res;
 }
 
 // ---- wide slices (k_decide's walk path): the non-zero bins of a slice are kept as 64-bin
@@ -587,6 +647,7 @@ __device__ __forceinline__ void scan_fast_body(const T* __restrict__ cover, T* _
     constexpr uint32_t NPB = (uint32_t)SB * SB;
     __shared__ uint32_t lds[HistCfg<T>::kLdsWords];
     __shared__ u64 wkey;
+    __shared__ uint32_t wor;
     const int b = blockIdx.y;
     const size_t npx = (size_t)H * W;
     const T* src = cover + (size_t)b * npx;
@@ -594,7 +655,7 @@ __device__ __forceinline__ void scan_fast_body(const T* __restrict__ cover, T* _
     uint32_t* ghist = ghist_all + (size_t)b * HistCfg<T>::kBins;
 
     for (int i = threadIdx.x; i < HistCfg<T>::kLdsWords; i += 1024) lds[i] = 0;
-    if (threadIdx.x == 0) wkey = 0;
+    if (threadIdx.x == 0) { wkey = 0; wor = 0; }
     __syncthreads();
 
     const int nbands = (H + SB - 1) / SB;
@@ -623,24 +684,24 @@ __device__ __forceinline__ void scan_fast_body(const T* __restrict__ cover, T* _
             V* d = dst ? reinterpret_cast<V*>(dst + rowpix) : nullptr;
             const int stride = W / 8;   // vectors per row
             int r = 0;
-            for (; r + 4 <= rows; r += 4) {
-                V v0 = ldv<NT>(s + (size_t)(r + 0) * stride);
-                V v1 = ldv<NT>(s + (size_t)(r + 1) * stride);
-                V v2 = ldv<NT>(s + (size_t)(r + 2) * stride);
-                V v3 = ldv<NT>(s + (size_t)(r + 3) * stride);
+            // RB rows in flight per lane (the whole 16-row block column): a small batch has
+            // few busy waves (one band = W/8 lanes), so each lane's serial load rounds were its
+            // time (1 x 2048^2: 4 rounds of 4 rows, 18 us; the workgroup holds the CU's LDS
+            // alone, so the 64 data VGPRs cost no occupancy)
+            constexpr int RB = SB < 16 ? SB : 16;
+            for (; r + RB <= rows; r += RB) {
+                V v[RB];
+#pragma unroll
+                for (int k = 0; k < RB; ++k) v[k] = ldv<NT>(s + (size_t)(r + k) * stride);
                 if (d) {
-                    stv<NT>(d + (size_t)(r + 0) * stride, v0);
-                    stv<NT>(d + (size_t)(r + 1) * stride, v1);
-                    stv<NT>(d + (size_t)(r + 2) * stride, v2);
-                    stv<NT>(d + (size_t)(r + 3) * stride, v3);
+#pragma unroll
+                    for (int k = 0; k < RB; ++k) stv<NT>(d + (size_t)(r + k) * stride, v[k]);
                 }
-                ones += lsb_count(v0) + lsb_count(v1) + lsb_count(v2) + lsb_count(v3);
-                vor |= vor_of(v0) | vor_of(v1) | vor_of(v2) | vor_of(v3);
-                if constexpr (HIST) {
-                    hist_add8<T>(lds, ghist, v0);
-                    hist_add8<T>(lds, ghist, v1);
-                    hist_add8<T>(lds, ghist, v2);
-                    hist_add8<T>(lds, ghist, v3);
+#pragma unroll
+                for (int k = 0; k < RB; ++k) {
+                    ones += lsb_count(v[k]);
+                    vor |= vor_of(v[k]);
+                    if constexpr (HIST) hist_add8<T>(lds, ghist, v[k]);
                 }
             }
             for (; r < rows; ++r) {
@@ -671,10 +732,14 @@ __device__ __forceinline__ void scan_fast_body(const T* __restrict__ cover, T* _
     else vor = (vor | (vor >> 8) | (vor >> 16) | (vor >> 24)) & 0xFFu;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) vor |= __shfl_xor(vor, o, 64);
-    if (lane == 0 && vor) atomicOr(&gor[b], vor);
+    // one global OR per workgroup (a same-address global atomic per wave serialised)
+    if (lane == 0 && vor) atomicOr(&wor, vor);
     __syncthreads();
     hist_flush<T>(lds, ghist);
-    if (threadIdx.x == 0 && wkey) atomicMax(&gkey[b], wkey);
+    if (threadIdx.x == 0) {
+        if (wkey) atomicMax(&gkey[b], wkey);
+        if (wor) atomicOr(&gor[b], wor);
+    }
 }
 
 template <typename T, int SB, bool NT, bool HIST = true>
@@ -1054,10 +1119,15 @@ struct ListTerm {
 // per SIMD (8 put three on one SIMD: 33.4 -> 32.0 us per slice, tools/decide_phases.py)
 #define DECIDE_RP 7
 #endif
+// split decision: a plane workgroup's "no value" (a NaN bit pattern, never a real H(X,Y))
+#define PLANE_NONE 0x7FF8DEAD00000001ull
 #ifdef DECIDE_TS   // diagnostic build only (tools/decide_phases.py): phase timestamps into the term scratch
-#define DTS(k) do { if (threadIdx.x == 0) reinterpret_cast<long long*>(gterms + (size_t)blockIdx.x * HistCfg<T>::kBins)[HistCfg<T>::kBins - 16 + (k)] = wall_clock64(); } while (0)
+#define DTS(k) do { if (threadIdx.x == 0 && blockIdx.y == 0) reinterpret_cast<long long*>(gterms + (size_t)blockIdx.x * HistCfg<T>::kBins)[HistCfg<T>::kBins - 16 + (k)] = wall_clock64(); } while (0)
+// plane workgroups of the split decision: 4 stamps each below the main's 16
+#define PTS(k) do { if (threadIdx.x == 0) reinterpret_cast<long long*>(gterms + (size_t)blockIdx.x * HistCfg<T>::kBins)[HistCfg<T>::kBins - 80 + 4 * (blockIdx.y - 1) + (k)] = wall_clock64(); } while (0)
 #else
 #define DTS(k) do { } while (0)
+#define PTS(k) do { } while (0)
 #endif
 // CODEC_DECIDE_WAVES=0 (host env, passed in codec_params.reserved bit 0) forces the
 // block-sequential decision path (A/B and tests)
@@ -1088,6 +1158,22 @@ __device__ void build_joint_order(u64 nzmask, int v0, uint32_t rank0, int plane,
     __syncthreads();
 }
 
+// build_joint_order with one packed scan (zero counts low, one counts high): m < 65536
+__device__ void build_joint_order_m16(u64 nzmask, int v0, uint32_t rank0, int plane, uint16_t* list, uint32_t* sh) {
+    uint32_t oc = 0;
+    for (u64 msk = nzmask; msk; msk &= msk - 1) oc += ((v0 + __ffsll((long long)msk) - 1) >> plane) & 1;
+    const uint32_t zc = (uint32_t)__popcll(nzmask) - oc;
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan<1024>(zc | (oc << 16), sh, &tot);
+    uint32_t zp = ex & 0xFFFFu, op = (ex >> 16) + (tot & 0xFFFFu);
+    uint32_t r = rank0;
+    for (u64 msk = nzmask; msk; msk &= msk - 1, ++r) {
+        const int v = v0 + __ffsll((long long)msk) - 1;
+        if ((v >> plane) & 1) list[op++] = (uint16_t)r; else list[zp++] = (uint16_t)r;
+    }
+    __syncthreads();
+}
+
 // EMBED: codec_encode's fused path -- after thread 0 has written the slice's windows, the
 // workgroup embeds the slice's payload itself (k_embed's work, without its launch)
 struct EmbedArgs {
@@ -1107,7 +1193,8 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
                                                  const double* __restrict__ lut, long long lut_len,
                                                  const codec_layout* __restrict__ table,
                                                  const int32_t* __restrict__ slice_class,
-                                                 codec_slice_meta* __restrict__ meta_all, EmbedArgs E) {
+                                                 codec_slice_meta* __restrict__ meta_all, EmbedArgs E,
+                                                 u64* __restrict__ plane_slots, int nsplit) {
     constexpr int R = HistCfg<T>::kBins;
     // `list` doubles as the wave-parallel path's arena: terms (8m B), rank -> value (2m B),
     // one joint-order list per plane in flight (2m B each)
@@ -1128,6 +1215,10 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
 
     const int b = blockIdx.x;
     const int t = threadIdx.x;
+    // split decision (small batches, nsplit > 0): blockIdx.y = 0 is the slice's main
+    // workgroup; blockIdx.y = 1 + i computes plane i's joint entropy on its own CU and
+    // publishes it in plane_slots[16 b + i] (see the plane branch below)
+    const int role = blockIdx.y;
     const uint32_t* hist = ghist_all + (size_t)b * R;
     double* terms = gterms + (size_t)b * R;
     const long long npx = (long long)P.H * P.W;
@@ -1135,14 +1226,20 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
     codec_slice_meta* M = meta_all + b;
 
     DTS(0);
+    if (role > 0) PTS(0);
     // the scan's block key, loaded now (used by the offset argmax after the decision)
-    const u64 key0 = (t == 0 && fast_blocks && P.fixed_offset < 0 && P.mode == CODEC_MODE_HYBRID) ? gkey[b] : 0ull;
+    const u64 key0 = (t == 0 && role == 0 && fast_blocks && P.fixed_offset < 0 && P.mode == CODEC_MODE_HYBRID) ? gkey[b] : 0ull;
+    // the slice's layout class (its layout for s is loaded once s is known)
+    constexpr int kLayW = (int)(sizeof(codec_layout) / 4);
+    static_assert(16 * kLayW <= 1024, "one int of the class's layouts per thread");
+    const int cls = role == 0 ? slice_class[b] : 0;
+    const int32_t* lay_all = reinterpret_cast<const int32_t*>(table + (size_t)cls * 16);
     // fused embed: the slice's payload words (<= 2 KiB) go to LDS now, read by the embed
     // loop after the decision instead of one dependent global load per bit
     constexpr int kPaySh = EMBED ? 256 : 1;
     __shared__ u64 pay_sh[kPaySh];
     const bool pay_in_lds = EMBED && E.pw <= kPaySh;
-    if (EMBED && pay_in_lds)
+    if (EMBED && pay_in_lds && role == 0)
         for (int w = t; w < E.pw; w += 1024) pay_sh[w] = E.payload[(size_t)b * E.pw + w];
     // ---- bins that can be non-zero: [0, Rp), Rp = next power of two above OR(pixels)
     const uint32_t orv = gor[b];
@@ -1197,6 +1294,10 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
         const u64 w = nzs[v0 >> 6];
         nzmask = bpt == 64 ? w : (w >> (v0 & 63)) & ((1ull << bpt) - 1);
     }
+    // small value ranges (every 12-bit slice): the non-zero counts are kept in LDS (`vals`,
+    // free until the sums) for the terms pass, instead of a second histogram round trip
+    uint32_t* cnt_sh = reinterpret_cast<uint32_t*>(vals);
+    const bool cnt_lds = !wide && Rp <= (int)(sizeof(vals) / 4);
     for (int k0 = 0; k0 < bpt && !wide; k0 += 16) {
         uint32_t cc[16];
 #pragma unroll
@@ -1208,6 +1309,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
         for (int u = 0; u < 16; ++u) {
             const int v = v0 + k0 + u;
             if (cc[u]) {
+                if (cnt_lds) cnt_sh[v] = cc[u];
                 nzmask |= 1ull << (k0 + u);
 #pragma unroll
                 for (int i = 0; i < 16; ++i) pop[i] += ((v >> i) & 1) ? cc[u] : 0u;
@@ -1215,6 +1317,9 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
         }
     }
     DTS(12);
+    // the entry prefetches are consumed here, with pass 1's loads (issued before them, so
+    // no extra wait): left to themselves they sink to their first use after the decision
+    asm volatile("" ::"v"((uint32_t)key0), "v"((uint32_t)(key0 >> 32)), "s"(cls));
     if (t < 16) pops_sh[t] = 0;
     uint32_t m;
     const uint32_t rank0 = block_excl_scan<1024>((uint32_t)__popcll(nzmask), sh, &m);
@@ -1267,7 +1372,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
                 if (msk) { vv[u] = v0 + __ffsll((long long)msk) - 1; msk &= msk - 1; ++k; }
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) cc[u] = vv[u] >= 0 ? hist[vv[u]] : 1u;
+            for (int u = 0; u < 8; ++u) cc[u] = vv[u] >= 0 ? (cnt_lds ? cnt_sh[vv[u]] : hist[vv[u]]) : 1u;
             double tt[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) tt[u] = plogp(lut, cc[u], Nd);
@@ -1284,6 +1389,96 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
     }
     __syncthreads();
 
+    if (role > 0) {
+        // ---- a plane workgroup: H(X,Y) of plane i over the whole CU -- the joint order by
+        // a block scan, numpy's pairwise sum by np_sum_block1024 (the same tree as the wave
+        // path's np_sum_wave, so the value is bit-identical) -- published as its bit pattern
+        // (never 0: the main workgroup polls for non-zero).  Planes the main workgroup will
+        // not read (constant plane, slice off the wave path) publish PLANE_NONE.
+        const int i = role - 1;
+        u64 pub = PLANE_NONE;
+        const uint32_t pp = pops_sh[i];
+        PTS(1);
+        if (wfast && i < min(P.nbits, 16) && pp != 0 && (long long)pp != npx) {
+            build_joint_order_m16(nzmask, v0, rank0, i, jl, sh);   // wave path: m < 65536
+            PTS(2);
+            const double h = -np_sum_block1024_w0(ListTerm{tl, jl}, (int)m, vals);
+            PTS(3);
+            pub = (u64)__double_as_longlong(h);
+            if (pub == 0ull) pub = 0x8000000000000000ull;   // +0.0 -> -0.0: same MI
+        }
+        if (t == 0) __hip_atomic_store(plane_slots + 16 * (size_t)b + i, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    // main workgroup of a split decision: wait for every plane workgroup's value (they read
+    // the histogram this workgroup clears at the end); the slots are cleared for the next
+    // call at the end, with the histogram (a store here would be waited for by the next
+    // vmcnt wait of the wave, ~2 us)
+    __shared__ u64 slot_sh[16];
+    __shared__ int slot_to;
+    bool collected = false;
+    auto collect = [&]() {
+        if (t == 0) slot_to = 0;
+        __syncthreads();
+        if (t < nsplit) {
+            u64* sp = plane_slots + 16 * (size_t)b + t;
+            u64 v = 0;
+            for (uint32_t k = 0; k < (1u << 24); ++k) {   // bounded: co-resident by construction
+                v = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (!v) { v = PLANE_NONE; slot_to = 1; }
+            slot_sh[t] = v;
+        }
+        __syncthreads();
+        collected = true;
+    };
+
+    // ---- start offset: first maximal float(np.var) block in raster order (codec.py:441-453);
+    // independent of s, so the split decision finds it while its plane workgroups work
+    const int sb = P.block;
+    const int nbx = (P.W + sb - 1) / sb;
+    double bsc = -1.0;
+    int bix = 0x7FFFFFFF;
+    bool offset_done = false;
+    auto find_offset = [&]() {
+        offset_done = true;
+        if (!(P.fixed_offset < 0 && P.mode == CODEC_MODE_HYBRID)) return;
+        const int cnt = exact_count(P.H, P.W, sb, exact_edge_only);
+        for (int e = t; e < cnt; e += 1024) {
+            int by, bx;
+            exact_block(e, P.H, P.W, sb, exact_edge_only, &by, &bx);
+            const double sc = exact[(size_t)b * exact_cap + e];
+            const int ix = by * nbx + bx;
+            if (sc > bsc || (sc == bsc && ix < bix)) { bsc = sc; bix = ix; }
+        }
+        if (t == 0 && fast_blocks) {
+            const u64 key = key0;
+            if (key) {
+                const uint32_t score = (uint32_t)(key >> 32);
+                const int ix = (int)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFu));
+                const double n2 = (double)sb * sb * (double)sb * sb;
+                const double sc = (double)score / n2;
+                if (sc > bsc || (sc == bsc && ix < bix)) { bsc = sc; bix = ix; }
+            }
+        }
+        // block argmax (score desc, raster index asc)
+        const int lane = t & 63, wv = t >> 6;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const double os = __shfl_xor(bsc, o, 64);
+            const int oi = __shfl_xor(bix, o, 64);
+            if (os > bsc || (os == bsc && oi < bix)) { bsc = os; bix = oi; }
+        }
+        if (lane == 0) { best_sc[wv] = bsc; best_ix[wv] = bix; }
+        __syncthreads();
+        if (t == 0) {
+            for (int w = 1; w < 16; ++w)
+                if (best_sc[w] > bsc || (best_sc[w] == bsc && best_ix[w] < bix)) { bsc = best_sc[w]; bix = best_ix[w]; }
+        }
+    };
+
     DTS(2);
     // ---- calculate_entropy (codec.py:489-502) = H(Y) inside calculate_mutual_information
     double Hy = 0.0;
@@ -1292,7 +1487,47 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
     double cum = 0.0;
     if (t < 16) mis_sh[t] = 0.0;
     const bool need_decision = (P.fixed_s <= 0);
-    if (wfast) {
+    if (wfast && nsplit > 0) {
+        // split decision: H(Y) here (wave 15) while the plane workgroups sum their orders,
+        // then thread 0 takes the planes in order exactly like the sequential loop
+        const int wv = t >> 6, lane = t & 63;
+        if (wv == 15) {
+            const double h = -np_sum_wave(RankTerm{tl}, (int)m);
+            if (lane == 0) hy_sh = h;
+        }
+        // H(X) of every plane meanwhile (its two table loads off thread 0's walk)
+        if (wv == 1 && lane < min(P.nbits, 16)) {
+            const uint32_t pp = pops_sh[lane];
+            hx_sh[lane] = (pp != 0 && (long long)pp != npx) ? -(plogp(lut, (uint32_t)(npx - pp), Nd) + plogp(lut, pp, Nd)) : 0.0;
+        }
+        // the class's 16 layouts (one per s) into LDS meanwhile (`vals` is free here)
+        if (t < 16 * kLayW) reinterpret_cast<int32_t*>(vals)[t] = lay_all[t];
+        find_offset();   // meanwhile (its barrier also orders hx_sh / hy_sh)
+        DTS(8);
+        collect();
+        DTS(14);
+        Hy = hy_sh;
+        if (t == 0) {
+            const double target0 = P.beta * Hy;
+            const int nb = min(P.nbits, 16);
+            for (int ii = 0; ii < nb; ++ii) {
+                if (!(need_decision && !decided) && !P.all_mi) break;
+                const uint32_t pp = pops_sh[ii];
+                double mi = 0.0;
+                if (pp != 0 && (long long)pp != npx) {                // codec.py:520-523
+                    const double hx = hx_sh[ii];
+                    const double hxy = __longlong_as_double((long long)slot_sh[ii]);
+                    mi = (hx + Hy) - hxy;                               // codec.py:554
+                    if (!(mi > 0.0)) mi = 0.0;
+                }
+                mis_sh[ii] = mi;
+                if (need_decision && !decided) {
+                    cum += mi;
+                    if (cum >= target0) { s = ii + 1; decided = true; }
+                }
+            }
+        }
+    } else if (wfast) {
         // H(Y) by wave 0; then rounds of `wplanes` planes, plane i0+w on wave w: its joint
         // bincount order (bit-i-clear bins ascending, then bit-i-set bins, codec.py:546-551)
         // is written to its own list and summed with np_sum_wave.  Thread 0 then walks the
@@ -1470,56 +1705,17 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
 
     // the slice's segment layout for its s (64 ints), loaded by one wave in one round trip
     // while the offset is found, instead of thread 0's dependent loads in the windows loop
-    __shared__ int32_t lay_sh[sizeof(codec_layout) / 4];
-    static_assert(sizeof(codec_layout) / 4 <= 64, "one wave loads the layout");
+    __shared__ int32_t lay_sh[kLayW];
     if (t == 0) ctl_sh[1] = s;
     __syncthreads();
     {
         const int sl = min(max(ctl_sh[1], 1), 16);
-        if (t < (int)(sizeof(codec_layout) / 4))
-            lay_sh[t] = reinterpret_cast<const int32_t*>(table + (size_t)slice_class[b] * 16 + (sl - 1))[t];
+        if (t < kLayW) lay_sh[t] = (wfast && nsplit > 0) ? reinterpret_cast<const int32_t*>(vals)[(sl - 1) * kLayW + t]
+                                                         : lay_all[(sl - 1) * kLayW + t];
     }
 
     DTS(3);
-    // ---- start offset: first maximal float(np.var) block in raster order (codec.py:441-453)
-    const int sb = P.block;
-    const int nbx = (P.W + sb - 1) / sb;
-    double bsc = -1.0;
-    int bix = 0x7FFFFFFF;
-    if (P.fixed_offset < 0 && P.mode == CODEC_MODE_HYBRID) {
-        const int cnt = exact_count(P.H, P.W, sb, exact_edge_only);
-        for (int e = t; e < cnt; e += 1024) {
-            int by, bx;
-            exact_block(e, P.H, P.W, sb, exact_edge_only, &by, &bx);
-            const double sc = exact[(size_t)b * exact_cap + e];
-            const int ix = by * nbx + bx;
-            if (sc > bsc || (sc == bsc && ix < bix)) { bsc = sc; bix = ix; }
-        }
-        if (t == 0 && fast_blocks) {
-            const u64 key = key0;
-            if (key) {
-                const uint32_t score = (uint32_t)(key >> 32);
-                const int ix = (int)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFu));
-                const double n2 = (double)sb * sb * (double)sb * sb;
-                const double sc = (double)score / n2;
-                if (sc > bsc || (sc == bsc && ix < bix)) { bsc = sc; bix = ix; }
-            }
-        }
-        // block argmax (score desc, raster index asc)
-        const int lane = t & 63, wv = t >> 6;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            const double os = __shfl_xor(bsc, o, 64);
-            const int oi = __shfl_xor(bix, o, 64);
-            if (os > bsc || (os == bsc && oi < bix)) { bsc = os; bix = oi; }
-        }
-        if (lane == 0) { best_sc[wv] = bsc; best_ix[wv] = bix; }
-        __syncthreads();
-        if (t == 0) {
-            for (int w = 1; w < 16; ++w)
-                if (best_sc[w] > bsc || (best_sc[w] == bsc && best_ix[w] < bix)) { bsc = best_sc[w]; bix = best_ix[w]; }
-        }
-    }
+    if (!offset_done) find_offset();
 
     __shared__ SliceWin Wsh;   // the fused embed's window cache, filled by thread 0 below
     // ... and its segments in perm order: bit j belongs to the first k with j < seg_end[k];
@@ -1578,6 +1774,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
     M->npix = (int)npx;
     M->nbits = P.nbits;
     M->status = lut_ok ? 0 : 1;
+    if (collected && slot_to) { M->status = 2; flags |= CODEC_FLAG_DECIDE_TIMEOUT; M->flags = flags; }
     M->nonzero_bins = (int)m;
     M->entropy = Hy;
     M->target = target;
@@ -1652,11 +1849,16 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
         }
         DTS(11);
     }
+    if (nsplit > 0 && !collected) {   // the other decision paths: slots still to clear
+        collect();
+        if (t == 0 && slot_to) { M->status = 2; M->flags |= CODEC_FLAG_DECIDE_TIMEOUT; }
+    }
     // leave the workspace clean for the next call (codec_plan does not memset it): every
     // histogram bin the scan can have touched lies below max(Rp, 2) (pixel values < Rp; a
     // 16-bit wrap fix-up also writes bin v + 1 <= Rp - 1, or bin 1 when Rp = 1), plus the
     // slice's block key and OR word.  All reads of them precede this barrier.
     __syncthreads();
+    if (t < nsplit) plane_slots[16 * (size_t)b + t] = 0ull;
     {
         const int zr = Rp < 2 ? 2 : Rp;
         uint32_t* hz = ghist_all + (size_t)b * R;
@@ -2241,7 +2443,7 @@ static int host_exact_count(const codec_params* P, bool edge_only) {
 }
 
 struct WsLayout {
-    size_t hist, keys, orv, exact, terms, total;
+    size_t hist, keys, orv, slots, exact, terms, total;
     int exact_cap;
 };
 
@@ -2254,7 +2456,8 @@ static WsLayout ws_layout(const codec_params* P) {
     L.hist = 0;
     L.keys = align_up(L.hist + (size_t)P->B * R * 4, 256);
     L.orv = align_up(L.keys + (size_t)P->B * 8, 256);
-    L.exact = align_up(L.orv + (size_t)P->B * 4, 256);       // [0, exact) is zeroed per call
+    L.slots = align_up(L.orv + (size_t)P->B * 4, 256);      // split decision: 16 u64 per slice
+    L.exact = align_up(L.slots + (size_t)P->B * 16 * 8, 256);  // [0, exact) is zeroed on errors
     L.terms = align_up(L.exact + (size_t)P->B * L.exact_cap * 8, 256);
     L.total = align_up(L.terms + (size_t)P->B * R * 8, 256);
     return L;
@@ -2473,10 +2676,17 @@ static int plan_impl(const codec_params* P, const void* cover, void* stego, cons
     codec_params Pv = *P;
     // bit 0: force the block-sequential decision; bit 1: no walk path for wide slices
     Pv.reserved = (knob("CODEC_DECIDE_WAVES", 1) ? 0 : 1) | (knob("CODEC_DECIDE_WALK", 1) ? 0 : 2);
+    // small batches: the per-plane joint entropies go to plane workgroups on otherwise idle
+    // CUs (1 + nb workgroups per slice, all co-resident: at most 240 of them, one per CU)
+    const int nbp = P->nbits < 16 ? P->nbits : 16;
+    const bool need_mi = P->fixed_s <= 0 || P->all_mi;
+    const int nsplit = (knob("CODEC_DECIDE_SPLIT", 1) && need_mi && (long long)P->B * (1 + nbp) <= 240) ? nbp : 0;
+    u64* slots = reinterpret_cast<u64*>(ws + L.slots);
     ProfScope prof(st, E ? CODEC_K_DECIDE_EMBED : CODEC_K_DECIDE);
     const EmbedArgs Ev = E ? *E : EmbedArgs{nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
-#define DEC(TT, EM) hipLaunchKernelGGL((k_decide<TT, EM>), dim3(P->B), dim3(1024), 0, st, Pv, hist, orv, terms, keys, exact, \
-                                       L.exact_cap, edge_only, fast ? 1 : 0, log2_lut, (long long)lut_len, table, slice_class, meta, Ev)
+#define DEC(TT, EM) hipLaunchKernelGGL((k_decide<TT, EM>), dim3(P->B, 1 + nsplit), dim3(1024), 0, st, Pv, hist, orv, terms, keys, exact, \
+                                       L.exact_cap, edge_only, fast ? 1 : 0, log2_lut, (long long)lut_len, table, slice_class, meta, Ev, \
+                                       slots, nsplit)
     if (P->in_bytes == 2) { if (E) DEC(uint16_t, true); else DEC(uint16_t, false); }
     else { if (E) DEC(uint8_t, true); else DEC(uint8_t, false); }
 #undef DEC

@@ -36,6 +36,7 @@ extern "C" {
 #define CODEC_FLAG_OVERLAP 1u   /* windows of different planes may share pixels   */
 #define CODEC_FLAG_LOSSY 2u     /* segments do not tile the payload (T < s, clamp) */
 #define CODEC_FLAG_BADLUT 4u    /* log2 table shorter than H*W (status error)      */
+#define CODEC_FLAG_DECIDE_TIMEOUT 8u /* split decision: a plane workgroup never reported (status 2) */
 
 /* Call parameters (one batch: all slices share shape and dtype). */
 typedef struct codec_params {

@@ -31,11 +31,15 @@ def _run_case(case):
     return codec, enc
 
 
-@pytest.fixture(params=["waves", "block"])
+@pytest.fixture(params=["split", "waves", "block"])
 def decide_path(request, monkeypatch):
-    """k_decide's wave-parallel MI path (default when the joint orders fit in LDS) and the
-    block-sequential one (CODEC_DECIDE_WAVES=0; also what large-m slices use).  The block
-    variant also runs codec_encode unfused (codec_plan then the separate k_embed launch)."""
+    """k_decide's split decision (default for small batches: one plane workgroup per MI
+    plane), its one-workgroup wave-parallel MI path (CODEC_DECIDE_SPLIT=0; the default for
+    big batches when the joint orders fit in LDS) and the block-sequential one
+    (CODEC_DECIDE_WAVES=0; also what large-m slices use).  The block variant also runs
+    codec_encode unfused (codec_plan then the separate k_embed launch)."""
+    if request.param == "waves":
+        monkeypatch.setenv("CODEC_DECIDE_SPLIT", "0")
     if request.param == "block":
         monkeypatch.setenv("CODEC_DECIDE_WAVES", "0")
         monkeypatch.setenv("CODEC_FUSED_EMBED", "0")

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """C3 LSB step (256 x 512^2 ct12: codec_plan + embed + codec_extract) a few times, for
-rocprofv3 kernel traces and knob sweeps:  python3 tools/c3_lsb.py [steps]"""
+rocprofv3 kernel traces and knob sweeps:  python3 tools/c3_lsb.py [steps]
+LSB_SHAPE=BxHxW overrides the shape (e.g. 1x2048x2048 for C2)."""
 import os
 import sys
 
@@ -11,7 +12,7 @@ import bench  # noqa: E402
 import codec_tcc_amd as ct  # noqa: E402
 from codec_tcc_amd import synth  # noqa: E402
 
-B, H, W = 256, 512, 512
+B, H, W = (int(x) for x in os.environ.get("LSB_SHAPE", "256x512x512").split("x"))
 dev = torch.device("cuda", 0)
 covers = bench.make_covers(torch, "ct12", B, H, W, dev, seed=1000)
 codec = ct.Codec(B, H, W, dtype="uint16", beta=0.4, block=16, device=dev)

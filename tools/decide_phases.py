@@ -21,7 +21,8 @@ def main():
     import codec_tcc_amd as ct
     from codec_tcc_amd import synth
     kind = sys.argv[1] if len(sys.argv) > 1 else "ct12"
-    B, H, W = 64, 2048, 2048
+    B = int(os.environ.get("DTS_B", "64"))
+    H = W = 2048
     dev = torch.device("cuda", 0)
     covers = bench.make_covers(torch, kind, B, H, W, dev, 0)
     codec = ct.Codec(B, H, W, dtype="uint16", device=dev)
@@ -32,15 +33,27 @@ def main():
     R = 65536
     keys = (B * R * 4 + 255) // 256 * 256
     orv = (keys + B * 8 + 255) // 256 * 256
-    exact = (orv + B * 4 + 255) // 256 * 256
+    slots = (orv + B * 4 + 255) // 256 * 256
+    exact = (slots + B * 16 * 8 + 255) // 256 * 256
     nby = (H + 15) // 16
     cap = nby * ((W + 15) // 16)
     terms = (exact + B * cap * 8 + 255) // 256 * 256
     ws = codec.workspace.cpu().numpy()
     raw = ws[terms: terms + B * R * 8].view(np.int64).reshape(B, R)[:, R - 16:]
     t = raw[:, :6]
-    w0 = raw[:, 6:8]   # wave 0 (plane 0): after its H(X,Y) sum, after its joint-order list
-    print("wave0: masks %.2f us, counts+scans %.2f us, list %.2f us, sum %.2f us, then to round end %.2f us" % (
+    split = B * 17 <= 240 and os.environ.get("CODEC_DECIDE_SPLIT", "1") != "0"
+    if split:   # plane workgroups: entry, after pass 1 + terms, after the list, after the sum
+        pr = ws[terms: terms + B * R * 8].view(np.int64).reshape(B, R)[:, R - 80:R - 16].reshape(B, 16, 4)
+        t0 = raw[:, 0:1]
+        act = pr[:, :, 3] > pr[:, :, 2]
+        print("split: plane start %.2f us after main, pass1+terms %.2f, list %.2f, sum %.2f, last plane done %.2f us "
+              "after main start; main: H(Y) done %.2f, collect done %.2f us" % (
+                  np.median(pr[:, :, 0] - t0) * 0.01, np.median((pr[:, :, 1] - pr[:, :, 0])) * 0.01,
+                  np.median((pr[:, :, 2] - pr[:, :, 1])[act]) * 0.01, np.median((pr[:, :, 3] - pr[:, :, 2])[act]) * 0.01,
+                  np.median(np.max(np.where(act, pr[:, :, 3], pr[:, :, 1]), axis=1) - t0[:, 0]) * 0.01,
+                  np.median(raw[:, 8] - raw[:, 0]) * 0.01, np.median(raw[:, 14] - raw[:, 0]) * 0.01))
+    w0 = raw[:, 6:8] if not split else None   # wave 0 (plane 0): after its H(X,Y) sum, after its joint-order list
+    if not split: print("wave0: masks %.2f us, counts+scans %.2f us, list %.2f us, sum %.2f us, then to round end %.2f us" % (
         np.median(raw[:, 8] - raw[:, 2]) * 0.01, np.median(raw[:, 9] - raw[:, 8]) * 0.01,
         np.median(w0[:, 1] - raw[:, 9]) * 0.01, np.median(w0[:, 0] - w0[:, 1]) * 0.01,
         np.median(raw[:, 3] - w0[:, 0]) * 0.01))
