@@ -353,11 +353,14 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
     res["kernels_ms"] = {k: round(v, 4) for k, v in kern.items()}
     # the launch path the dispatcher chose (codec_pee.hip pee_use_slice_serial): the
     # slice-serial kernels for chip-filling batches in place / small slices, else look-back
-    emb = next((k for k in ("k_pee_embed_ss", "k_pee_embed1", "k_pee_scan") if k in kern), None)
+    emb = next((k for k in ("k_pee_embed_ss_auto", "k_pee_embed_ss", "k_pee_embed1", "k_pee_scan") if k in kern), None)
     ext = next((k for k in ("k_pee_extract_ss", "k_pee_extract1") if k in kern), None)
     res["embed_kernel"], res["extract_kernel"] = emb, ext
     ss_d = os.environ.get("CODEC_PEE_SS_D", "2") if inplace else "4"   # ring depth (codec_pee.hip dispatch)
     inst = {"k_pee_embed_ss": "<unsigned short, true, %s, %s, true>" % ("true" if inplace else "false", ss_d),
+            # T = 'auto' where the embed is slice-serial: the capacity phase fused in (codec_pee_embed_auto)
+            "k_pee_embed_ss_auto": "<unsigned short, true, %s, %s, true, true>" % (("true", "2") if inplace
+                                                                                 else ("false", "4")),
             "k_pee_extract_ss": "<unsigned short, true, %s, 4>" % ("true" if inplace else "false"),
             "k_pee_embed1": "<unsigned short, true, %s>" % ("true" if inplace else "false"),
             "k_pee_extract1": "<unsigned short, true, %s>" % ("true" if inplace else "false")}
@@ -366,7 +369,7 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
         # (candidates + their neighbours), its candidate row written back
         prefix_px = sum(((r.end // 4) + 1) * 16 for r in recs if r.end >= 0)
         by = prefix_px * 2 + prefix_px // 2 * 2
-        if emb in ("k_pee_embed_ss", "k_pee_embed1") and kern[emb] > 0:
+        if emb in ("k_pee_embed_ss_auto", "k_pee_embed_ss", "k_pee_embed1") and kern[emb] > 0:
             res["roofline"] = _roof(emb, by, kern[emb], pmc_traffic(emb + inst[emb], B, H, W, kind))
         if ext and kern[ext] > 0:
             # extract reads the same items plus their location-map words, writes the rows back
@@ -377,7 +380,7 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
                                 pmc_traffic(emb + inst.get(emb, ""), B, H, W, kind))
     if ext:
         res["extract_roofline"] = _roof(ext, B * H * W * 4, kern[ext], pmc_traffic(ext + inst[ext], B, H, W, kind))
-    t_emb = sum(kern.get(k, 0.0) for k in ("k_pee_embed_ss", "k_pee_embed1", "k_pee_scan", "k_pee_locate",
+    t_emb = sum(kern.get(k, 0.0) for k in ("k_pee_embed_ss_auto", "k_pee_embed_ss", "k_pee_embed1", "k_pee_scan", "k_pee_locate",
                                            "k_pee_embed")) / 1e3
     if t_emb > 0:
         # north-star figure: cover bytes read / t_embed / peak (an out-of-place embed also

@@ -92,6 +92,8 @@ _SIGS = {
     "codec_pee_extract": (C.c_int, [C.POINTER(PeeParams), _VP, _VP, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),
     "codec_pee_embed_ts": (C.c_int, [C.POINTER(PeeParams), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),
     "codec_pee_capacity": (C.c_int, [C.POINTER(PeeParams), _VP, C.c_int32, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),
+    "codec_pee_embed_auto": (C.c_int, [C.POINTER(PeeParams), _VP, _VP, _VP, _VP, C.c_int32, _VP, _VP, _VP, _VP,
+                                       C.c_size_t, _VP]),
     "codec_quality_moments": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP, _VP, _VP, _VP]),
     "codec_block_variance": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP, _VP, _VP]),
     "codec_lsb_runs": (C.c_int, [C.c_int32, C.c_int64, C.c_int32, _VP, _VP, _VP, C.c_int64, _VP, C.c_int32, _VP]),
@@ -103,7 +105,8 @@ KERNEL_TAGS = {1: "k_scan_fast", 2: "k_scan_generic", 3: "k_block_exact", 4: "k_
                11: "k_pee_embed", 12: "k_pee_copy", 13: "k_pee_dcount", 14: "k_pee_recover",
                15: "k_pee_embed1", 16: "k_pee_extract1", 17: "k_scan_read", 18: "k_unxor",
                19: "k_scan_rows", 20: "k_scan_rows_read", 21: "k_quality", 22: "k_decide_embed",
-               23: "k_pee_capacity", 24: "k_pee_embed_ss", 25: "k_pee_extract_ss"}
+               23: "k_pee_capacity", 24: "k_pee_embed_ss", 25: "k_pee_extract_ss",
+               26: "k_pee_embed_ss_auto"}
 EXPORTS = tuple(_SIGS)
 
 _lib = None

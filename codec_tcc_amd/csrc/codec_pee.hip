@@ -389,6 +389,44 @@ __device__ __forceinline__ void pee_select_slice(uint32_t* h, int tmax, long lon
     if (t_out) *t_out = tsel ? tsel : tmax;
 }
 
+// Capacity histogram update for the 4 candidates of one item (or the first nq of them):
+// bin u = folded error (e >= 0 ? e : -e - 1) of every candidate whose expansion p + 2e (+1)
+// stays in [0, maxval]; equal bins merged, then one independent read-add-write per distinct
+// bin into the lane's own counters cnt[u * NLANES + lane] (no LDS atomics, conflict-free:
+// a lane always hits its own bank).  Shared by k_pee_ehist and the fused capacity phase of
+// k_pee_embed_ss.
+template <int NLANES>
+__device__ __forceinline__ void ehist_add4(uint32_t* cnt, int lane_ix, const int (&x)[4], const int (&a)[4],
+                                           const int (&bb)[4], const int (&cc)[4], int nq, int tmax, int maxval) {
+    int u[4];
+    uint32_t c[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int p = med3(a[q], bb[q], cc[q]), e = x[q] - p;
+        const int uq = e >= 0 ? e : -e - 1;
+        u[q] = uq;
+        c[q] = (q < nq) & (uq < tmax) & (p + 2 * e >= 0) & (p + 2 * e + 1 <= maxval) ? 1u : 0u;
+    }
+#pragma unroll
+    for (int q = 1; q < 4; ++q)
+#pragma unroll
+        for (int r = 0; r < q; ++r) {   // branch-free merge (& instead of &&)
+            const bool same = (c[r] != 0u) & (c[q] != 0u) & (u[r] == u[q]);
+            c[r] += same ? c[q] : 0u;
+            c[q] = same ? 0u : c[q];
+        }
+    uint32_t old[4];
+    int ad[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        ad[q] = min(u[q], tmax - 1) * NLANES + lane_ix;
+        old[q] = cnt[ad[q]];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        if (c[q]) cnt[ad[q]] = old[q] + c[q];   // masked: a merged duplicate must not write back
+}
+
 template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void k_pee_ehist(const T* __restrict__ img, int H, int W, int maxval, int tmax,
                                                    int per_wg, uint32_t* __restrict__ hist_all,
@@ -401,36 +439,8 @@ __global__ __launch_bounds__(256) void k_pee_ehist(const T* __restrict__ img, in
     const T* src = img + (size_t)b * H * W;
     for (int u = 0; u < tmax; ++u) cnt[u * 256 + tid] = 0u;
     if (tid < tmax) bins[tid] = 0u;
-    // the 4 candidates of one item (or 1 on the scalar path): bins merged, then one
-    // independent read-add-write per distinct bin (the lane's own counters only)
     auto add4 = [&](const int (&x)[4], const int (&a)[4], const int (&bb)[4], const int (&cc)[4], int nq) {
-        int u[4];
-        uint32_t c[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int p = med3(a[q], bb[q], cc[q]), e = x[q] - p;
-            const int uq = e >= 0 ? e : -e - 1;
-            u[q] = uq;
-            c[q] = (q < nq) & (uq < tmax) & (p + 2 * e >= 0) & (p + 2 * e + 1 <= maxval) ? 1u : 0u;
-        }
-#pragma unroll
-        for (int q = 1; q < 4; ++q)
-#pragma unroll
-            for (int r = 0; r < q; ++r) {   // branch-free merge (& instead of &&)
-                const bool same = (c[r] != 0u) & (c[q] != 0u) & (u[r] == u[q]);
-                c[r] += same ? c[q] : 0u;
-                c[q] = same ? 0u : c[q];
-            }
-        uint32_t old[4];
-        int ad[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            ad[q] = min(u[q], tmax - 1) * 256 + tid;
-            old[q] = cnt[ad[q]];
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (c[q]) cnt[ad[q]] = old[q] + c[q];   // masked: a merged duplicate must not write back
+        ehist_add4<256>(cnt, tid, x, a, bb, cc, nq, tmax, maxval);
     };
     __syncthreads();
     if constexpr (VEC) {
@@ -1789,18 +1799,31 @@ __device__ __forceinline__ void ss_scan(uint32_t n, uint32_t (*wtot)[16], int pa
     *wbase = wb;
 }
 
-template <typename T, bool NT, bool INPLACE, int D, bool PAY_LDS>
+// counters of the fused capacity phase (AUTO): the top tmax * 1024 words of the pad, below
+// its last word; the payload (PAY_LDS) sits at the bottom
+#define SS_AUTO_CNT_BASE(tmax) (SS_PAD_WORDS - 1 - (tmax) * SS_THREADS)
+#define SS_AUTO_TMAX 16
+
+// AUTO (capacity control fused in, codec_pee_embed_auto): before embedding, the workgroup
+// streams its whole slice once and builds the capacity histogram of k_pee_ehist in
+// lane-private LDS counters, then takes the smallest T <= tmax whose capacity holds the
+// slice's payload (pee_select_slice's rule).  The embed that follows re-reads the slice from
+// the MALL (C3: 134 MB batch); no second launch, no global histogram, no arrival counter.
+template <typename T, bool NT, bool INPLACE, int D, bool PAY_LDS, bool AUTO = false>
 __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict__ cover, T* stego, int H, int W, int T0,
                                                              int maxval, const int32_t* __restrict__ lengths,
                                                              const int32_t* __restrict__ tps,
                                                              const u64* __restrict__ payload_all, int pw,
                                                              codec_pee_meta* __restrict__ meta_all,
-                                                             u64* __restrict__ lm_all, int lmw, char* __restrict__ sink) {
+                                                             u64* __restrict__ lm_all, int lmw, char* __restrict__ sink,
+                                                             int tmax, int32_t* __restrict__ t_out) {
     typedef typename Vec8<T>::type V;
     __shared__ uint32_t ss_pad[SS_PAD_WORDS];
     __shared__ uint32_t wtot[2][16];
     __shared__ uint32_t red[2][16];
     __shared__ int s_end;
+    __shared__ uint32_t s_bins[AUTO ? PEE_TMAX_MAX : 1];
+    __shared__ int s_T;
 #ifdef PEE_SS_TRACE
     __shared__ unsigned long long ss_trace[SS_TRACE_N];
 #endif
@@ -1812,7 +1835,7 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
     const int nc = (H / 2) * (W / 2);
     const int ntiles = (nc + PEE_TILE - 1) / PEE_TILE;
     const uint32_t L = (uint32_t)max(0, lengths[b]);
-    const int Tthr = tps ? tps[b] : T0;
+    int Tthr = tps ? tps[b] : T0;
     const size_t npx = (size_t)H * W;
     const T* src = cover + b * npx;
     T* dst = stego + b * npx;
@@ -1834,6 +1857,58 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
         SsCursor l;
         l.init(items - 1u, (uint32_t)CR, (uint32_t)W);
         off_last = l.o;
+    }
+    if constexpr (AUTO) {
+        // capacity phase: 4 items per thread per step, their 8 loads issued together; plain
+        // loads (the embed below re-reads the slice), lane-private counters (no barrier)
+        uint32_t* cnt = ss_pad + SS_AUTO_CNT_BASE(tmax);
+        for (int u = 0; u < tmax; ++u) cnt[u * SS_THREADS + tid] = 0u;
+        constexpr int U = 4;
+        SsCursor cur;
+        cur.init((uint32_t)tid, (uint32_t)CR, (uint32_t)W);
+        for (uint32_t it = (uint32_t)tid; it < items; it += SS_THREADS * U) {
+            V a0[U], a1[U];
+            bool in[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                in[k] = it + (uint32_t)(SS_THREADS * k) < items;
+                ss_load_at<T, false>(src, (uint32_t)W, in[k] ? cur.o : 0u, a0[k], a1[k]);
+                cur.step(dr, (uint32_t)CR, ostep, owrap);
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                int x[4], a[4], bb[4], cc[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    x[q] = (int)get_px(a1[k], 2 * q + 1); a[q] = (int)get_px(a1[k], 2 * q);
+                    bb[q] = (int)get_px(a0[k], 2 * q + 1); cc[q] = (int)get_px(a0[k], 2 * q);
+                }
+                ehist_add4<SS_THREADS>(cnt, tid, x, a, bb, cc, in[k] ? 4 : 0, tmax, maxval);
+            }
+        }
+        lds_barrier();
+        // bin u: wave u % 16 sums the 1024 lane counters (16 per lane, then the wave)
+        for (int u = wv; u < tmax; u += SS_THREADS / 64) {
+            uint32_t s = 0;
+#pragma unroll
+            for (int j = 0; j < SS_THREADS / 64; ++j) s += cnt[u * SS_THREADS + j * 64 + lane];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+            if (lane == 0) s_bins[u] = s;
+        }
+        lds_barrier();
+        if (tid == 0) {   // pee_select_slice's rule: the smallest T whose capacity >= L, else tmax
+            long long run = 0;
+            int tsel = 0;
+            for (int t = 1; t <= tmax; ++t) {
+                run += (long long)s_bins[t - 1];
+                if (!tsel && run >= (long long)L) tsel = t;
+            }
+            s_T = tsel ? tsel : tmax;
+            if (t_out) t_out[b] = s_T;
+        }
+        lds_barrier();
+        Tthr = s_T;
     }
     // ro[d]: the offset ring slot d was loaded from (= the item's store offset)
     uint32_t ro[D];
@@ -2423,7 +2498,7 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
 #define PES1(TT, NTV, IP, PL) hipLaunchKernelGGL((k_pee_embed_ss<TT, NTV, IP, 4, PL>), dim3((unsigned)P->B), dim3(SS_THREADS), 0, st, \
             static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, tps, \
             reinterpret_cast<const u64*>(payload), P->payload_words, meta, reinterpret_cast<u64*>(lm), P->lm_words, \
-            static_cast<char*>(workspace) + L.sink)
+            static_cast<char*>(workspace) + L.sink, 0, nullptr)
 #define PES(TT, NTV, IP) do { if (pay_lds) PES1(TT, NTV, IP, true); else PES1(TT, NTV, IP, false); } while (0)
         // ring depth of the in-place embed: it does not know `end` in advance, so the D - 1
         // chunks it has in flight past it are wasted reads; at 256 x 2048^2 the steady state
@@ -2433,7 +2508,7 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
 #define PES1D(TT, NTV, IP, DD) hipLaunchKernelGGL((k_pee_embed_ss<TT, NTV, IP, DD, true>), dim3((unsigned)P->B), dim3(SS_THREADS), 0, st, \
             static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, tps, \
             reinterpret_cast<const u64*>(payload), P->payload_words, meta, reinterpret_cast<u64*>(lm), P->lm_words, \
-            static_cast<char*>(workspace) + L.sink)
+            static_cast<char*>(workspace) + L.sink, 0, nullptr)
         if (P->bytes == 2) {
             if (inplace) {
                 if (ss_d == 2 && nt) PES1D(uint16_t, true, true, 2);
@@ -2549,6 +2624,47 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
 #undef PEMB
         LAUNCH_CHECK("k_pee_embed");
     }
+    return 0;
+}
+
+int codec_pee_embed_auto(const codec_pee_params* P, const void* cover, void* stego, const uint64_t* payload,
+                         const int32_t* lengths, int32_t tmax, int32_t* t_out, codec_pee_meta* meta, uint64_t* lm,
+                         void* workspace, size_t workspace_bytes, void* stream) {
+    int rc = pee_check(P);
+    if (rc) return rc;
+    if (!cover || !stego || !payload || !lengths || !t_out || !meta || !lm || !workspace)
+        return set_err(CODEC_EINVAL, "codec_pee_embed_auto: NULL pointer argument");
+    if (tmax < 1 || tmax > PEE_TMAX_MAX) return set_err(CODEC_EINVAL, "tmax must be in 1..64");
+    const PeeWs L = pee_ws(P);
+    if (workspace_bytes < L.total) return set_err(CODEC_EINVAL, "workspace too small");
+    hipStream_t st = as_stream(stream);
+    const bool inplace = cover == stego;
+    const bool vec = (P->W % 8) == 0 && ((uintptr_t)cover % 16) == 0 && ((uintptr_t)stego % 16) == 0;
+    const long long items = (long long)(P->H / 2) * (P->W / 8);
+    // fused single launch where the embed is slice-serial anyway (chip-filling batches of
+    // <= 64-chunk slices, e.g. C3, or in place) and the counters fit beside the payload in
+    // the LDS pad; elsewhere the capacity pass and the per-slice-T embed as two launches
+    const bool fused = P->bytes == 2 && vec && items > 0 && knob("CODEC_PEE_ONEPASS", -1) != 0 &&
+                       knob("CODEC_PEE_AUTO_FUSED", 1) != 0 && tmax <= SS_AUTO_TMAX &&
+                       P->payload_words <= SS_PAY_WORDS && knob("CODEC_PEE_SS_PAYLDS", 1) != 0 &&
+                       2LL * P->payload_words <= (long long)SS_AUTO_CNT_BASE(tmax) && pee_use_slice_serial(P, inplace);
+    if (!fused) {
+        rc = codec_pee_capacity(P, cover, tmax, lengths, nullptr, t_out, workspace, workspace_bytes, stream);
+        if (rc) return rc;
+        return codec_pee_embed_ts(P, cover, stego, payload, lengths, t_out, meta, lm, workspace, workspace_bytes, stream);
+    }
+    const bool nt = knob("CODEC_NT", 1) != 0;
+    ProfScope prof(st, CODEC_K_PEE_EMBED_SS_AUTO);
+#define PEA(NTV, IP, DD) hipLaunchKernelGGL((k_pee_embed_ss<uint16_t, NTV, IP, DD, true, true>), dim3((unsigned)P->B), \
+            dim3(SS_THREADS), 0, st, static_cast<const uint16_t*>(cover), static_cast<uint16_t*>(stego), P->H, P->W, \
+            P->T, P->maxval, lengths, nullptr, reinterpret_cast<const u64*>(payload), P->payload_words, meta, \
+            reinterpret_cast<u64*>(lm), P->lm_words, static_cast<char*>(workspace) + L.sink, (int)tmax, t_out)
+    // ring depths as in codec_pee_embed_ts (in place 2, out of place 4)
+    if (inplace) { if (nt) PEA(true, true, 2); else PEA(false, true, 2); }
+    else { if (nt) PEA(true, false, 4); else PEA(false, false, 4); }
+#undef PEA
+    LAUNCH_CHECK("k_pee_embed_ss(auto)");
+    if ((P->H & 1) && !inplace) HIP_TRY(pee_copy_last_rows(P, cover, stego, st));
     return 0;
 }
 

@@ -104,16 +104,17 @@ class PeeCodec:
             meta = torch.empty((self.B, _lib.PEE_META_BYTES), dtype=torch.uint8, device=self.device)
         P = self._params(words.shape[1])
         lib = _lib.load()
-        tps = None
-        if self.auto:   # capacity control: per-slice T from one read-only pass, on the device
-            _lib.check(lib.codec_pee_capacity(C.byref(P), covers.data_ptr(), self.tmax, lens_t.data_ptr(), None,
-                                              self.t_slices.data_ptr(), self.workspace.data_ptr(),
-                                              self.workspace.numel(), _stream()), "codec_pee_capacity")
-            tps = self.t_slices.data_ptr()
-        _lib.check(lib.codec_pee_embed_ts(C.byref(P), covers.data_ptr(), stego.data_ptr(), words.data_ptr(),
-                                          lens_t.data_ptr(), tps, meta.data_ptr(), lm.data_ptr(),
-                                          self.workspace.data_ptr(), self.workspace.numel(), _stream()),
-                   "codec_pee_embed")
+        if self.auto:   # capacity control: per-slice T on the device (fused into the embed
+            # launch where it runs slice-serial, else one read-only capacity pass first)
+            _lib.check(lib.codec_pee_embed_auto(C.byref(P), covers.data_ptr(), stego.data_ptr(), words.data_ptr(),
+                                                lens_t.data_ptr(), self.tmax, self.t_slices.data_ptr(),
+                                                meta.data_ptr(), lm.data_ptr(), self.workspace.data_ptr(),
+                                                self.workspace.numel(), _stream()), "codec_pee_embed_auto")
+        else:
+            _lib.check(lib.codec_pee_embed_ts(C.byref(P), covers.data_ptr(), stego.data_ptr(), words.data_ptr(),
+                                              lens_t.data_ptr(), None, meta.data_ptr(), lm.data_ptr(),
+                                              self.workspace.data_ptr(), self.workspace.numel(), _stream()),
+                       "codec_pee_embed")
         enc = PeeEncoded(stego=stego, lm=lm, meta=meta, lengths=list(lengths), payload_words=int(words.shape[1]))
         if check:
             _raise_lookback(enc.records())

@@ -262,6 +262,16 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
  * once (its error bins are cleared at the end of every call, not at the start). */
 int codec_pee_capacity(const codec_pee_params* P, const void* cover, int32_t tmax, const int32_t* lengths,
                        int32_t* caps, int32_t* t_out, void* workspace, size_t workspace_bytes, void* stream);
+/* Capacity-controlled embed in one call: t_out[B] (device int32, required) receives the
+ * per-slice T chosen by codec_pee_capacity's rule (1 <= tmax <= 64), and the slices are
+ * embedded with it (meta.T records it) -- results identical to codec_pee_capacity(t_out)
+ * followed by codec_pee_embed_ts(t_out).  Where the embed runs slice-serial (chip-filling
+ * batches of small slices, or in place; uint16, tmax <= 16) the capacity pass is fused into
+ * the embed launch: each slice's workgroup counts its slice, then embeds it, re-reading the
+ * slice from the Infinity Cache. */
+int codec_pee_embed_auto(const codec_pee_params* P, const void* cover, void* stego, const uint64_t* payload,
+                         const int32_t* lengths, int32_t tmax, int32_t* t_out, codec_pee_meta* meta, uint64_t* lm,
+                         void* workspace, size_t workspace_bytes, void* stream);
 /* stego -> exact payload bits + restored cover.  cover_out == stego is allowed (in
  * place: only the items up to `end` are read and written). */
 int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_pee_meta* meta,
@@ -307,6 +317,7 @@ int codec_quality_moments(int32_t B, int32_t H, int32_t W, int32_t bytes, const 
 #define CODEC_K_PEE_CAPACITY 23
 #define CODEC_K_PEE_EMBED_SS 24
 #define CODEC_K_PEE_EXTRACT_SS 25
+#define CODEC_K_PEE_EMBED_SS_AUTO 26
 int codec_profile_begin(int32_t capacity);
 /* after the stream has been synchronised: fills ms[i], tag[i] for the recorded pairs and
  * returns their count (closes the window and frees the events). */

@@ -64,10 +64,13 @@ def _pee_batch_check(covers, sample, T=2, chars=1024):
     packed = codec.pack_payloads(payloads)
     enc = codec.embed(covers, None, packed=packed)
     recs = enc.records()
+    t_dev = codec.t_slices.cpu().numpy() if T == "auto" else None
     for i in sample:
         cov = covers[i].cpu().numpy()
         Ti = P.select_T(cov, len(payloads[i]), codec.tmax) if T == "auto" else T
         assert recs[i].T == Ti
+        if t_dev is not None:
+            assert t_dev[i] == Ti, i
         st, side = P.pee_embed(cov, payloads[i], Ti)
         assert recs[i].status == 0 and recs[i].end == side["end"], i
         np.testing.assert_array_equal(enc.stego[i].cpu().numpy(), st)
@@ -93,10 +96,15 @@ def test_c3_lsb_256x512():
     _lsb_batch_check(covers, msgs, sample=range(0, B, 16))
 
 
-@pytest.mark.parametrize("ss", ["auto", "0"])
+@pytest.mark.parametrize("ss", ["auto", "0", "unfused"])
 def test_c3_pee_256x512(ss, monkeypatch):
-    """1 KB per 512^2 ct12 slice needs T ~ 4-5 (T = 2 holds ~4.4 kbit): capacity control."""
-    if ss != "auto":
+    """1 KB per 512^2 ct12 slice needs T ~ 4-5 (T = 2 holds ~4.4 kbit): capacity control.
+    "auto": the default launch, capacity fused into the slice-serial embed
+    (codec_pee_embed_auto); "unfused": capacity pass + slice-serial embed as two launches;
+    "0": capacity pass + look-back embed."""
+    if ss == "unfused":
+        monkeypatch.setenv("CODEC_PEE_AUTO_FUSED", "0")
+    elif ss != "auto":
         monkeypatch.setenv("CODEC_PEE_SS", ss)
     _pee_batch_check(_batch(256, 512, 512, seed=2000), sample=range(3, 256, 16), T="auto")
 

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--kind", default="ct12")
     ap.add_argument("--no-check", action="store_true", help="diagnostic builds: skip the round-trip check")
     ap.add_argument("--lib", default=None, help="alternative build of libcodec_hip.so")
+    ap.add_argument("--T", default="2", help="PEE threshold, or 'auto' (capacity control, e.g. C3)")
+    ap.add_argument("--modes", default="oop,ip", help="comma list of oop (out of place) / ip (in place)")
     a = ap.parse_args()
     import torch
     if a.lib:
@@ -35,14 +37,16 @@ def main():
     dev = torch.device("cuda", 0)
     B, H, W = a.batch, a.size, a.size
     covers = bench.make_covers(torch, a.kind, B, H, W, dev, 0)
-    args = types.SimpleNamespace(payload_chars=1024, pee_T=2, warmup=2, steps=10, no_profile=False)
+    T = a.T if a.T == "auto" else int(a.T)
+    args = types.SimpleNamespace(payload_chars=1024, pee_T=T, warmup=2, steps=10, no_profile=False, kind=a.kind)
+    modes = [m == "ip" for m in a.modes.split(",")]
     res = {}
     for _ in range(a.rounds):
         for i, cfg in enumerate(configs):
             saved = {k: os.environ.get(k) for k in cfg}
             os.environ.update(cfg)
-            for mode in (False, True):
-                r = bench.bench_pee(args, torch, None, 1, dev, covers, B, H, W, inplace=mode)
+            for mode in modes:
+                r = bench.bench_pee(args, torch, None, 1, 0, dev, covers, B, H, W, inplace=mode)
                 assert a.no_check or r["roundtrip_ok"], (cfg, mode)
                 d = res.setdefault((i, mode), {})
                 for k, v in r["kernels_ms"].items():
