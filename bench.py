@@ -361,7 +361,7 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
             # T = 'auto' where the embed is slice-serial: the capacity phase fused in (codec_pee_embed_auto)
             "k_pee_embed_ss_auto": "<unsigned short, true, %s, %s, true, true>" % (("true", "2") if inplace
                                                                                  else ("false", "4")),
-            "k_pee_extract_ss": "<unsigned short, true, %s, 4>" % ("true" if inplace else "false"),
+            "k_pee_extract_ss": "<unsigned short, true, %s>" % ("true, 4" if inplace else "false, 2"),
             "k_pee_embed1": "<unsigned short, true, %s>" % ("true" if inplace else "false"),
             "k_pee_extract1": "<unsigned short, true, %s>" % ("true" if inplace else "false")}
     if inplace:
@@ -496,6 +496,8 @@ def bench_c3(args, torch, dist, world, dev, rank):
     res = {"workload": f"{args.kind} 512x512 uint16 x 256 slices (C3), MED-PEE with capacity control "
                        f"(T = 'auto': a {args.payload_chars}-char payload needs T ~ 4-5 on a 512^2 ct12 slice)"}
     res.update(bench_pee(args, torch, dist, 1, rank, dev, covers, B, H, W, steps=4 * args.steps, T="auto"))
+    # unique HBM bytes of the step (cover read + stego write + stego read + cover write) / step time
+    res["step_hbm_gbs"] = round(B * H * W * 8 / (res["ms_per_step"] / 1e3) / 1e9, 1)
     lsb = bench_lsb(args, torch, dist, 1, rank, dev, covers, B, H, W, steps=4 * args.steps, seed0=5000)
     lsb.pop("_stego", None)
     res["lsb"] = lsb

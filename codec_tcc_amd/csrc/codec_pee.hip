@@ -1886,6 +1886,22 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
                 ehist_add4<SS_THREADS>(cnt, tid, x, a, bb, cc, in[k] ? 4 : 0, tmax, maxval);
             }
         }
+    }
+    // ro[d]: the offset ring slot d was loaded from (= the item's store offset)
+    uint32_t ro[D];
+    SsCursor ahead;
+    ahead.init((uint32_t)tid, (uint32_t)CR, (uint32_t)W);
+    uint32_t it_a = (uint32_t)tid;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        ro[d] = it_a < items ? ahead.o : off_last;
+        ss_load_at<T, NT>(src, (uint32_t)W, ro[d], r0[d], r1[d]);
+        ahead.step(dr, (uint32_t)CR, ostep, owrap);
+        it_a += SS_THREADS;
+    }
+    if constexpr (AUTO) {
+        // the ring's first loads are in flight (they do not depend on T): reduce the counters
+        uint32_t* cnt = ss_pad + SS_AUTO_CNT_BASE(tmax);
         lds_barrier();
         // bin u: wave u % 16 sums the 1024 lane counters (16 per lane, then the wave)
         for (int u = wv; u < tmax; u += SS_THREADS / 64) {
@@ -1909,18 +1925,6 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
         }
         lds_barrier();
         Tthr = s_T;
-    }
-    // ro[d]: the offset ring slot d was loaded from (= the item's store offset)
-    uint32_t ro[D];
-    SsCursor ahead;
-    ahead.init((uint32_t)tid, (uint32_t)CR, (uint32_t)W);
-    uint32_t it_a = (uint32_t)tid;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-        ro[d] = it_a < items ? ahead.o : off_last;
-        ss_load_at<T, NT>(src, (uint32_t)W, ro[d], r0[d], r1[d]);
-        ahead.step(dr, (uint32_t)CR, ostep, owrap);
-        it_a += SS_THREADS;
     }
     if (PAY_LDS) {   // the payload in LDS once: no dependent global round trip per chunk
         const int nw = min(pw, (int)((L + 63u) >> 6));
@@ -2680,7 +2684,7 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
     uint32_t* cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.cnt);
     uint32_t* off = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.off);
     const long long nbytes = (long long)P->H * P->W * P->B * P->bytes;
-    const bool nt = knob("CODEC_NT", 1) != 0;
+    const bool nt = knob("CODEC_PEE_X_NT", knob("CODEC_NT", 1)) != 0;   // CODEC_PEE_X_NT: extract only (A/B)
     const size_t va = P->bytes == 2 ? 16 : 8;
     const bool vec = (P->W % 8) == 0 && ((uintptr_t)stego % va) == 0 && ((uintptr_t)cover_out % va) == 0;
     const long long items = (long long)(P->H / 2) * (P->W / 8);
@@ -2690,10 +2694,18 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
         // slice-serial: writes every payload word itself (no memset) and never sets the flag
         uint32_t* ctl = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.ctl);
         ProfScope prof(st, CODEC_K_PEE_EXTRACT_SS);
-#define PXS(TT, NTV, IP) hipLaunchKernelGGL((k_pee_extract_ss<TT, NTV, IP, 4>), dim3((unsigned)P->B), dim3(SS_THREADS), 0, st, \
+#define PXSD(TT, NTV, IP, DD) hipLaunchKernelGGL((k_pee_extract_ss<TT, NTV, IP, DD>), dim3((unsigned)P->B), dim3(SS_THREADS), 0, st, \
             static_cast<const TT*>(stego), static_cast<TT*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm), \
             P->lm_words, reinterpret_cast<u64*>(payload_out), P->payload_words, ctl + 1, static_cast<char*>(workspace) + L.sink)
-        if (P->bytes == 2) {
+#define PXS(TT, NTV, IP) PXSD(TT, NTV, IP, 4)
+        // ring depth (knob: 2, 4, 6).  Out of place (slices of <= 64 chunks, e.g. C3) 2: the
+        // ring refills right behind the chunk, 0.0531 -> 0.0517 ms at 256 x 512^2; in place 4
+        // (2: 0.0747 -> 0.0761 ms at 256 x 2048^2; 6 is slower everywhere, 0.064 / 0.086)
+        const long long xd = knob("CODEC_PEE_SSX_D", inplace ? 4 : 2);
+        if (P->bytes == 2 && nt && xd != 4) {
+            if (inplace) { if (xd == 2) PXSD(uint16_t, true, true, 2); else PXSD(uint16_t, true, true, 6); }
+            else { if (xd == 2) PXSD(uint16_t, true, false, 2); else PXSD(uint16_t, true, false, 6); }
+        } else if (P->bytes == 2) {
             if (inplace) { if (nt) PXS(uint16_t, true, true); else PXS(uint16_t, false, true); }
             else { if (nt) PXS(uint16_t, true, false); else PXS(uint16_t, false, false); }
         } else {
@@ -2701,6 +2713,7 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
             else { if (nt) PXS(uint8_t, true, false); else PXS(uint8_t, false, false); }
         }
 #undef PXS
+#undef PXSD
         LAUNCH_CHECK("k_pee_extract_ss");
         if ((P->H & 1) && !inplace) HIP_TRY(pee_copy_last_rows(P, stego, cover_out, st));
         return 0;

@@ -78,7 +78,10 @@ PATHS = {"auto": {}, "onepass": {"CODEC_PEE_ONEPASS": "1"}, "twopass": {"CODEC_P
          # ... with the payload read from global memory (wave-uniform scalar loads; the
          # default stages it in LDS) and with the 4-deep ring in place (default 2)
          "slice_serial_gpay": {"CODEC_PEE_SS": "1", "CODEC_PEE_SS_PAYLDS": "0"},
-         "slice_serial_d4": {"CODEC_PEE_SS": "1", "CODEC_PEE_SS_D": "4"}}
+         "slice_serial_d4": {"CODEC_PEE_SS": "1", "CODEC_PEE_SS_D": "4"},
+         # extract ring depths other than the defaults (2 out of place, 4 in place)
+         "slice_serial_xd4": {"CODEC_PEE_SS": "1", "CODEC_PEE_SSX_D": "4"},
+         "slice_serial_xd6": {"CODEC_PEE_SS": "1", "CODEC_PEE_SSX_D": "6"}}
 
 
 @pytest.fixture(params=sorted(PATHS))
