@@ -408,3 +408,49 @@ def test_gpu_capacity_control(kind, h, w, bsz, inplace, pee_path):
         n = min(len(payloads[i]), int(curves[i][-1]))
         np.testing.assert_array_equal(framing.unpack_bits(host[i], n), payloads[i][:n])
     np.testing.assert_array_equal(cover.cpu().numpy(), covers)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inplace", [False, True])
+@pytest.mark.parametrize("h,w,maxval,tmax", [(65, 64, 4095, 16), (128, 96, None, 5), (66, 128, 4095, 1)])
+def test_gpu_embed_auto_fused_edges(h, w, maxval, tmax, inplace, monkeypatch):
+    """codec_pee_embed_auto's fused launch (slice-serial forced on a small batch) on the
+    shapes it must get right: an odd height (last row copied, never a candidate), a
+    non-default maxval, tmax 1 and 5, and per-slice payloads of 0 bits, exactly the capacity
+    at some T, one bit more, and beyond tmax's capacity (truncated, status 1).  Per-slice T,
+    device T array, stego, map, status/end equal the oracle and the unfused two-launch path."""
+    torch = pytest.importorskip("torch")
+    from codec_tcc_amd import framing
+    from codec_tcc_amd.pee import PeeCodec, lm_bits
+    monkeypatch.setenv("CODEC_PEE_SS", "1")
+    bsz = 6
+    covers = np.stack([synth.ct12(h, w, 900 + i) for i in range(bsz)])
+    curves = [P.capacity_curve(c, tmax, maxval) for c in covers]
+    lens = [0, int(curves[1][0]), int(curves[2][-1]), int(curves[3][min(1, tmax - 1)]) + 1,
+            int(curves[4][-1]) + 37, 5]
+    payloads = [_bits(n, 700 + i) for i, n in enumerate(lens)]
+    runs = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("CODEC_PEE_AUTO_FUSED", fused)
+        codec = PeeCodec(bsz, h, w, dtype="uint16", T="auto", tmax=tmax, maxval=maxval)
+        dev = torch.from_numpy(covers.copy()).cuda()
+        enc = codec.embed(dev, payloads, stego=dev if inplace else None)
+        runs[fused] = (codec, enc, enc.records(), enc.stego.cpu().numpy(), codec.t_slices.cpu().numpy())
+    codec, enc, recs, stego, t_dev = runs["1"]
+    _, enc0, recs0, stego0, t_dev0 = runs["0"]
+    np.testing.assert_array_equal(stego, stego0)
+    np.testing.assert_array_equal(t_dev, t_dev0)
+    for i in range(bsz):
+        T = P.select_T(covers[i], lens[i], tmax, maxval)
+        assert recs[i].T == T == t_dev[i], i
+        st, side = P.pee_embed(covers[i], payloads[i], T, maxval=maxval, truncate=True)
+        assert (recs[i].status, recs[i].end) == (side["status"], side["end"]) == (recs0[i].status, recs0[i].end), i
+        np.testing.assert_array_equal(stego[i], st)
+        np.testing.assert_array_equal(lm_bits(enc, i), side["lm"])
+    words, cover = codec.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words,
+                                 cover=enc.stego if inplace else None)
+    host = words.cpu().numpy()
+    for i in range(bsz):
+        n = min(lens[i], int(curves[i][-1]))
+        np.testing.assert_array_equal(framing.unpack_bits(host[i], n), payloads[i][:n])
+    np.testing.assert_array_equal(cover.cpu().numpy(), covers)
