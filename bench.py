@@ -628,6 +628,7 @@ def main():
                 out["cpu_baseline"]["reference_path"]["pool"] = pools["lsb"]
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.barrier()   # rank 0 ran its C3 leg alone: every rank leaves the group together
         dist.destroy_process_group()
 
 
