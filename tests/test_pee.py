@@ -454,3 +454,50 @@ def test_gpu_embed_auto_fused_edges(h, w, maxval, tmax, inplace, monkeypatch):
         n = min(lens[i], int(curves[i][-1]))
         np.testing.assert_array_equal(framing.unpack_bits(host[i], n), payloads[i][:n])
     np.testing.assert_array_equal(cover.cpu().numpy(), covers)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,W,chars", [(1, 2048, 2048, 1024), (3, 256, 264, 100)])
+def test_gpu_pee_step_graph_replay(B, H, W, chars):
+    """The embed + extract step captured once as a HIP graph (codec_tcc_amd.graphs) and
+    replayed on refreshed inputs (same buffers) gives the eager results: stego, map, meta,
+    payload and restored cover of every replay equal an eager call on the same inputs."""
+    torch = pytest.importorskip("torch")
+    from codec_tcc_amd import graphs
+    from codec_tcc_amd.pee import PeeCodec, lm_bits
+    codec = PeeCodec(B, H, W, dtype="uint16", T=2)
+    cov = torch.empty((B, H, W), dtype=torch.uint16, device="cuda")
+    packed = codec.pack_payloads([synth.payload(chars, 40 + i) for i in range(B)])
+    stego, cov2 = torch.empty_like(cov), torch.empty_like(cov)
+    lm = torch.empty((B, codec.lm_words), dtype=torch.int64, device="cuda")
+    meta = torch.empty((B, 64), dtype=torch.uint8, device="cuda")
+    pw = packed[0].shape[1]
+    outw = torch.empty((B, pw), dtype=torch.int64, device="cuda")
+
+    def step():
+        codec.embed(cov, None, stego=stego, lm=lm, meta=meta, packed=packed, check=False)
+        codec.extract(stego, meta, lm, payload_words=pw, cover=cov2, payload=outw)
+
+    cov.copy_(torch.from_numpy(np.stack([synth.ct12(H, W, 500 + i) for i in range(B)])).cuda())
+    g = graphs.capture(step)
+    for seed in (600, 700):
+        host = np.stack([synth.ct12(H, W, seed + i) for i in range(B)])
+        cov.copy_(torch.from_numpy(host).cuda())
+        g.replay()
+        torch.cuda.synchronize()
+        got = [t.clone() for t in (stego, meta, outw, cov2)]
+        enc = codec.embed(torch.from_numpy(host).cuda(), None, packed=packed)
+        words, back = codec.extract(enc.stego, enc.meta, enc.lm, payload_words=pw)
+        for a, b in zip(got, (enc.stego, enc.meta, words, back)):
+            assert torch.equal(a.view(torch.uint8), b.view(torch.uint8))
+        for b, r in enumerate(enc.records()):   # the map is defined over candidates 0..end
+            bits = np.unpackbits(lm[b].cpu().numpy().view(np.uint8), bitorder="little")[: r.end + 1]
+            np.testing.assert_array_equal(bits.astype(bool), lm_bits(enc, b))
+        np.testing.assert_array_equal(got[3].cpu().numpy(), host)
+        st, side = P.pee_embed(host[0], framing_bits(packed, 0), 2)
+        np.testing.assert_array_equal(got[0][0].cpu().numpy(), st)
+
+
+def framing_bits(packed, b):
+    from codec_tcc_amd import framing
+    return framing.unpack_bits(packed[0][b].cpu().numpy(), packed[1][b])
