@@ -501,3 +501,71 @@ def test_gpu_pee_step_graph_replay(B, H, W, chars):
 def framing_bits(packed, b):
     from codec_tcc_amd import framing
     return framing.unpack_bits(packed[0][b].cpu().numpy(), packed[1][b])
+
+
+# ---- known-answer vectors of the scheme (tests/golden/pee_kat.json, made by the scalar
+# restatement tests/pee_scalar.py via tests/golden/make_pee_golden.py)
+def _kats():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "pee_kat.json")) as f:
+        return json.load(f)
+
+
+def _kat_inputs(k):
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "make_pee_golden", os.path.join(os.path.dirname(__file__), "golden", "make_pee_golden.py"))
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    img = g.make_image(k["kind"], k["h"], k["w"], k["seed"], k["maxval"], k["clip"])
+    mv = int(np.iinfo(img.dtype).max) if k["maxval"] is None else int(k["maxval"])
+    return img, g.payload_bits(k["L_in"], k["seed"]), mv
+
+
+def _kat_id(k):
+    return f'{k["kind"]}-{k["h"]}x{k["w"]}-T{k["T"]}-{k["rule"]}'
+
+
+@pytest.mark.parametrize("k", _kats(), ids=_kat_id)
+def test_oracle_matches_scheme_kats(k):
+    """The vectorised oracle (pee_cpu) reproduces the scalar restatement's known answers:
+    stego digest, end, capacity, status, location map; extract inverts it exactly."""
+    import hashlib
+    import pee_scalar as S
+    img, bits, mv = _kat_inputs(k)
+    st, side = P.pee_embed(img, bits, k["T"], maxval=mv, truncate=True)
+    assert hashlib.sha256(st.tobytes()).hexdigest() == k["stego_sha256"]
+    assert (side["L"], side["end"], side["capacity"], side["status"]) == (k["L"], k["end"], k["capacity"], k["status"])
+    assert np.packbits(side["lm"], bitorder="little").tobytes().hex() == k["lm_hex"]
+    got, back = P.pee_extract(st, side)
+    np.testing.assert_array_equal(got, bits[: k["L"]])
+    np.testing.assert_array_equal(back, img)
+    # and the scalar restatement itself still produces them
+    st2, side2 = S.embed(img.tolist(), [int(b) for b in bits], k["T"], mv)
+    assert np.array_equal(np.array(st2, dtype=img.dtype), st) and side2["end"] == k["end"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ss", ["default", "slice_serial"])
+@pytest.mark.parametrize("k", _kats(), ids=_kat_id)
+def test_gpu_matches_scheme_kats(k, ss, monkeypatch):
+    """The HIP path on each known-answer input: stego digest, end, status, embedded bit count
+    and location map equal the committed answers; extract returns the payload and cover."""
+    import hashlib
+    torch = pytest.importorskip("torch")
+    from codec_tcc_amd import framing
+    from codec_tcc_amd.pee import PeeCodec, lm_bits
+    if ss == "slice_serial":
+        monkeypatch.setenv("CODEC_PEE_SS", "1")
+    img, bits, mv = _kat_inputs(k)
+    codec = PeeCodec(1, k["h"], k["w"], dtype=str(img.dtype), T=k["T"], maxval=mv)
+    enc = codec.embed(torch.from_numpy(img[None]).cuda(), [bits])
+    r = enc.records()[0]
+    assert (r.end, r.status) == (k["end"], k["status"])
+    assert hashlib.sha256(enc.stego[0].cpu().numpy().tobytes()).hexdigest() == k["stego_sha256"]
+    assert np.packbits(lm_bits(enc, 0), bitorder="little").tobytes().hex() == k["lm_hex"]
+    words, cover = codec.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words)
+    np.testing.assert_array_equal(framing.unpack_bits(words[0].cpu().numpy(), k["L"]), bits[: k["L"]])
+    np.testing.assert_array_equal(cover[0].cpu().numpy(), img)
