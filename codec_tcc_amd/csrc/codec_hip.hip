@@ -2124,6 +2124,69 @@ __global__ __launch_bounds__(NTH) void k_restore_gs(const T* __restrict__ stego,
     }
 }
 
+// Slice-serial variant (batches of at least one slice per CU, small slices: C3's 256 x 512^2):
+// one 1024-thread workgroup per slice.  D vectors per thread stay in flight in a register
+// ring while the workgroup copies its slice in order -- a pure straight-line copy, so hipcc
+// counts vmcnt exactly and never drains the ring -- then fixes up the window hull (rewrites
+// the <= a few thousand pixels of span_lo/span_len with their restored values; the copy's
+// stores to them completed at the barrier before).  The slice's payload gather runs first,
+// its pixel loads behind the ring's.  At C3 the grid-stride pass streams 2048 short-lived
+// workgroups (0.073 ms); this keeps one contiguous region per CU, the order this chip copies
+// fastest in.
+template <typename T, bool NT, int D, int G>
+__global__ __launch_bounds__(1024) void k_restore_ss(const T* __restrict__ stego, T* __restrict__ cover, uint32_t npx,
+                                                     const codec_slice_meta* __restrict__ meta,
+                                                     const u64* __restrict__ maps_all, int mw,
+                                                     u64* __restrict__ payload_out, int pw, int gather_late) {
+    typedef typename Vec8<T>::type V;
+    const int b = blockIdx.x;
+    const uint32_t t = threadIdx.x;
+    const uint32_t nv = npx / 8;                  // a multiple of 1024 * D * G (host check)
+    const V* src = reinterpret_cast<const V*>(stego + (size_t)b * npx);
+    V* dst = reinterpret_cast<V*>(cover + (size_t)b * npx);
+    V r[D][G];
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int g = 0; g < G; ++g) r[d][g] = ldv<NT>(src + (uint32_t)(d * G + g) * 1024u + t);
+    if (payload_out && !gather_late) gather_body<T, 1024>(stego, (long long)npx, meta, payload_out, pw, b);
+    const uint32_t step = 1024u * D * G;
+    uint32_t base = 0;
+    for (; base + step < nv; base += step) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const uint32_t idx = base + (uint32_t)(d * G + g) * 1024u + t;
+                stv<NT>(dst + idx, r[d][g]);
+                r[d][g] = ldv<NT>(src + idx + step);   // refill from the next group
+            }
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int g = 0; g < G; ++g) stv<NT>(dst + base + (uint32_t)(d * G + g) * 1024u + t, r[d][g]);
+    if (payload_out && gather_late) gather_body<T, 1024>(stego, (long long)npx, meta, payload_out, pw, b);
+    __syncthreads();   // waits for every store above (vmcnt(0)) before the hull is rewritten
+    const codec_slice_meta* M = meta + b;
+    const long long lo = M->span_lo, len = M->span_len;
+    if (len > 0) {
+        const uint32_t first = (uint32_t)(lo / 8), last = (uint32_t)((lo + len + 7) / 8);
+        const u64* maps = maps_all + (size_t)b * mw;
+        for (uint32_t i = t; i < last - first; i += 1024u) {
+            uint32_t idx = first + i;
+            if (idx >= nv) idx -= nv;
+            const long long q0 = (long long)idx * 8;
+            if (span_hit(q0, lo, len, npx)) {
+                V v = src[idx];
+                restore_chunk<T>(v, q0, M, maps, npx);
+                dst[idx] = v;
+            }
+        }
+    }
+}
+
 // scalar variant for slices whose rows are not 8-pixel aligned
 template <typename T>
 __global__ __launch_bounds__(256) void k_restore_scalar(const T* __restrict__ stego, T* __restrict__ cover,
@@ -2777,7 +2840,31 @@ int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps
         } else {
         const long long nchunks = npx / 8;
         const bool gs = knob("CODEC_RESTORE_GS", 1) != 0 && (npx % 8) == 0 && nchunks * P->B < 0xFFFFFFFFLL;
-        if (gs) {
+        // slice-serial (k_restore_ss): CODEC_RESTORE_SS -1 = batches of >= one slice per CU
+        // with slices of <= CODEC_RESTORE_SS_MAXPX pixels, 0 = never, 1 = wherever it applies
+        const long long ssk = knob("CODEC_RESTORE_SS", -1);
+        const int ncu = device_cu_count();
+        const bool ss = ssk != 0 && (npx % 65536) == 0 && npx <= 0x7FFFFFFFLL &&
+                        (ssk == 1 || (P->B >= ncu && npx <= knob("CODEC_RESTORE_SS_MAXPX", 1 << 20)));
+        if (ss) {
+            ProfScope prof(st, CODEC_K_RESTORE);
+            const bool ntg = knob("CODEC_NT", 1) != 0;
+            const u64* mp = reinterpret_cast<const u64*>(maps);
+            u64* po = reinterpret_cast<u64*>(payload_out);
+            // vectors in flight per thread (A/B knob CODEC_RESTORE_SS_DEPTH: 4, 8 or 16)
+            const long long dep = knob("CODEC_RESTORE_SS_DEPTH", 8);
+#define RSS(TT, NTV, DD) hipLaunchKernelGGL((k_restore_ss<TT, NTV, DD, 2>), dim3((unsigned)P->B), dim3(1024), 0, st, \
+                static_cast<const TT*>(stego), static_cast<TT*>(cover_out), (uint32_t)npx, meta, mp, P->map_words, po, \
+                P->payload_words, glate)
+            const int glate = (int)knob("CODEC_RESTORE_SS_GLATE", 0);   // payload gather after the copy (A/B)
+            if (P->in_bytes == 2 && ntg && dep == 16 && npx % 131072 == 0) RSS(uint16_t, true, 8);
+            else if (P->in_bytes == 2 && ntg && dep == 4 && npx % 32768 == 0) RSS(uint16_t, true, 2);
+            else if (P->in_bytes == 2) { if (ntg) RSS(uint16_t, true, 4); else RSS(uint16_t, false, 4); }
+            else { if (ntg) RSS(uint8_t, true, 4); else RSS(uint8_t, false, 4); }
+#undef RSS
+            LAUNCH_CHECK("k_restore_ss");
+            gathered = payload_out != nullptr;
+        } else if (gs) {
             const bool ntg = knob("CODEC_NT", 1) != 0;
             const long long g = knob("CODEC_RESTORE_GS_WGS", 1 << 30);   // default: one 1024-chunk block per WG
             const uint32_t total = (uint32_t)(nchunks * P->B);

@@ -2308,18 +2308,6 @@ static PeeWs pee_ws(const codec_pee_params* P) {
     return L;
 }
 
-// slice-serial dispatch: the batch fills whole rounds of one workgroup per CU
-static int device_cu_count() {
-    static int cached[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cached[dev]) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-        cached[dev] = n;
-    }
-    return cached[dev];
-}
 
 // Measured at B = 256 (profiles/r02/ss_vs_lookback.json): in place the slice-serial pass
 // wins at every size (2048^2 embed 0.145 -> 0.111 ms, extract 0.115 -> 0.109); out of place

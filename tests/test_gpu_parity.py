@@ -362,3 +362,33 @@ def test_workspace_reuse_stays_clean(dtype, kinds, monkeypatch):
             assert recs[i].s == exp["s"], (step, kind, i)
             assert recs[i].start_offset == exp["start_offset"], (step, kind, i)
             np.testing.assert_array_equal(stego[i], exp["stego"])
+
+
+@pytest.mark.parametrize("restore", ["ss", "ss_d4", "ss_d16", "ss_late", "gs"])
+@pytest.mark.parametrize("kind,h,w,bsz,chars", [("ct12", 512, 512, 5, 1024), ("u8", 256, 256, 3, 2500),
+                                                ("u16", 256, 512, 2, 4000), ("ct12", 256, 256, 4, 3000)])
+def test_restore_paths_vs_oracle(kind, h, w, bsz, chars, restore, monkeypatch):
+    """codec_extract's out-of-place restore through the slice-serial pass (k_restore_ss: ring
+    copy + window-hull rewrite + fused payload gather; forced here, the default for batches of
+    >= one slice per CU) and the grid-stride pass: payload bits and restored cover exact,
+    stego vs the oracle; long payloads make windows wrap past the slice end."""
+    monkeypatch.setenv("CODEC_RESTORE_SS", "0" if restore == "gs" else "1")
+    if restore in ("ss_d4", "ss_d16"):   # ring depths other than the default 8 vectors per thread
+        monkeypatch.setenv("CODEC_RESTORE_SS_DEPTH", restore[4:])
+    if restore == "ss_late":             # payload gather after the copy instead of before it
+        monkeypatch.setenv("CODEC_RESTORE_SS_GLATE", "1")
+    gen = synth.GENERATORS[kind]
+    covers = np.stack([gen(h, w, 300 + i) for i in range(bsz)])
+    msgs = [synth.payload(chars - 17 * i, 60 + i) for i in range(bsz)]
+    codec = Codec(bsz, h, w, dtype=str(covers.dtype), beta=0.4, block=16)
+    enc = codec.encode(torch.from_numpy(covers).cuda(), msgs)
+    recs = enc.records()
+    bits, cover = K.decode(enc)
+    stego = enc.stego.cpu().numpy()
+    for i in range(bsz):
+        mb = R.message_to_bits(msgs[i])
+        exp = R.encode_slice(covers[i], mb, beta=0.4, sb=16)
+        assert recs[i].s == exp["s"] and recs[i].start_offset == exp["start_offset"]
+        np.testing.assert_array_equal(stego[i], exp["stego"])
+        assert framing.bits_to_str(bits[i]) == mb
+    np.testing.assert_array_equal(cover.cpu().numpy(), covers)
