@@ -82,14 +82,19 @@ def pmc_traffic(kernel: str, b: int, h: int, w: int, kind: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, tools/pmc_summary.py: FETCH_SIZE x2 (gfx950 correction)
     + WRITE_SIZE, KB -> bytes), when it was collected on this exact configuration."""
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-    except (OSError, ValueError):
-        return None
-    cfg = d.get("config", {})
-    if (cfg.get("batch"), cfg.get("h"), cfg.get("w"), cfg.get("kind")) != (b, h, w, kind):
+    d = None
+    for name in ("pmc_traffic.json", "pmc_traffic_c3.json"):   # headline shape, C3 shape
+        path = os.path.join(REPO, "profiles", name)
+        try:
+            with open(path) as f:
+                cand = json.load(f)
+        except (OSError, ValueError):
+            continue
+        cfg = cand.get("config", {})
+        if (cfg.get("batch"), cfg.get("h"), cfg.get("w"), cfg.get("kind")) == (b, h, w, kind):
+            d = cand
+            break
+    if d is None:
         return None
     ks = d.get("kernels", {})
     k = ks.get(kernel)
@@ -388,14 +393,14 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
         prefix_px = sum(((r.end // 4) + 1) * 16 for r in recs if r.end >= 0)
         by = prefix_px * 2 + prefix_px // 2 * 2
         if emb in ("k_pee_embed_ss_auto", "k_pee_embed_ss", "k_pee_embed1") and kern[emb] > 0:
-            res["roofline"] = _roof(emb, by, kern[emb], pmc_traffic(emb + inst[emb], B, H, W, kind))
+            res["roofline"] = _roof(emb, by, kern[emb], pmc_traffic(emb.replace("_auto", "") + inst[emb], B, H, W, kind))
         if ext and kern[ext] > 0:
             # extract reads the same items plus their location-map words, writes the rows back
             res["extract_roofline"] = _roof(ext, by, kern[ext], pmc_traffic(ext + inst[ext], B, H, W, kind))
         return res
     if emb:
         res["roofline"] = _roof(emb, B * H * W * 4, kern[emb],   # read cover + write stego
-                                pmc_traffic(emb + inst.get(emb, ""), B, H, W, kind))
+                                pmc_traffic(emb.replace("_auto", "") + inst.get(emb, ""), B, H, W, kind))
     if ext:
         res["extract_roofline"] = _roof(ext, B * H * W * 4, kern[ext], pmc_traffic(ext + inst[ext], B, H, W, kind))
     t_emb = sum(kern.get(k, 0.0) for k in ("k_pee_embed_ss_auto", "k_pee_embed_ss", "k_pee_embed1", "k_pee_scan", "k_pee_locate",
