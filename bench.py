@@ -78,10 +78,15 @@ def make_covers(torch, kind, b, h, w, device, seed):
     return out
 
 
-def pmc_traffic(kernel: str, b: int, h: int, w: int, kind: str):
+def pmc_traffic(kernel: str, b: int, h: int, w: int, kind: str, targs=None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, tools/pmc_summary.py: FETCH_SIZE x2 (gfx950 correction)
-    + WRITE_SIZE, KB -> bytes), when it was collected on this exact configuration."""
+    + WRITE_SIZE, KB -> bytes), when it was collected on this exact configuration.
+
+    The summaries are keyed per template instantiation (`k<unsigned short, true, ...>`):
+    `kernel` is the bare name, and `targs` {index: "value"} selects among its
+    instantiations by template argument (e.g. {2: "true"} = the in-place PEE kernels);
+    the lookup succeeds only when exactly one instantiation matches."""
     d = None
     for name in ("pmc_traffic.json", "pmc_traffic_c3.json"):   # headline shape, C3 shape
         path = os.path.join(REPO, "profiles", name)
@@ -96,14 +101,18 @@ def pmc_traffic(kernel: str, b: int, h: int, w: int, kind: str):
             break
     if d is None:
         return None
-    ks = d.get("kernels", {})
-    k = ks.get(kernel)
-    if not k:   # keyed per template instantiation: accept the unique one of this kernel
-        hits = [v for n, v in ks.items() if n.split("<")[0] == kernel]
-        if len(hits) != 1:
-            return None
-        k = hits[0]
-    return {"hbm_bytes_per_launch": k["hbm_bytes_per_launch"], "source": d.get("source", path)}
+    hits = []
+    for n, v in d.get("kernels", {}).items():
+        bare, _, rest = n.partition("<")
+        if bare != kernel:
+            continue
+        args = [a.strip() for a in rest.rstrip(">").split(",")] if rest else []
+        if all(i < len(args) and args[i] == val for i, val in (targs or {}).items()):
+            hits.append((n, v))
+    if len(hits) != 1:
+        return None
+    name, k = hits[0]
+    return {"hbm_bytes_per_launch": k["hbm_bytes_per_launch"], "source": d.get("source", path), "instance": name}
 
 
 def _cpu_model() -> str:
@@ -278,6 +287,7 @@ def _roof(kernel, by, t_ms, traffic=None):
     if traffic is not None:
         r["traffic"] = traffic["hbm_bytes_per_launch"]
         r["traffic_source"] = traffic["source"]
+        r["traffic_instance"] = traffic.get("instance")
     return r
 
 
@@ -361,14 +371,20 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
     if T == "auto":
         res["T_chosen"] = {str(t): int(sum(1 for r in recs if r.T == t)) for t in sorted({r.T for r in recs})}
     if xch is not None:
+        # every timed gather was wide enough (device-side count, read once now), and this
+        # rank's rows of the last one are its own meta + map prefix (zeroed past `end`)
+        narrow = xch.overflows()
         om, ol = xch.own_rows(rank)
-        res["exchange_ok"] = bool(torch.equal(om.contiguous().view(torch.uint8)[:, : _lib.PEE_META_BYTES], meta)) and \
-            bool(torch.equal(ol, lm[:, : xch.lm_words]))
+        res["exchange_ok"] = narrow == 0 and \
+            bool(torch.equal(om.contiguous().view(torch.uint8)[:, : _lib.PEE_META_BYTES], meta)) and \
+            bool(torch.equal(ol, D.map_prefix(meta, lm, xch.lm_words)))
         t_g = _timed(torch, dist, world, dev, lambda: (xch.start(meta, lm), xch.join()), steps) / steps
         t_k = _timed(torch, dist, world, dev, kernels, steps) / steps
         res["distributed"] = {
             "allgather_ms": round(t_g * 1e3, 4),
-            "allgather_bytes": int((xch.meta_padded.numel() + xch._lm_padded.numel()) * 8),
+            "allgather_bytes": int(xch._out.numel() * 8),
+            "collectives_per_step": 1,
+            "narrow_gathers": narrow,
             "lm_words_gathered": xch.lm_words,
             "kernels_only_ms_per_step": round(t_k * 1e3, 4),
             "kernels_only_value": round(B * H * W * world / t_k / 1e6, 1)}
@@ -379,30 +395,41 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
     emb = next((k for k in ("k_pee_embed_ss_auto", "k_pee_embed_ss", "k_pee_embed1", "k_pee_scan") if k in kern), None)
     ext = next((k for k in ("k_pee_extract_ss", "k_pee_extract1") if k in kern), None)
     res["embed_kernel"], res["extract_kernel"] = emb, ext
-    ss_d = os.environ.get("CODEC_PEE_SS_D", "2") if inplace else "4"   # ring depth (codec_pee.hip dispatch)
-    inst = {"k_pee_embed_ss": "<unsigned short, true, %s, %s, true>" % ("true" if inplace else "false", ss_d),
-            # T = 'auto' where the embed is slice-serial: the capacity phase fused in (codec_pee_embed_auto)
-            "k_pee_embed_ss_auto": "<unsigned short, true, %s, %s, true, true>" % (("true", "2") if inplace
-                                                                                 else ("false", "4")),
-            "k_pee_extract_ss": "<unsigned short, true, %s>" % ("true, 4" if inplace else "false, 2"),
-            "k_pee_embed1": "<unsigned short, true, %s>" % ("true" if inplace else "false"),
-            "k_pee_extract1": "<unsigned short, true, %s>" % ("true" if inplace else "false")}
+    # PMC instantiation of each tag: template argument 2 is INPLACE for every PEE kernel; the
+    # slice-serial embed's argument 5 is AUTO (the capacity phase fused in, codec_pee_embed_auto)
+    ip = "true" if inplace else "false"
+    targs = {"k_pee_embed_ss": ("k_pee_embed_ss", {2: ip, 5: "false"}),
+             "k_pee_embed_ss_auto": ("k_pee_embed_ss", {2: ip, 5: "true"}),
+             "k_pee_extract_ss": ("k_pee_extract_ss", {2: ip}),
+             "k_pee_embed1": ("k_pee_embed1", {2: ip}),
+             "k_pee_extract1": ("k_pee_extract1", {2: ip})}
+
+    def traffic(tag):
+        name, ta = targs.get(tag, (tag, None))
+        return pmc_traffic(name, B, H, W, kind, ta)
+
     if inplace:
         # algorithmic bytes: every 8-px x 2-row item up to the one holding `end` is read
         # (candidates + their neighbours), its candidate row written back
         prefix_px = sum(((r.end // 4) + 1) * 16 for r in recs if r.end >= 0)
         by = prefix_px * 2 + prefix_px // 2 * 2
+        # only the prefix is processed in place: `value` counts those pixels; the whole
+        # slices' pixel rate (what the out-of-place step processes) is `nominal_mpx_s`
+        res["nominal_mpx_s"] = res["value"]
+        res["value"] = round(prefix_px * world * steps / el / 1e6, 1)
+        res["value_basis"] = ("pixels read up to each slice's `end` (items of 8 px x 2 rows); nominal_mpx_s "
+                              "counts every pixel of the batch")
+        res["prefix_pixels_per_step"] = int(prefix_px)
         if emb in ("k_pee_embed_ss_auto", "k_pee_embed_ss", "k_pee_embed1") and kern[emb] > 0:
-            res["roofline"] = _roof(emb, by, kern[emb], pmc_traffic(emb.replace("_auto", "") + inst[emb], B, H, W, kind))
+            res["roofline"] = _roof(emb, by, kern[emb], traffic(emb))
         if ext and kern[ext] > 0:
             # extract reads the same items plus their location-map words, writes the rows back
-            res["extract_roofline"] = _roof(ext, by, kern[ext], pmc_traffic(ext + inst[ext], B, H, W, kind))
+            res["extract_roofline"] = _roof(ext, by, kern[ext], traffic(ext))
         return res
     if emb:
-        res["roofline"] = _roof(emb, B * H * W * 4, kern[emb],   # read cover + write stego
-                                pmc_traffic(emb.replace("_auto", "") + inst.get(emb, ""), B, H, W, kind))
+        res["roofline"] = _roof(emb, B * H * W * 4, kern[emb], traffic(emb))   # read cover + write stego
     if ext:
-        res["extract_roofline"] = _roof(ext, B * H * W * 4, kern[ext], pmc_traffic(ext + inst[ext], B, H, W, kind))
+        res["extract_roofline"] = _roof(ext, B * H * W * 4, kern[ext], traffic(ext))
     t_emb = sum(kern.get(k, 0.0) for k in ("k_pee_embed_ss_auto", "k_pee_embed_ss", "k_pee_embed1", "k_pee_scan", "k_pee_locate",
                                            "k_pee_embed")) / 1e3
     if t_emb > 0:
@@ -433,7 +460,7 @@ def bench_lsb(args, torch, dist, world, rank, dev, covers, B, H, W, *, exchange=
     xch = D.RecordExchange(B, pl.map_words, world, dev) if exchange else None
 
     def kernels():
-        codec.encode(covers, pl, stego=stego, maps=maps, meta=meta)
+        codec.encode(covers, pl, stego=stego, maps=maps, meta=meta, check=False)
         if xch is not None:
             xch.mark()
         codec.decode(stego, maps, meta, payload_words=pl.payload_words, map_words=pl.map_words,
@@ -453,9 +480,12 @@ def bench_lsb(args, torch, dist, world, rank, dev, covers, B, H, W, *, exchange=
     cover_ok = bool(torch.equal(cover_out.view(torch.int16), covers.view(torch.int16)))
     pay_ok = payload_equal(payload_out, pl.words, [r.total_used for r in recs]) and \
         all(r.total_used == n for r, n in zip(recs, pl.lengths))
+    # a non-zero status (e.g. 2 = a split decision timed out) means s may differ from the
+    # reference's decision even though the round trip itself is exact
+    status_ok = all(r.status == 0 for r in recs)
     res = {"value": round(B * H * W * world * steps / el / 1e6, 1), "unit": "Mpixels/s",
-           "ms_per_step": round(el / steps * 1e3, 4), "roundtrip_ok": cover_ok and pay_ok,
-           "cover_ok": cover_ok, "payload_ok": pay_ok, "s_values": sorted({r.s for r in recs}),
+           "ms_per_step": round(el / steps * 1e3, 4), "roundtrip_ok": cover_ok and pay_ok and status_ok,
+           "cover_ok": cover_ok, "payload_ok": pay_ok, "status_ok": status_ok, "s_values": sorted({r.s for r in recs}),
            "path": "the reference's pixel path (bit-plane LSB embed + true decode, src/codec.py:412-487, "
                    "752-793), bit-exact with it"}
     if xch is not None:   # this rank's rows of the gathered records are its own packed records
@@ -489,7 +519,7 @@ def bench_lsb_inplace(args, torch, dist, world, dev, covers, B, H, W):
     pay = torch.empty((B, pl.payload_words), dtype=torch.int64, device=dev)
 
     def step():
-        codec.encode(work, pl, stego=work, maps=maps, meta=meta)
+        codec.encode(work, pl, stego=work, maps=maps, meta=meta, check=False)
         codec.decode(work, maps, meta, payload_words=pl.payload_words, map_words=pl.map_words, cover=work,
                      payload=pay)
 
@@ -500,8 +530,9 @@ def bench_lsb_inplace(args, torch, dist, world, dev, covers, B, H, W):
     recs = ct.meta_records(meta)
     cover_ok = bool(torch.equal(work.view(torch.int16), covers.view(torch.int16)))
     pay_ok = payload_equal(pay, pl.words, [r.total_used for r in recs])
+    status_ok = all(r.status == 0 for r in recs)
     res = {"value": round(B * H * W * world * args.steps / el / 1e6, 1), "unit": "Mpixels/s",
-           "ms_per_step": round(el / args.steps * 1e3, 4), "roundtrip_ok": cover_ok and pay_ok,
+           "ms_per_step": round(el / args.steps * 1e3, 4), "roundtrip_ok": cover_ok and pay_ok and status_ok,
            "kernels_ms": {k: round(v, 4) for k, v in kern.items()}}
     rk = next((k for k in ("k_scan_rows_read", "k_scan_read") if k in kern), None)
     if rk:
@@ -572,8 +603,80 @@ def bench_quality(args, torch, covers, stego, B, H, W):
     return res
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` without a launcher: start N fresh rank processes of this script
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, as torchrun sets them),
+    wait for all of them and forward rank 0's JSON line.  This process never touches the GPU
+    (no HIP call, no torch.cuda query) and never execs: the ranks are child processes, and a
+    rank that fails stops the others (exit status of the first failure)."""
+    import signal
+    import subprocess
+    n = int(args.gpus)
+    env0 = dict(os.environ)
+    env0.setdefault("MASTER_ADDR", "127.0.0.1")
+    env0["MASTER_PORT"] = str(_free_port()) if "MASTER_PORT" not in os.environ else os.environ["MASTER_PORT"]
+    env0["WORLD_SIZE"] = str(n)
+    env0["LOCAL_WORLD_SIZE"] = str(n)
+    env0.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC (RCCL / cross-process tensors)
+    cmd = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+    procs = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r), GROUP_RANK="0")
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else None,
+                                      start_new_session=True, text=True))
+    line = None
+    rc = 0
+    try:
+        for raw in procs[0].stdout:          # rank 0's output: forward the JSON line, echo the rest
+            if raw.startswith("{"):
+                line = raw.strip()
+            else:
+                sys.stderr.write(raw)
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    for q in procs:          # one rank failed: the others would wait forever
+                        try:
+                            os.killpg(q.pid, signal.SIGTERM)
+                        except ProcessLookupError:
+                            pass
+            time.sleep(0.05)
+    finally:
+        for q in procs:
+            try:
+                os.killpg(q.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+    if rc == 0 and line:
+        print(line, flush=True)
+    elif rc == 0:
+        sys.stderr.write("bench.py: rank 0 printed no JSON line\n")
+        rc = 1
+    return rc
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))          # before anything touches the GPU
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world} (the launcher started a different "
+                 "number of ranks)")
     import torch
     import torch.distributed as dist
 
@@ -586,7 +689,10 @@ def main():
         pools["pee"] = cpu_baseline_pool(args, "pee")
         if args.cpu_ref_seconds > 0:
             pools["lsb"] = cpu_baseline_pool(args, "lsb")
-    ndev = torch.cuda.device_count()
+    ndev = torch.cuda.device_count()   # counting devices does not initialise the GPU
+    if world > 1 and args.backend == "nccl" and ndev < world:
+        sys.exit(f"bench.py: {world} ranks over RCCL need {world} GPUs, {ndev} visible "
+                 "(--backend gloo rehearses the multi-rank path with several ranks per GPU)")
     if world > 1:
         torch.cuda.set_device(local % ndev)
         if args.backend == "nccl":

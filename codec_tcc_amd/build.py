@@ -33,24 +33,55 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
-def needs_build() -> bool:
-    if not os.path.exists(OUT):
+def _obj(src: str) -> str:
+    return os.path.join(HERE, "build_obj", os.path.basename(src) + ".o")
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
         return True
-    t = os.path.getmtime(OUT)
-    deps = SRCS + HDRS + [os.path.join(INC, "codec_tcc.h"), __file__]
+    t = os.path.getmtime(target)
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _common_deps():
+    return HDRS + [os.path.join(INC, "codec_tcc.h"), __file__]
+
+
+def needs_build() -> bool:
+    return _stale(OUT, SRCS + _common_deps())
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile each translation unit to an object (in parallel, only the stale ones), then
+    link the shared library."""
     if not force and not needs_build():
         return OUT
+    os.makedirs(os.path.join(HERE, "build_obj"), exist_ok=True)
+    jobs = []
+    for src in SRCS:
+        obj = _obj(src)
+        if force or _stale(obj, [src] + _common_deps()):
+            cmd = [hipcc(), *[f for f in FLAGS if f != "-shared"], f"-I{INC}", "-c", src, "-o", obj + ".tmp"]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            jobs.append((obj, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)))
+    errs = []
+    for obj, p in jobs:
+        _out, err = p.communicate()
+        if p.returncode != 0:
+            errs.append(f"hipcc failed ({p.returncode}) for {os.path.basename(obj)}:\n{err[-6000:]}")
+        else:
+            os.replace(obj + ".tmp", obj)
+    if errs:
+        raise RuntimeError("\n".join(errs))
     tmp = OUT + ".tmp"
-    cmd = [hipcc(), *FLAGS, f"-I{INC}", *SRCS, "-o", tmp]
+    cmd = [hipcc(), *FLAGS, *[_obj(s) for s in SRCS], "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-6000:]}")
+        raise RuntimeError(f"hipcc link failed ({r.returncode}):\n{r.stderr[-6000:]}")
     os.replace(tmp, OUT)
     return OUT
 

@@ -154,6 +154,20 @@ def meta_dict(m: _lib.SliceMeta) -> dict:
     }
 
 
+def check_status(recs, what: str = "codec_encode"):
+    """Raise when a slice's meta.status says its decision may differ from the reference's:
+    1 = the log2 table does not cover the slice (no exact entropy), 2 = a split decision's
+    plane workgroup never published (CODEC_FLAG_DECIDE_TIMEOUT: that plane's MI is unknown,
+    so `s` can differ).  The round trip of such a slice is still exact (decode reads s from
+    the meta), which is why a caller has to look."""
+    bad = [(i, r.status) for i, r in enumerate(recs) if r.status != 0]
+    if bad:
+        why = {1: "log2 table too short", 2: "split decision timed out"}
+        raise RuntimeError(f"{what}: slices without the reference's decision: "
+                           + ", ".join(f"{i} (status {s}: {why.get(s, 'unknown')})" for i, s in bad[:8])
+                           + (" ..." if len(bad) > 8 else ""))
+
+
 @dataclass
 class Encoded:
     stego: object      # torch [B,H,W]
@@ -230,7 +244,10 @@ class Codec:
             raise ValueError("pixel tensor must be contiguous")
 
     # -- encode: codec_encode (= codec_plan + codec_embed, fused when the dtypes allow)
-    def encode(self, covers, payloads, *, stego=None, maps=None, meta=None) -> Encoded:
+    def encode(self, covers, payloads, *, stego=None, maps=None, meta=None, check: bool = True) -> Encoded:
+        """check=True (default) reads the per-slice status back (one sync) and raises when a
+        slice's decision is not the reference's (check_status); check=False keeps the call
+        asynchronous (benchmarks, graph capture) -- inspect enc.records() afterwards."""
         torch = _torch()
         self._check_pixels(covers, self.in_bytes)
         pl = payloads if isinstance(payloads, Payloads) else make_payloads(payloads, self.device)
@@ -249,10 +266,12 @@ class Codec:
                                     self.lut.numel(), pl.table.data_ptr(), pl.classes.data_ptr(),
                                     meta.data_ptr(), self.workspace.data_ptr(), self.workspace.numel(),
                                     pl.words.data_ptr(), maps.data_ptr(), st), "codec_encode")
+        if check:
+            check_status(meta_records(meta), "codec_encode")
         return Encoded(stego=stego, maps=maps, meta=meta, payloads=pl, config=dict(self.config))
 
     # -- plan only (decomposition + offset, no payload writes)
-    def plan(self, covers, payloads, *, stego=None, meta=None):
+    def plan(self, covers, payloads, *, stego=None, meta=None, check: bool = True):
         torch = _torch()
         self._check_pixels(covers, self.in_bytes)
         pl = payloads if isinstance(payloads, Payloads) else make_payloads(payloads, self.device)
@@ -264,6 +283,8 @@ class Codec:
                                   self.lut.data_ptr(), self.lut.numel(), pl.table.data_ptr(),
                                   pl.classes.data_ptr(), meta.data_ptr(), self.workspace.data_ptr(),
                                   self.workspace.numel(), _stream()), "codec_plan")
+        if check:
+            check_status(meta_records(meta), "codec_plan")
         return meta
 
     # -- decode: payload recovery + cover restore
@@ -330,10 +351,24 @@ def _as_batch(covers):
     return covers.contiguous()
 
 
-def encode(covers, payloads: Sequence, *, beta: float = 0.4, block: int = 16, align: bool = False,
-           mode: str = "hybrid", nbits: Optional[int] = None) -> Encoded:
-    """Embed one payload per slice.  Defaults are main()'s (codec.py:868 beta=0.4,
-    codec.py:875 search_block_size=16)."""
+def encode(covers, payloads: Sequence, *, method: str = "lsb", beta: float = 0.4, block: int = 16,
+           align: bool = False, mode: str = "hybrid", nbits: Optional[int] = None, T=2, tmax: int = 16,
+           maxval: Optional[int] = None):
+    """Embed one payload per slice.
+
+    method="lsb" (default): the reference's bit-plane scheme, bit-exact with src/codec.py;
+    defaults are main()'s (codec.py:868 beta=0.4, codec.py:875 search_block_size=16).
+    Returns an Encoded.
+    method="pee": MED-predictor prediction-error expansion (the north star's algorithm; the
+    reference has none): T = expansion threshold or "auto" (capacity control,
+    smallest T <= tmax per slice), maxval = largest legal pixel value (4095 for 12-bit data).
+    Returns a pee.PeeEncoded; beta/block/align/mode/nbits do not apply.
+    decode() takes either result."""
+    if method == "pee":
+        from . import pee
+        return pee.encode(covers, payloads, T=T, tmax=tmax, maxval=maxval)
+    if method != "lsb":
+        raise ValueError("method must be 'lsb' or 'pee'")
     _require_gpu()
     covers = _as_batch(covers)
     if isinstance(payloads, (str, bytes, bytearray)):
@@ -343,9 +378,13 @@ def encode(covers, payloads: Sequence, *, beta: float = 0.4, block: int = 16, al
     return codec.encode(covers, payloads)
 
 
-def decode(enc: Encoded, *, restore: bool = True):
+def decode(enc, *, restore: bool = True):
     """True extraction.  Returns (payload_bit_lists, cover) where payload_bit_lists[b] is a
-    numpy 0/1 vector of the embedded bits in message order and cover the restored [B,H,W]."""
+    numpy 0/1 vector of the embedded bits in message order and cover the restored [B,H,W]
+    (LSB: positional recovery; MED-PEE: the exact inverse)."""
+    from . import pee
+    if isinstance(enc, pee.PeeEncoded):
+        return pee.decode(enc, restore=restore)
     _require_gpu()
     c = _codec_for(tuple(enc.stego.shape), _in_dtype_name(enc), **_codec_kw(enc))
     words, cover = c.decode(enc.stego, enc.maps, enc.meta, payload_words=enc.payloads.payload_words,

@@ -1121,6 +1121,10 @@ struct ListTerm {
 #endif
 // split decision: a plane workgroup's "no value" (a NaN bit pattern, never a real H(X,Y))
 #define PLANE_NONE 0x7FF8DEAD00000001ull
+// a split decision's main workgroup that stopped waiting for a plane slot marks it ABANDONED
+// (CAS 0 -> ABANDONED); the late plane workgroup's CAS then fails and it clears the slot
+// itself, so no value of this launch can be read by the next one
+#define PLANE_ABANDONED 0x7FF8DEAD00000002ull
 #ifdef DECIDE_TS   // diagnostic build only (tools/decide_phases.py): phase timestamps into the term scratch
 #define DTS(k) do { if (threadIdx.x == 0 && blockIdx.y == 0) reinterpret_cast<long long*>(gterms + (size_t)blockIdx.x * HistCfg<T>::kBins)[HistCfg<T>::kBins - 16 + (k)] = wall_clock64(); } while (0)
 // plane workgroups of the split decision: 4 stamps each below the main's 16
@@ -1194,7 +1198,8 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
                                                  const codec_layout* __restrict__ table,
                                                  const int32_t* __restrict__ slice_class,
                                                  codec_slice_meta* __restrict__ meta_all, EmbedArgs E,
-                                                 u64* __restrict__ plane_slots, int nsplit) {
+                                                 u64* __restrict__ plane_slots, int nsplit, uint32_t spin_max,
+                                                 int dbg_late) {
     constexpr int R = HistCfg<T>::kBins;
     // `list` doubles as the wave-parallel path's arena: terms (8m B), rank -> value (2m B),
     // one joint-order list per plane in flight (2m B each)
@@ -1407,7 +1412,21 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
             pub = (u64)__double_as_longlong(h);
             if (pub == 0ull) pub = 0x8000000000000000ull;   // +0.0 -> -0.0: same MI
         }
-        if (t == 0) __hip_atomic_store(plane_slots + 16 * (size_t)b + i, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == 0) {
+            u64* sp = plane_slots + 16 * (size_t)b + i;
+            if (b == 0 && i == dbg_late) {
+                // CODEC_DECIDE_DEBUG_LATE (tests only): this plane publishes only after the main
+                // workgroup has given up on it -- the late-publication path, made deterministic
+                for (uint32_t k = 0; k < (1u << 20); ++k) {   // bounded (~0.2 s)
+                    if (__hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+                    __builtin_amdgcn_s_sleep(8);
+                }
+            }
+            u64 expect = 0ull;
+            if (!__hip_atomic_compare_exchange_strong(sp, &expect, pub, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT) && expect == PLANE_ABANDONED)
+                __hip_atomic_store(sp, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // nobody reads it: clear
+        }
         return;
     }
     // main workgroup of a split decision: wait for every plane workgroup's value (they read
@@ -1417,18 +1436,29 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
     __shared__ u64 slot_sh[16];
     __shared__ int slot_to;
     bool collected = false;
+    bool abandoned = false;   // thread t < nsplit: slot t was given up (the late writer clears it)
     auto collect = [&]() {
         if (t == 0) slot_to = 0;
         __syncthreads();
         if (t < nsplit) {
             u64* sp = plane_slots + 16 * (size_t)b + t;
             u64 v = 0;
-            for (uint32_t k = 0; k < (1u << 24); ++k) {   // bounded: co-resident by construction
+            for (uint32_t k = 0; k < spin_max; ++k) {   // bounded: co-resident by construction
                 v = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (v) break;
                 __builtin_amdgcn_s_sleep(2);
             }
-            if (!v) { v = PLANE_NONE; slot_to = 1; }
+            if (!v) {   // give up -- unless the value lands between the last poll and the mark
+                u64 expect = 0ull;
+                if (__hip_atomic_compare_exchange_strong(sp, &expect, PLANE_ABANDONED, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    v = PLANE_NONE;
+                    slot_to = 1;
+                    abandoned = true;
+                } else {
+                    v = expect;
+                }
+            }
             slot_sh[t] = v;
         }
         __syncthreads();
@@ -1858,7 +1888,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
     // 16-bit wrap fix-up also writes bin v + 1 <= Rp - 1, or bin 1 when Rp = 1), plus the
     // slice's block key and OR word.  All reads of them precede this barrier.
     __syncthreads();
-    if (t < nsplit) plane_slots[16 * (size_t)b + t] = 0ull;
+    if (t < nsplit && !abandoned) plane_slots[16 * (size_t)b + t] = 0ull;
     {
         const int zr = Rp < 2 ? 2 : Rp;
         uint32_t* hz = ghist_all + (size_t)b * R;
@@ -2745,11 +2775,17 @@ static int plan_impl(const codec_params* P, const void* cover, void* stego, cons
     const bool need_mi = P->fixed_s <= 0 || P->all_mi;
     const int nsplit = (knob("CODEC_DECIDE_SPLIT", 1) && need_mi && (long long)P->B * (1 + nbp) <= 240) ? nbp : 0;
     u64* slots = reinterpret_cast<u64*>(ws + L.slots);
+    // bound of the main workgroup's wait for each plane slot (polls of ~0.1 us); the plane
+    // workgroups are co-resident by construction, so it only trips on a broken launch --
+    // CODEC_DECIDE_SPINS / CODEC_DECIDE_DEBUG_LATE=i+1 (plane i of slice 0 publishes only
+    // after the main workgroup gave up) exist to test that path
+    const uint32_t spin_max = (uint32_t)knob("CODEC_DECIDE_SPINS", 1 << 24);
+    const int dbg_late = (int)knob("CODEC_DECIDE_DEBUG_LATE", 0) - 1;
     ProfScope prof(st, E ? CODEC_K_DECIDE_EMBED : CODEC_K_DECIDE);
     const EmbedArgs Ev = E ? *E : EmbedArgs{nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
 #define DEC(TT, EM) hipLaunchKernelGGL((k_decide<TT, EM>), dim3(P->B, 1 + nsplit), dim3(1024), 0, st, Pv, hist, orv, terms, keys, exact, \
                                        L.exact_cap, edge_only, fast ? 1 : 0, log2_lut, (long long)lut_len, table, slice_class, meta, Ev, \
-                                       slots, nsplit)
+                                       slots, nsplit, spin_max, dbg_late)
     if (P->in_bytes == 2) { if (E) DEC(uint16_t, true); else DEC(uint16_t, false); }
     else { if (E) DEC(uint8_t, true); else DEC(uint8_t, false); }
 #undef DEC

@@ -431,7 +431,8 @@ template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void k_pee_ehist(const T* __restrict__ img, int H, int W, int maxval, int tmax,
                                                    int per_wg, uint32_t* __restrict__ hist_all,
                                                    uint32_t* __restrict__ arrivals, const int32_t* __restrict__ lengths,
-                                                   int32_t* __restrict__ caps, int32_t* __restrict__ t_out) {
+                                                   int32_t* __restrict__ caps, int32_t* __restrict__ t_out,
+                                                   int dbg_delay) {
     typedef typename Vec8<T>::type V;
     extern __shared__ uint32_t cnt[];                 // [tmax][256]
     __shared__ uint32_t bins[PEE_TMAX_MAX];
@@ -489,6 +490,14 @@ __global__ __launch_bounds__(256) void k_pee_ehist(const T* __restrict__ img, in
             add4(x, a, bb, cc, 1);
         }
     }
+    if (dbg_delay >= 0 && b == 0 && (int)blockIdx.x == dbg_delay % (int)gridDim.x) {
+        // CODEC_PEE_EHIST_DEBUG_DELAY (tests only): this workgroup flushes its bins ~1 ms after
+        // every other workgroup of the slice, i.e. it arrives last and selects T over bins
+        // flushed long before -- or, with the delay after its own flush (odd knob values),
+        // it arrives last right behind its own returning atomics
+        if (!(dbg_delay & 1))
+            for (int k = 0; k < 300; ++k) __builtin_amdgcn_s_sleep(127);
+    }
     __syncthreads();
     // bin u of the workgroup: thread t sums lanes t / tmax, + 256 / tmax ... of bin t % tmax
     const int g = 256 / tmax;
@@ -509,6 +518,8 @@ __global__ __launch_bounds__(256) void k_pee_ehist(const T* __restrict__ img, in
         asm volatile("" ::"v"(prev));   // wait for the atomic's return
     }
     __shared__ uint32_t ticket;
+    if (dbg_delay >= 0 && (dbg_delay & 1) && b == 0 && (int)blockIdx.x == dbg_delay % (int)gridDim.x)
+        for (int k = 0; k < 300; ++k) __builtin_amdgcn_s_sleep(127);
     __syncthreads();
     if (tid == 0) ticket = atomicAdd(&arrivals[b], 1u);
     __syncthreads();
@@ -2415,11 +2426,12 @@ int codec_pee_capacity(const codec_pee_params* P, const void* cover, int32_t tma
     ProfScope prof(st, CODEC_K_PEE_CAPACITY);
     {   // launched even when there is nothing to count: the last workgroup writes caps / t_out
         const long long per = knob("CODEC_PEE_EHIST_PER_WG", 4096);
+        const int dbg_delay = (int)knob("CODEC_PEE_EHIST_DEBUG_DELAY", 0) - 1;
         dim3 grid((unsigned)max(1LL, (units + per - 1) / per), (unsigned)P->B);
         const size_t lds = (size_t)tmax * 256 * 4;   // lane-private counters
         uint32_t* arrivals = hist + (size_t)P->B * PEE_TMAX_MAX;
 #define PEH(TT, VV) hipLaunchKernelGGL((k_pee_ehist<TT, VV>), grid, dim3(256), lds, st, static_cast<const TT*>(cover), P->H, \
-                                       P->W, P->maxval, (int)tmax, (int)per, hist, arrivals, lengths, caps, t_out)
+                                       P->W, P->maxval, (int)tmax, (int)per, hist, arrivals, lengths, caps, t_out, dbg_delay)
         if (P->bytes == 2) { if (vec) PEH(uint16_t, true); else PEH(uint16_t, false); }
         else { if (vec) PEH(uint8_t, true); else PEH(uint8_t, false); }
 #undef PEH

@@ -8,10 +8,10 @@ slice's location map -- is an `all_gather_into_tensor` of fixed-size records:
 
 * LSB path (`RecordExchange`): codec_slice_meta + packed maps, ~1.6 KB per slice, one
   collective; never the dense s*H*W bitmaps (335 MB for 2048 x 512^2).
-* MED-PEE path (`PeeRecordExchange`): two collectives -- the 64-byte codec_pee_meta of
-  every slice, then every slice's location-map prefix [0, end] padded to the longest one
-  in the whole job (read from the gathered metas, so every rank agrees on the width
-  without another collective).
+* MED-PEE path (`PeeRecordExchange`): one collective of records = the 64-byte
+  codec_pee_meta of every slice + its location-map prefix [0, end], padded to a job-wide
+  width that is agreed once and then carried from step to step without a host sync (the
+  device checks every gather against the width its metas needed; see the class).
 
 Uneven shards (e.g. 2049 slices over 8 ranks) are padded to ceil(N / world) rows per
 rank, the collective stays one equal-sized all-gather, and the padding rows are dropped
@@ -220,19 +220,53 @@ PEE_META_WORDS = (_lib.PEE_META_BYTES + 7) // 8
 PEE_END_FIELD = 3          # int32 index of codec_pee_meta.end
 
 
+def map_prefix(meta, lm, lmw: int, out=None):
+    """The first `lmw` location-map words of every slice with the words past its own
+    ceil((end + 1) / 64) zeroed (the embed leaves them unwritten) -- what a gathered row holds."""
+    import torch
+    ends = meta.contiguous().view(torch.int32)[:, PEE_END_FIELD].to(torch.int64)
+    words = torch.div(ends + 64, 64, rounding_mode="floor")           # ceil((end + 1) / 64)
+    cols = torch.arange(lmw, device=lm.device, dtype=torch.int64)
+    if out is None:
+        out = torch.empty((lm.shape[0], lmw), dtype=torch.int64, device=lm.device)
+    return out.copy_(lm[:, :lmw]).masked_fill_(cols[None, :] >= words[:, None], 0)
+
+
+def _map_words_needed(ends, cap: int):
+    """Device int64 scalar: map words the slices with these `end` fields need,
+    ceil((max end + 1) / 64) clamped to [1, cap] (no host read)."""
+    import torch
+    e = ends.max().to(torch.int64)
+    return torch.clamp(torch.div(e + 64, 64, rounding_mode="floor"), 1, int(cap))
+
+
 class PeeRecordExchange:
     """The MED-PEE side information of every slice to every rank (north star: "an RCCL
     all-gather of per-slice location maps").
 
-    Phase 1 gathers the fixed 64-byte codec_pee_meta records (T, L, end, maxval, status,
-    capacity ...).  Their `end` fields bound every location map (candidates 0..end), so
-    phase 2 gathers each slice's first ceil((end_max + 1) / 64) map words, end_max taken
-    over the whole job from the gathered metas -- the same number on every rank, hence one
-    equal-sized collective, with no extra agreement round.  The host reads that one
-    integer (a sync of the side stream only: decode's kernels were queued before
-    ``start`` and keep running).  Uneven shards are padded as in RecordExchange."""
+    One collective per step: every slice's record is its fixed 64-byte codec_pee_meta (T, L,
+    end, maxval, status, capacity ...) followed by the first `lm_words` words of its location
+    map.  A map only means something up to candidate `end`, so `lm_words` only has to cover
+    ceil((end_max + 1) / 64), end_max over the whole job -- but that number is on the device.
+    Reading it every step would block the host on the side stream, so the width is carried
+    over instead (no host sync in ``start``):
 
-    def __init__(self, batch: int, world: int, device, group=None, n_total: Optional[int] = None):
+    * the first gather agrees it exactly: metas first, one host read of end_max (a sync of
+      the side stream only), then the maps;
+    * every gather computes, on the device, the width its own metas needed, bumps a sticky
+      device counter (``overflows()``) when it exceeded the width used, and copies the
+      figure into pinned host memory behind an event; a later ``start`` adopts a larger
+      width as soon as that event has completed (``Event.query``, never a wait);
+    * ``join(verify=True)`` (or ``verify()`` before the next embed overwrites meta/lm) makes
+      one host read of the figure and re-gathers at the wider width if the gather was too
+      narrow, so a caller that needs the maps immediately still gets exact rows.
+
+    Words past a slice's own end are zeroed before the gather (the embed leaves them
+    unwritten), so every gathered row is exactly its map zero-extended.  Uneven shards are
+    padded as in RecordExchange."""
+
+    def __init__(self, batch: int, world: int, device, group=None, n_total: Optional[int] = None,
+                 lm_words: Optional[int] = None):
         import torch
         self.group = group
         self.world = int(world)
@@ -242,58 +276,130 @@ class PeeRecordExchange:
             raise ValueError("batch exceeds the per-rank row count of n_total")
         self.batch = int(batch)
         self.device = torch.device(device)
-        self.meta_rec = torch.zeros((self.rows, PEE_META_WORDS), dtype=torch.int64, device=device)
-        self.meta_padded = torch.empty((self.world * self.rows, PEE_META_WORDS), dtype=torch.int64, device=device)
         self.even = self.rows * self.world == self.n_total
         self.index = None if self.even else torch.tensor(valid_rows(self.n_total, self.world), device=device)
-        self._lm_flat = None
-        self._lm_out_flat = None
-        self.lm_words = 0
+        self.lm_words = int(lm_words) if lm_words else 0
+        self._rec_flat = None
+        self._out_flat = None
+        self._rec = self._out = None
+        self._cuda = self.device.type == "cuda"
+        self._need = torch.zeros((), dtype=torch.int64, device=device)
+        self._overflow = torch.zeros((), dtype=torch.int64, device=device)
+        self._need_host = torch.zeros(1, dtype=torch.int64, pin_memory=self._cuda)
+        self._need_ev = torch.cuda.Event() if self._cuda else None
+        self._pending = False
+        self._last = None
         self._side = _SideStream(device)
 
+    # -- buffers: [rows, META_WORDS + lmw] records, [world * rows, ...] gathered
     def _buffers(self, lmw: int):
         import torch
-        need = self.rows * lmw
-        if self._lm_flat is None or self._lm_flat.numel() < need:
-            self._lm_flat = torch.zeros(need, dtype=torch.int64, device=self.device)
-            self._lm_out_flat = torch.empty(self.world * need, dtype=torch.int64, device=self.device)
-        rec = self._lm_flat[:need].view(self.rows, lmw)
-        out = self._lm_out_flat[: self.world * need].view(self.world * self.rows, lmw)
-        return rec, out
+        width = PEE_META_WORDS + lmw
+        need = self.rows * width
+        if self._rec_flat is None or self._rec_flat.numel() < need:
+            self._rec_flat = torch.zeros(need, dtype=torch.int64, device=self.device)
+            self._out_flat = torch.empty(self.world * need, dtype=torch.int64, device=self.device)
+        self._rec = self._rec_flat[:need].view(self.rows, width)
+        self._out = self._out_flat[: self.world * need].view(self.world * self.rows, width)
+        return self._rec, self._out
+
+    @property
+    def meta_padded(self):
+        return self._out[:, :PEE_META_WORDS]
+
+    @property
+    def _lm_padded(self):
+        return self._out[:, PEE_META_WORDS:]
 
     def mark(self):
         self._side.mark()
 
-    def start(self, meta, lm):
-        """meta: uint8 [B, PEE_META_BYTES]; lm: int64 [B, lm_words] (PeeCodec outputs)."""
+    def _adopt_width(self, cap: int):
+        """Take a wider width from an earlier gather whose figure has landed on the host."""
+        if self._pending and (self._need_ev is None or self._need_ev.query()):
+            need = int(self._need_host[0])
+            self._pending = False
+            if need > self.lm_words:
+                self.lm_words = min(need, cap)
+
+    def _gather(self, meta, lm, lmw: int):
+        """Pack meta + the masked map prefix into the records and gather them (side stream)."""
         import torch
         B = meta.shape[0]
+        rec, out = self._buffers(lmw)
+        rec[:B, :PEE_META_WORDS].view(torch.uint8)[:, : _lib.PEE_META_BYTES].copy_(meta)
+        map_prefix(meta, lm, lmw, out=rec[:B, PEE_META_WORDS:])
+        if B < self.rows:
+            rec[B:].zero_()
+        gather_records(rec, self.group, out=out, rows=self.rows)
+        # the width this gather needed, over the whole job (every rank computes the same)
+        gends = out[:, :PEE_META_WORDS].contiguous().view(torch.int32)[:, PEE_END_FIELD]
+        need = _map_words_needed(gends, int(lm.shape[1]))
+        self._need.copy_(need)
+        self._overflow.add_((need > lmw).to(torch.int64))
+        self._need_host.copy_(need.view(1), non_blocking=self._cuda)
+        if self._need_ev is not None:
+            self._need_ev.record()
+        self._pending = True
+
+    def start(self, meta, lm):
+        """meta: uint8 [B, PEE_META_BYTES]; lm: int64 [B, lm_words] (PeeCodec outputs).
+        Queues the gather on the side stream; the host never waits on the device here except
+        on the very first call (the exact initial width)."""
+        import torch
+        cap = int(lm.shape[1])
+        self._adopt_width(cap)
+        self._last = (meta, lm)
         with self._side.enter():
-            self.meta_rec[:B].view(torch.uint8)[:, : _lib.PEE_META_BYTES].copy_(meta)
-            if B < self.rows:
-                self.meta_rec[B:].zero_()
-            gather_records(self.meta_rec, self.group, out=self.meta_padded, rows=self.rows)
-            end_max = int(self.meta_padded.view(torch.int32)[:, PEE_END_FIELD].max().item())
-            lmw = min(max(1, (end_max + 1 + 63) // 64), int(lm.shape[1]))
-            rec, out = self._buffers(lmw)
-            rec[:B].copy_(lm[:, :lmw])
-            if B < self.rows:
-                rec[B:].zero_()
-            gather_records(rec, self.group, out=out, rows=self.rows)
-            self.lm_words = lmw
-            self._lm_padded = out
+            if self.lm_words <= 0:
+                # first call: agree the width exactly (metas first, one host read)
+                self._buffers(1)
+                self._rec[: meta.shape[0], :PEE_META_WORDS].view(torch.uint8)[:, : _lib.PEE_META_BYTES].copy_(meta)
+                if meta.shape[0] < self.rows:
+                    self._rec[meta.shape[0]:].zero_()
+                mrec = self._rec[:, :PEE_META_WORDS].contiguous()
+                mout = gather_records(mrec, self.group, rows=self.rows)
+                self.lm_words = int(_map_words_needed(mout.view(torch.int32)[:, PEE_END_FIELD], cap).item())
+            self.lm_words = min(self.lm_words, cap)
+            self._gather(meta, lm, self.lm_words)
+
+    def verify(self) -> bool:
+        """One host read: was the last gather wide enough?  If not, re-gather it at the
+        needed width (meta/lm of that step must still be intact) and keep that width.
+        Returns True when the last gather had to be repeated."""
+        if self._last is None:
+            return False
+        self._side.join()
+        need = int(self._need.item())
+        if need <= self.lm_words:
+            return False
+        meta, lm = self._last
+        self.lm_words = min(need, int(lm.shape[1]))
+        with self._side.enter():
+            self._gather(meta, lm, self.lm_words)
+            self._overflow.sub_(1)   # repaired: this step's rows are now complete
+        return True
+
+    def overflows(self) -> int:
+        """Gathers (since construction) whose width was too narrow and not repaired by
+        verify(): their map rows were cut short (one host read)."""
+        self._side.join()
+        return int(self._overflow.item())
 
     def own_rows(self, rank: int):
         """(meta, lm) rows of this rank in the gathered (padded) buffers."""
         a = rank * self.rows
         return self.meta_padded[a: a + self.batch], self._lm_padded[a: a + self.batch]
 
-    def join(self):
+    def join(self, verify: bool = False):
         """(meta uint8 [n_total, PEE_META_BYTES], lm int64 [n_total, lm_words]) in global
-        slice order; a slice's full map is its row zero-extended to the codec's lm_words."""
+        slice order; a slice's full map is its row zero-extended to the codec's lm_words.
+        verify=True: exact rows guaranteed now (one host read, see verify())."""
         import torch
+        if verify:
+            self.verify()
         self._side.join()
         meta, lm = self.meta_padded, self._lm_padded
         if not self.even:
             meta, lm = meta.index_select(0, self.index), lm.index_select(0, self.index)
-        return meta.view(torch.uint8)[:, : _lib.PEE_META_BYTES], lm
+        return meta.contiguous().view(torch.uint8)[:, : _lib.PEE_META_BYTES], lm

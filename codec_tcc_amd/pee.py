@@ -9,8 +9,8 @@ oracle/pee_cpu.py (parity unpinned) and summarised in include/codec_tcc.h.
 from __future__ import annotations
 
 import ctypes as C
-from dataclasses import dataclass
-from typing import List, Optional
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
 
 import numpy as np
 
@@ -25,6 +25,7 @@ class PeeEncoded:
     meta: object       # torch.uint8 [B, sizeof(codec_pee_meta)]
     lengths: List[int]
     payload_words: int
+    config: dict = field(default_factory=dict)   # the PeeCodec's T / tmax / maxval (decode())
 
     def records(self) -> List[_lib.PeeMeta]:
         raw = self.meta.detach().cpu().contiguous().numpy().tobytes()
@@ -56,6 +57,8 @@ class PeeCodec:
         self.maxval = vmax if maxval is None else int(maxval)
         self.nc = (self.H // 2) * (self.W // 2)
         self.lm_words = max(1, (self.nc + 63) // 64)
+        self.config = dict(method="pee", T="auto" if self.auto else self.T, tmax=self.tmax, maxval=self.maxval,
+                           dtype="uint16" if nbytes == 2 else "uint8")
         P = self._params(1)
         ws = _lib.load().codec_pee_workspace_bytes(C.byref(P))
         if ws == 0:
@@ -115,7 +118,8 @@ class PeeCodec:
                                               lens_t.data_ptr(), None, meta.data_ptr(), lm.data_ptr(),
                                               self.workspace.data_ptr(), self.workspace.numel(), _stream()),
                        "codec_pee_embed")
-        enc = PeeEncoded(stego=stego, lm=lm, meta=meta, lengths=list(lengths), payload_words=int(words.shape[1]))
+        enc = PeeEncoded(stego=stego, lm=lm, meta=meta, lengths=list(lengths), payload_words=int(words.shape[1]),
+                         config=self.config)
         if check:
             _raise_lookback(enc.records())
         return enc
@@ -163,6 +167,53 @@ class PeeCodec:
             raise RuntimeError("codec_pee_extract: in-place cursor look-back timed out; the recovered "
                                "payload is invalid (the restored cover is exact)")
         return [framing.unpack_bits(host[i], enc.lengths[i]) for i in range(self.B)], cover
+
+
+_CODECS = {}
+
+
+def _codec_for(shape, dtype: str, *, T, tmax: int, maxval: Optional[int]) -> PeeCodec:
+    torch = _torch()
+    if maxval is None:
+        maxval = 65535 if "16" in dtype else 255
+    key = (tuple(shape), dtype, T, int(tmax), int(maxval), torch.cuda.current_device())
+    c = _CODECS.get(key)
+    if c is None:
+        c = PeeCodec(*shape, dtype=dtype, T=T, tmax=tmax, maxval=maxval)
+        _CODECS[key] = c
+    return c
+
+
+def encode(covers, payloads: Sequence, *, T=2, tmax: int = 16, maxval: Optional[int] = None) -> PeeEncoded:
+    """MED-PEE embed of one payload per slice (the package's `encode(..., method="pee")`).
+    covers: [B,H,W] / [H,W] uint8/uint16 torch tensor or numpy array; T: expansion threshold
+    or "auto" (smallest T <= tmax whose capacity holds each slice's payload); maxval: the
+    largest legal pixel value (e.g. 4095 for 12-bit DICOM; default the dtype's maximum).
+    Raises ValueError when a payload exceeds its slice's capacity."""
+    from .codec import _as_batch
+    _require_gpu()
+    covers = _as_batch(covers)
+    if isinstance(payloads, (str, bytes, bytearray)):
+        payloads = [payloads]
+    dt = "uint16" if _elem_bytes(covers) == 2 else "uint8"
+    codec = _codec_for(tuple(covers.shape), dt, T=T, tmax=tmax, maxval=maxval)
+    enc = codec.embed(covers, payloads)
+    bad = [i for i, r in enumerate(enc.records()) if r.status != 0]
+    if bad:
+        raise ValueError(f"payload exceeds PEE capacity in slices {bad} (T={T}, tmax={tmax})")
+    return enc
+
+
+def decode(enc: PeeEncoded, *, restore: bool = True):
+    """Exact extraction: (payload_bit_lists, cover) like the LSB decode() -- payload_bit_lists[b]
+    is a numpy 0/1 vector of slice b's embedded bits, cover the restored [B,H,W] tensor
+    (None with restore=False)."""
+    _require_gpu()
+    cfg = enc.config
+    codec = _codec_for(tuple(enc.stego.shape), cfg.get("dtype", "uint16"), T=cfg.get("T", 2),
+                       tmax=cfg.get("tmax", 16), maxval=cfg.get("maxval"))
+    bits, cover = codec.decode(enc)
+    return bits, (cover if restore else None)
 
 
 def _raise_lookback(recs):

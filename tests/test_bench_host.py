@@ -55,3 +55,28 @@ def test_pmc_traffic_lookup(tmp_path, monkeypatch):
     assert bench.pmc_traffic("k_scan_rows", 4, 8, 8, "ct12")["hbm_bytes_per_launch"] == 123
     assert bench.pmc_traffic("k_pee_embed1", 4, 8, 8, "ct12") is None      # ambiguous instantiation
     assert bench.pmc_traffic("k_scan_rows", 8, 8, 8, "ct12") is None       # other configuration
+    # template-argument selection (argument 2 = INPLACE of the PEE kernels)
+    assert bench.pmc_traffic("k_pee_embed1", 4, 8, 8, "ct12", {2: "true"})["hbm_bytes_per_launch"] == 2
+    r = bench.pmc_traffic("k_pee_embed1", 4, 8, 8, "ct12", {2: "false"})
+    assert r["hbm_bytes_per_launch"] == 1 and r["instance"] == "k_pee_embed1<unsigned short, true, false>"
+    assert bench.pmc_traffic("k_pee_embed1", 4, 8, 8, "ct12", {5: "true"}) is None
+
+
+def test_committed_pmc_summaries_resolve_every_bench_instance():
+    """The roofline objects of the headline, in-place and C3 legs find their PMC rows in the
+    committed summaries (the in-place lookup never matched)."""
+    for tag, ta in (("k_pee_embed1", {2: "false"}), ("k_pee_extract1", {2: "false"}),
+                    ("k_pee_embed_ss", {2: "true", 5: "false"}), ("k_pee_extract_ss", {2: "true"})):
+        assert bench.pmc_traffic(tag, 256, 2048, 2048, "ct12", ta) is not None, tag
+    for tag, ta in (("k_pee_embed_ss", {2: "false", 5: "true"}), ("k_pee_extract_ss", {2: "false"})):
+        assert bench.pmc_traffic(tag, 256, 512, 512, "ct12", ta) is not None, tag
+
+
+def test_gpus_world_size_mismatch_is_refused():
+    """bench.py --gpus N under a launcher that started a different number of ranks exits
+    non-zero before touching the GPU."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr

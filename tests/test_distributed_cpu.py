@@ -117,7 +117,28 @@ def _worker(rank, world, port, n_slices, q):
         nw = (37 * g + 5 + 1 + 63) // 64
         ok &= torch.equal(glm[g, :nw], torch.arange(nw, dtype=torch.int64) * 1000 + g)
     om, ol = px.own_rows(rank)
-    ok &= torch.equal(om.view(torch.uint8)[:, : _lib.PEE_META_BYTES], pmeta) and torch.equal(ol, lm[:, : px.lm_words])
+    ok &= torch.equal(om.contiguous().view(torch.uint8)[:, : _lib.PEE_META_BYTES], pmeta)
+    # words past each slice's own end were garbage (-7): the gathered rows carry zeros there
+    for i in range(B):
+        nw = (37 * (lo + i) + 5 + 1 + 63) // 64
+        ok &= torch.equal(ol[i, :nw], lm[i, :nw]) and not ol[i, nw:].any()
+    ok &= px.overflows() == 0
+    # ---- a later step whose maps are longer: the carried width is too narrow for that
+    # gather (the device counts it), verify() re-gathers it at the needed width, and the
+    # following step adopts that width without any host read
+    w0 = px.lm_words
+    pmeta2, lm2 = _pee_records(lo, hi, lm_words)
+    for i in range(B):
+        pmeta2[i].view(torch.int32)[3] = 64 * (w0 + 1) + i          # end -> w0 + 2 words
+        lm2[i, : w0 + 2] = torch.arange(w0 + 2, dtype=torch.int64) + 100 * (lo + i)
+    px.start(pmeta2, lm2)
+    ok &= px.overflows() == 1 and px.lm_words == w0
+    ok &= px.verify() is True and px.overflows() == 0 and px.lm_words == w0 + 2
+    gmeta2, glm2 = px.join()
+    for g in range(n_slices):
+        ok &= torch.equal(glm2[g, : w0 + 2], torch.arange(w0 + 2, dtype=torch.int64) + 100 * g)
+    px.start(pmeta2, lm2)
+    ok &= px.lm_words == w0 + 2 and px.overflows() == 0 and px.verify() is False
     # ---- the plain gather helper with equal shards
     rec = D.pack_records(*_lsb_records(lo, hi, 4))
     ok &= D.gather_records(rec, rows=D.shard_rows(n_slices, world)).shape[0] == world * D.shard_rows(n_slices, world)

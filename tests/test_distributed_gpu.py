@@ -96,7 +96,50 @@ def test_exchanges_on_gpu_streams_world2():
     procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=110) for _ in procs]
-    for p in procs:
-        p.join(timeout=30)
-    assert all(ok for _r, ok, _e in res), res
+    res = []
+    try:
+        res = [q.get(timeout=110) for _ in procs]
+    finally:
+        # a rank that hangs or dies without reporting must not keep holding the GPU for the
+        # tests after this one
+        for p in procs:
+            p.join(timeout=30)
+        for p in procs:
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
+    assert len(res) == world and all(ok for _r, ok, _e in res), res
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+@pytest.mark.timeout(600)
+def test_bench_launches_its_own_ranks():
+    """`python bench.py --gpus 2 --backend gloo` with no launcher: the
+    script starts two rank processes itself before touching the GPU (both on cuda:0 here),
+    and rank 0's JSON line reports the 2-rank job -- the headline MED-PEE step with its
+    record exchange, and the C4 leg (256 x 512^2 per rank, T = auto, exchange)."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    cmd = [sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--backend", "gloo", "--batch", "8",
+           "--size", "512", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0", "--c2", "0", "--no-profile",
+           "--payload-chars", "256"]   # within a 512^2 slice's T = 2 capacity
+    r = subprocess.run(cmd, env=env, cwd=repo, capture_output=True, text=True, timeout=540)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 16
+    assert out["roundtrip_ok"] is True and out["pee"]["exchange_ok"] is True, out["pee"]
+    assert out["pee"]["distributed"]["narrow_gathers"] == 0
+    assert out["lsb"]["roundtrip_ok"] is True and out["lsb"]["exchange_ok"] is True, out["lsb"]
+    assert out["c4"]["roundtrip_ok"] is True and out["c4"]["exchange_ok"] is True, out["c4"]
+    # a launcher that started a different number of ranks is refused
+    bad = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2"],
+                         env=dict(env, WORLD_SIZE="1", RANK="0"), cwd=repo, capture_output=True, text=True, timeout=120)
+    assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr

@@ -126,10 +126,12 @@ def test_headline_lsb_256x2048_with_kats():
     _lsb_batch_check(covers, msgs, sample=(0, 85, 170, 255), kats=kats)
 
 
-@pytest.mark.parametrize("ss", ["auto", "0"])
+@pytest.mark.parametrize("ss", ["auto", "1"])
 def test_headline_pee_256x2048(ss, monkeypatch):
-    """Default launch at this shape: the slice-serial single pass (one workgroup per slice);
-    "0": the look-back single pass (chunk-parallel) on the same batch."""
+    """Default dispatch at this shape (codec_pee.hip pee_use_slice_serial): out of place the
+    look-back single pass (k_pee_embed1 / k_pee_extract1, chunk-parallel), in place the
+    slice-serial pass (k_pee_embed_ss / k_pee_extract_ss).  "1" forces the slice-serial
+    kernels out of place too, so the out-of-place k_pee_embed_ss runs once at 2048^2."""
     if ss != "auto":
         monkeypatch.setenv("CODEC_PEE_SS", ss)
     _pee_batch_check(_batch(256, 2048, 2048, seed=11), sample=(0, 101, 255))

@@ -392,3 +392,34 @@ def test_restore_paths_vs_oracle(kind, h, w, bsz, chars, restore, monkeypatch):
         np.testing.assert_array_equal(stego[i], exp["stego"])
         assert framing.bits_to_str(bits[i]) == mb
     np.testing.assert_array_equal(cover.cpu().numpy(), covers)
+
+
+def test_split_decision_timeout_leaves_no_stale_slot(monkeypatch):
+    """a split decision whose main workgroup gives up on a plane slot (status 2,
+    CODEC_FLAG_DECIDE_TIMEOUT) must not leave a value behind for the next call.  With
+    CODEC_DECIDE_DEBUG_LATE=1 plane 0 of slice 0 publishes only after the main workgroup
+    abandoned its slot (and CODEC_DECIDE_SPINS=200 makes it give up early, possibly on other
+    slots too); Codec.encode raises on the status by default.  The next normal call must
+    then decide every slice exactly as before (same s, MI values, stego, maps)."""
+    from codec_tcc_amd import _lib
+    B, H, W = 2, 512, 512
+    covers = torch.from_numpy(np.stack([synth.ct12(H, W, 90 + i) for i in range(B)])).cuda()
+    msgs = [synth.payload(300, 40 + i) for i in range(B)]
+    codec = Codec(B, H, W, dtype="uint16", beta=0.4, block=16, all_mi=True)
+    ref = codec.encode(covers, msgs)
+    rr = ref.records()
+    assert all(r.status == 0 for r in rr)
+    monkeypatch.setenv("CODEC_DECIDE_SPINS", "200")
+    monkeypatch.setenv("CODEC_DECIDE_DEBUG_LATE", "1")
+    with pytest.raises(RuntimeError, match="timed out"):
+        codec.encode(covers, msgs)
+    bad = codec.encode(covers, msgs, check=False).records()
+    assert bad[0].status == 2 and (bad[0].flags & _lib.FLAG_DECIDE_TIMEOUT)
+    monkeypatch.delenv("CODEC_DECIDE_SPINS")
+    monkeypatch.delenv("CODEC_DECIDE_DEBUG_LATE")
+    for _ in range(2):
+        enc = codec.encode(covers, msgs)
+        torch.cuda.synchronize()
+        assert torch.equal(enc.meta, ref.meta)
+        assert torch.equal(enc.stego.view(torch.int16), ref.stego.view(torch.int16))
+        assert torch.equal(enc.maps, ref.maps)

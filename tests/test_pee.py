@@ -569,3 +569,73 @@ def test_gpu_matches_scheme_kats(k, ss, monkeypatch):
     words, cover = codec.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words)
     np.testing.assert_array_equal(framing.unpack_bits(words[0].cpu().numpy(), k["L"]), bits[: k["L"]])
     np.testing.assert_array_equal(cover[0].cpu().numpy(), img)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [2, "auto"])
+def test_package_encode_decode_pee(T):
+    """MED-PEE through the package's own call surface:
+    codec_tcc_amd.encode(covers, payloads, method="pee") / codec_tcc_amd.decode(enc), the
+    batched counterpart of the reference's main() (src/codec.py:847-913) and decode_bin()
+    (:795-842).  Stego, location map, per-slice T and `end` equal the oracle on every slice;
+    decode recovers every payload bit and the cover exactly."""
+    torch = pytest.importorskip("torch")
+    import codec_tcc_amd as ct
+    from codec_tcc_amd import framing
+    from codec_tcc_amd.pee import lm_bits
+    covers = np.stack([synth.ct12(256, 256, 70 + i) for i in range(2)])
+    msgs = [synth.payload(100, 900), "Mensagem de teste para esteganografia!"]   # <= T = 2 capacity
+    enc = ct.encode(torch.from_numpy(covers).cuda(), msgs, method="pee", T=T, maxval=4095)
+    assert isinstance(enc, ct.PeeEncoded)
+    recs = enc.records()
+    for i, m in enumerate(msgs):
+        bits = framing.to_bits(m)
+        Ti = P.select_T(covers[i], len(bits), 16, maxval=4095) if T == "auto" else T
+        st, side = P.pee_embed(covers[i], bits, Ti, maxval=4095)
+        assert recs[i].T == Ti and recs[i].status == 0 and recs[i].end == side["end"]
+        np.testing.assert_array_equal(enc.stego[i].cpu().numpy(), st)
+        np.testing.assert_array_equal(lm_bits(enc, i), side["lm"])
+    got, cover = ct.decode(enc)
+    assert torch.equal(cover.cpu().view(torch.int16), torch.from_numpy(covers).view(torch.int16))
+    for i, m in enumerate(msgs):
+        np.testing.assert_array_equal(got[i], framing.to_bits(m))
+    # numpy covers and a single 2-D slice go through the same surface
+    enc1 = ct.encode(covers[0], msgs[0], method="pee", T=T, maxval=4095)
+    g1, c1 = ct.decode(enc1)
+    np.testing.assert_array_equal(g1[0], framing.to_bits(msgs[0]))
+    assert torch.equal(c1[0].cpu().view(torch.int16), torch.from_numpy(covers[0]).view(torch.int16))
+    with pytest.raises(ValueError):
+        ct.encode(covers[0], msgs[0], method="jxl")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("per_wg,delay", [("4096", None), ("512", None), ("64", None), ("512", "1"), ("512", "4"),
+                                          ("64", "8"), ("64", "15"), ("100000", "2")])
+def test_gpu_capacity_pass_forced_reorder(per_wg, delay, monkeypatch):
+    """k_pee_ehist's last-arrival selection: the slice's last
+    workgroup to arrive turns the summed bins into the capacity curve and picks T, with no
+    fence -- it relies on every other workgroup's returning device-scope bin atomics having
+    completed before that workgroup's arrival atomic.  Swept over grid sizes
+    (CODEC_PEE_EHIST_PER_WG: 1 .. 64 workgroups per slice) and with one workgroup of slice 0
+    forced to arrive ~1 ms after all others (CODEC_PEE_EHIST_DEBUG_DELAY=k+1: even k delays
+    its flush, odd k its arrival right after its own flush), the curve and T of every slice
+    equal the oracle's (pee_cpu.capacity_curve / select_T)."""
+    torch = pytest.importorskip("torch")
+    from codec_tcc_amd.pee import PeeCodec
+    monkeypatch.setenv("CODEC_PEE_EHIST_PER_WG", per_wg)
+    if delay is not None:
+        monkeypatch.setenv("CODEC_PEE_EHIST_DEBUG_DELAY", delay)
+    monkeypatch.setenv("CODEC_PEE_AUTO_FUSED", "0")          # the standalone capacity pass
+    tmax, bsz, h, w = 12, 4, 256, 256
+    covers = np.stack([synth.ct12(h, w, 330 + i) for i in range(bsz)])
+    curves = np.stack([P.capacity_curve(c, tmax) for c in covers])
+    codec = PeeCodec(bsz, h, w, dtype="uint16", T="auto", tmax=tmax)
+    dev = torch.from_numpy(covers).cuda()
+    for rep in range(3):                                     # bins and counters left clean
+        np.testing.assert_array_equal(codec.capacity(dev).cpu().numpy(), curves)
+    lens = [int(curves[i][(2 * i + 3) % tmax]) for i in range(bsz)]
+    enc = codec.embed(dev, [_bits(n, 70 + i) for i, n in enumerate(lens)])
+    t_dev = codec.t_slices.cpu().numpy()
+    for i in range(bsz):
+        T = P.select_T(covers[i], lens[i], tmax)
+        assert enc.records()[i].T == T and t_dev[i] == T, (i, T)

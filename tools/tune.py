@@ -54,7 +54,7 @@ def main():
     lib = _lib.load()
 
     def step():
-        codec.encode(covers, pl, stego=stego, maps=maps, meta=meta)
+        codec.encode(covers, pl, stego=stego, maps=maps, meta=meta, check=False)
         codec.decode(stego, maps, meta, payload_words=pl.payload_words, map_words=pl.map_words, cover=cov2,
                      payload=pay)
 
@@ -62,7 +62,7 @@ def main():
         work = covers.clone()
 
         def step():   # noqa: F811
-            codec.encode(work, pl, stego=work, maps=maps, meta=meta)
+            codec.encode(work, pl, stego=work, maps=maps, meta=meta, check=False)
             codec.decode(work, maps, meta, payload_words=pl.payload_words, map_words=pl.map_words, cover=work,
                          payload=pay)
         cov2 = work
