@@ -392,7 +392,8 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
     res["kernels_ms"] = {k: round(v, 4) for k, v in kern.items()}
     # the launch path the dispatcher chose (codec_pee.hip pee_use_slice_serial): the
     # slice-serial kernels for chip-filling batches in place / small slices, else look-back
-    emb = next((k for k in ("k_pee_embed_ss_auto", "k_pee_embed_ss", "k_pee_embed1", "k_pee_scan") if k in kern), None)
+    emb = next((k for k in ("k_pee_embed_res", "k_pee_embed_ss_auto", "k_pee_embed_ss", "k_pee_embed1", "k_pee_scan")
+                if k in kern), None)
     ext = next((k for k in ("k_pee_extract_ss", "k_pee_extract1") if k in kern), None)
     res["embed_kernel"], res["extract_kernel"] = emb, ext
     # PMC instantiation of each tag: template argument 2 is INPLACE for every PEE kernel; the
@@ -420,7 +421,7 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
         res["value_basis"] = ("pixels read up to each slice's `end` (items of 8 px x 2 rows); nominal_mpx_s "
                               "counts every pixel of the batch")
         res["prefix_pixels_per_step"] = int(prefix_px)
-        if emb in ("k_pee_embed_ss_auto", "k_pee_embed_ss", "k_pee_embed1") and kern[emb] > 0:
+        if emb in ("k_pee_embed_res", "k_pee_embed_ss_auto", "k_pee_embed_ss", "k_pee_embed1") and kern[emb] > 0:
             res["roofline"] = _roof(emb, by, kern[emb], traffic(emb))
         if ext and kern[ext] > 0:
             # extract reads the same items plus their location-map words, writes the rows back
@@ -430,8 +431,8 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
         res["roofline"] = _roof(emb, B * H * W * 4, kern[emb], traffic(emb))   # read cover + write stego
     if ext:
         res["extract_roofline"] = _roof(ext, B * H * W * 4, kern[ext], traffic(ext))
-    t_emb = sum(kern.get(k, 0.0) for k in ("k_pee_embed_ss_auto", "k_pee_embed_ss", "k_pee_embed1", "k_pee_scan", "k_pee_locate",
-                                           "k_pee_embed")) / 1e3
+    t_emb = sum(kern.get(k, 0.0) for k in ("k_pee_embed_res", "k_pee_embed_ss_auto", "k_pee_embed_ss", "k_pee_embed1",
+                                           "k_pee_scan", "k_pee_locate", "k_pee_embed")) / 1e3
     if t_emb > 0:
         # north-star figure: cover bytes read / t_embed / peak (an out-of-place embed also
         # writes as many bytes, so this cannot exceed ~0.5 of the shared HBM bandwidth)

@@ -2106,6 +2106,259 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
     }
 }
 
+// ---- resident fused auto embed (out of place, uint16, small slices: C3 / C4 at 512^2) ----
+// k_pee_embed_ss<..., AUTO> streams a slice twice: a capacity pass (histogram of folded
+// errors -> T), then the embed at T re-reads it (PMC: 1.43x the algorithmic bytes at C3).
+// Here the slice is read ONCE and kept on the CU in between: a 512-thread workgroup (two
+// waves per SIMD, up to 256 VGPRs per lane) keeps, per item, the odd row's 16-B vector (the
+// candidates x and their W neighbours a) and the 4 prediction errors clamped to 8 bits
+// (exact wherever they are used: expansion needs |e| < T <= 16, shifting only the sign) in
+// registers -- 20 B per item, 5 VGPRs, NI items per lane.  The even rows hold no candidate,
+// so the read phase writes them to the stego at once (their writes overlap the reads);
+// after T is chosen, the embed phase rewrites only the odd rows, from registers: no load.
+// HBM traffic = read cover + write stego, the algorithmic bytes.
+#define RES_THREADS 512
+#define RES_WAVES (RES_THREADS / 64)
+#define RES_PAD_WORDS (24 * 1024)   // 96 KB static pad: one workgroup per CU
+#define RES_CNT_BASE(tmax) (RES_PAD_WORDS - (tmax) * RES_THREADS)
+
+// exclusive scan of n (0..7) over the RES_WAVES waves (ss_scan_small for 8 waves)
+__device__ __forceinline__ void res_scan_small(uint32_t n, uint32_t (*wtot)[RES_WAVES], int par, uint32_t* excl,
+                                               uint32_t* tot) {
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    uint32_t wt;
+    const uint32_t ex = wave_excl_small(n, &wt);
+    if (lane == 0) wtot[par][wv] = wt;
+    lds_barrier();
+    int x = (lane & 15) < RES_WAVES ? (int)wtot[par][lane & (RES_WAVES - 1)] : 0;
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);   // row_shr:4
+    const uint32_t t = (uint32_t)__builtin_amdgcn_readlane(x, RES_WAVES - 1);
+    const uint32_t wb = wv ? (uint32_t)__builtin_amdgcn_readlane(x, wv - 1) : 0u;
+    *excl = wb + ex;
+    *tot = t;
+}
+
+template <int NI, bool NT>
+__global__ __launch_bounds__(RES_THREADS) void k_pee_embed_res(const uint16_t* __restrict__ cover,
+                                                               uint16_t* __restrict__ stego, int H, int W, int maxval,
+                                                               const int32_t* __restrict__ lengths,
+                                                               const u64* __restrict__ payload_all, int pw,
+                                                               codec_pee_meta* __restrict__ meta_all,
+                                                               u64* __restrict__ lm_all, int lmw, char* __restrict__ sink,
+                                                               int tmax, int32_t* __restrict__ t_out) {
+    typedef uint4 V;
+    __shared__ uint32_t pad[RES_PAD_WORDS];
+    __shared__ uint32_t wtot[2][RES_WAVES];
+    __shared__ uint32_t red[RES_WAVES];
+    __shared__ uint32_t s_bins[SS_AUTO_TMAX];
+    __shared__ int s_end, s_T;
+    __shared__ uint32_t s_cap;
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int CR = W / 8;
+    const uint32_t items = (uint32_t)(H / 2) * (uint32_t)CR;
+    const int nc = (H / 2) * (W / 2);
+    const int ntiles = (nc + PEE_TILE - 1) / PEE_TILE;
+    const uint32_t L = (uint32_t)max(0, lengths[b]);
+    const size_t npx = (size_t)H * W;
+    const uint16_t* src = cover + b * npx;
+    uint16_t* dst = stego + b * npx;
+    u64* lm = lm_all + (size_t)b * lmw;
+    V* sink_v = reinterpret_cast<V*>(sink + SS_SINK_SLOT(b, tid));
+    uint32_t* sink_w = reinterpret_cast<uint32_t*>(sink + SS_SINK_SLOT(b, tid) + 32);
+    uint32_t* cnt = pad + RES_CNT_BASE(tmax);     // lane-private capacity counters [tmax][512]
+    const u64* payload = payload_all + (size_t)b * pw;
+    u64* pay = reinterpret_cast<u64*>(pad);       // the slice's payload words
+    for (int u = 0; u < tmax; ++u) cnt[u * RES_THREADS + tid] = 0u;
+    if (tid == 0) s_end = -1;
+    {   // the payload into LDS now (its loads overlap the read phase)
+        const int nw = min(pw, (int)((L + 63u) >> 6));
+        for (int w = tid; w < nw; w += RES_THREADS) pay[w] = payload[w];
+    }
+    const uint32_t dq = RES_THREADS / (uint32_t)CR, dr = RES_THREADS % (uint32_t)CR;
+    const uint32_t ostep = 2u * (uint32_t)W * dq + 8u * dr, owrap = 2u * (uint32_t)W - 8u * (uint32_t)CR;
+    lds_barrier();   // counters zeroed before any lane adds
+
+    // ---- read phase: every item once; even row -> stego now, odd row + errors kept
+    V r1[NI];
+    uint32_t re[NI];
+    {
+        constexpr int G = 4;   // items per thread whose loads are in flight ahead of use
+        static_assert(NI % G == 0, "NI must be a multiple of G");
+        V v0[2][G];
+        uint32_t oo[2][G];
+        SsCursor cur;
+        cur.init((uint32_t)tid, (uint32_t)CR, (uint32_t)W);
+        auto issue = [&](int g, int s) {
+#pragma unroll
+            for (int i = 0; i < G; ++i) {
+                const int k = g * G + i;
+                const bool in = (uint32_t)(k * RES_THREADS + tid) < items;
+                const uint32_t o = in ? cur.o : 0u;
+                oo[s][i] = in ? cur.o : 0xFFFFFFFFu;
+                v0[s][i] = ldv<NT>(reinterpret_cast<const V*>(src + o));
+                r1[k] = ldv<NT>(reinterpret_cast<const V*>(src + o + W));
+                cur.step(dr, (uint32_t)CR, ostep, owrap);
+            }
+        };
+        issue(0, 0);
+#pragma unroll
+        for (int g = 0; g < NI / G; ++g) {
+            const int s = g & 1;
+            // the next group's loads go out here and no earlier: left free, hipcc hoisted every
+            // load of the slice to the top (2 x NI vectors live at once: spills at NI = 16)
+            asm volatile("" ::: "memory");
+            if (g + 1 < NI / G) issue(g + 1, s ^ 1);
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int i = 0; i < G; ++i) {
+                const int k = g * G + i;
+                V& a0 = v0[s][i];
+                V& a1 = r1[k];
+                // one item at a time: left free, hipcc interleaved the G items' unpacked pixels
+                // and masks (~25 VGPRs each) for ILP and spilled the kept rows at NI = 16
+                asm volatile("" : "+v"(a0.x), "+v"(a0.y), "+v"(a0.z), "+v"(a0.w), "+v"(a1.x), "+v"(a1.y), "+v"(a1.z),
+                             "+v"(a1.w));
+                const bool in = oo[s][i] != 0xFFFFFFFFu;
+                int x[4], a[4], bb[4], cc[4];
+                uint32_t ep = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    x[q] = (int)get_px(a1, 2 * q + 1); a[q] = (int)get_px(a1, 2 * q);
+                    bb[q] = (int)get_px(a0, 2 * q + 1); cc[q] = (int)get_px(a0, 2 * q);
+                    const int e = x[q] - med3(a[q], bb[q], cc[q]);
+                    ep |= ((uint32_t)min(127, max(-128, e)) & 0xFFu) << (8 * q);
+                }
+                // computed here, in the read phase: left free, hipcc sank it into the embed phase
+                // and kept the even row's pixels alive for it (spills at NI = 16)
+                asm volatile("" : "+v"(ep));
+                re[k] = ep;
+                ehist_add4<RES_THREADS>(cnt, tid, x, a, bb, cc, in ? 4 : 0, tmax, maxval);
+                stv<NT>(in ? reinterpret_cast<V*>(dst + oo[s][i]) : sink_v, a0);
+            }
+        }
+    }
+    lds_barrier();
+    // ---- T: the smallest T <= tmax whose capacity holds L (pee_select_slice's rule)
+    for (int u = wv; u < tmax; u += RES_WAVES) {
+        uint32_t s = 0;
+#pragma unroll
+        for (int j = 0; j < RES_THREADS / 64; ++j) s += cnt[u * RES_THREADS + j * 64 + lane];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+        if (lane == 0) s_bins[u] = s;
+    }
+    lds_barrier();
+    if (tid == 0) {
+        long long run = 0, cap = 0;
+        int tsel = 0;
+        for (int t = 1; t <= tmax; ++t) {
+            run += (long long)s_bins[t - 1];
+            if (!tsel && run >= (long long)L) { tsel = t; cap = run; }
+        }
+        s_T = tsel ? tsel : tmax;
+        s_cap = (uint32_t)(tsel ? cap : run);   // the exact capacity at T over the whole slice
+        if (t_out) t_out[b] = s_T;
+    }
+    lds_barrier();
+    const int Tthr = s_T;
+
+    // ---- embed phase: the odd rows from registers, in item order (no loads)
+    uint32_t running = 0, unsafe_n = 0;
+    int par = 0;
+    bool live = L > 0;
+    SsCursor cur;
+    cur.init((uint32_t)tid, (uint32_t)CR, (uint32_t)W);
+    const uint32_t* pay32 = reinterpret_cast<const uint32_t*>(pay);
+    const uint32_t pmax = (uint32_t)max(2 * pw - 2, 0);
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const uint32_t it = (uint32_t)k * RES_THREADS + tid;
+        const bool ok = it < items;
+        V& v1 = r1[k];
+        uint32_t ep = re[k];
+        // this chunk's values enter here: nothing derived from them (unpacked pixels, errors,
+        // the store offset) is computed ahead for all chunks at once
+        asm volatile("" : "+v"(v1.x), "+v"(v1.y), "+v"(v1.z), "+v"(v1.w), "+v"(ep), "+v"(cur.o), "+v"(cur.cc));
+        const uint32_t o1 = cur.o + (uint32_t)W;
+        cur.step(dr, (uint32_t)CR, ostep, owrap);
+        uint32_t wm = 0;
+        if (live) {   // uniform; no vector memory instruction inside
+            uint32_t esm = 0, safem = 0, rightm = 0, expm = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int x = (int)get_px(v1, 2 * q + 1);
+                const int e = (int)(int8_t)(uint8_t)(ep >> (8 * q));
+                const bool expand = (unsigned)(e + Tthr) < (unsigned)(2 * Tthr);
+                const bool right = e >= Tthr;
+                const bool ok_e = (unsigned)(x + e) < (unsigned)maxval, ok_r = x <= maxval - Tthr, ok_l = x >= Tthr;
+                const bool safe = (expand & ok_e) | (!expand & right & ok_r) | (!expand & !right & ok_l);
+                safem |= safe ? 1u << q : 0u;
+                rightm |= right ? 1u << q : 0u;
+                expm |= expand ? 1u << q : 0u;
+                esm |= (expand & safe) ? 1u << q : 0u;
+            }
+            if (!ok) esm = 0u;
+            const uint32_t n = (uint32_t)__popc(esm);
+            uint32_t ex, tot;
+            res_scan_small(n, wtot, par, &ex, &tot);
+            par ^= 1;
+            const uint32_t rs = running + ex;
+            const uint32_t m = (ok & (L > rs)) ? min(L - rs, 4u) : 0u;
+            const uint32_t w = min(rs >> 5, pmax);
+            const uint32_t field = __builtin_amdgcn_alignbit(pay32[w + 1], pay32[w], rs & 31u);
+            uint32_t procm = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {   // branch-free
+                const uint32_t bit = 1u << q;
+                const uint32_t pre = (uint32_t)__popc(esm & (bit - 1u));
+                const bool proc = pre < m;
+                procm |= proc ? bit : 0u;
+                const int x = (int)get_px(v1, 2 * q + 1);
+                const int e = (int)(int8_t)(uint8_t)(ep >> (8 * q));
+                const int nv_e = x + e + (int)((field >> pre) & 1u);   // p + 2e + bit
+                const int nv_s = (rightm & bit) ? x + Tthr : x - Tthr;
+                const int nv = (proc & ((safem & bit) != 0u)) ? ((expm & bit) ? nv_e : nv_s) : x;
+                set_px(v1, 2 * q + 1, (uint32_t)nv);
+            }
+            if (m != 0 && L - rs <= n) s_end = (int)(4 * it) + 31 - __clz(procm & esm);
+            const uint32_t nib = procm & ~safem;
+            unsafe_n += (uint32_t)__popc(nib);
+            wm = nib << (4 * (lane & 7));
+            wm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+            wm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+            wm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0x141, 0xF, 0xF, false);   // row_half_mirror
+            running += tot;
+            if (running >= L) live = false;
+        }
+        // stores, unconditional: the map word halves (zeros past `end`), the odd row
+        const uint32_t wix = (4 * it) >> 6;
+        *(ok && (lane & 7) == 0 && (int)wix < lmw ? reinterpret_cast<uint32_t*>(lm + wix) + ((lane >> 3) & 1) : sink_w) = wm;
+        stv<NT>(ok ? reinterpret_cast<V*>(dst + o1) : sink_v + 1, v1);
+    }
+    // lm_count: one block reduction
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) unsafe_n += __shfl_xor(unsafe_n, o, 64);
+    if (lane == 0) red[wv] = unsafe_n;
+    lds_barrier();
+    if (tid == 0) {
+        uint32_t un = 0;
+        for (int w = 0; w < RES_WAVES; ++w) un += red[w];
+        codec_pee_meta* M = meta_all + b;
+        M->T = Tthr; M->maxval = maxval; M->L = (int)L; M->nc = nc; M->ntiles = ntiles; M->h = H; M->w = W;
+        M->lm_count = (int)un;
+        M->capacity = (int)s_cap;   // exact: the read phase counted the whole slice
+        M->flags = 0;
+        M->reserved[0] = M->reserved[1] = M->reserved[2] = 0;
+        if (L == 0) { M->end = -1; M->tile_end = -1; M->status = 0; }
+        else if (running < L) { M->end = nc - 1; M->tile_end = ntiles - 1; M->status = 1; }   // truncated
+        else { M->end = s_end; M->tile_end = s_end / PEE_TILE; M->status = 0; }
+    }
+}
+
 template <typename T, bool NT, bool INPLACE, int D>
 __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restrict__ stego, T* cover, int H, int W,
                                                                const codec_pee_meta* __restrict__ meta_all,
@@ -2658,6 +2911,23 @@ int codec_pee_embed_auto(const codec_pee_params* P, const void* cover, void* ste
         return codec_pee_embed_ts(P, cover, stego, payload, lengths, t_out, meta, lm, workspace, workspace_bytes, stream);
     }
     const bool nt = knob("CODEC_NT", 1) != 0;
+    // resident variant (out of place, slices of <= 512 x 32 items, e.g. C3 / C4's 512^2): the
+    // cover is read once and kept on the CU between the capacity and the embed phase
+    const long long nres = (items + RES_THREADS - 1) / RES_THREADS;
+    if (!inplace && knob("CODEC_PEE_RES", 1) != 0 && nres <= 32 && 2LL * P->payload_words <= RES_CNT_BASE(tmax)) {
+        ProfScope prof(st, CODEC_K_PEE_EMBED_RES);
+#define PRES(NI, NTV) hipLaunchKernelGGL((k_pee_embed_res<NI, NTV>), dim3((unsigned)P->B), dim3(RES_THREADS), 0, st, \
+            static_cast<const uint16_t*>(cover), static_cast<uint16_t*>(stego), P->H, P->W, P->maxval, lengths, \
+            reinterpret_cast<const u64*>(payload), P->payload_words, meta, reinterpret_cast<u64*>(lm), P->lm_words, \
+            static_cast<char*>(workspace) + L.sink, (int)tmax, t_out)
+        if (nres <= 8) { if (nt) PRES(8, true); else PRES(8, false); }
+        else if (nres <= 16) { if (nt) PRES(16, true); else PRES(16, false); }
+        else { if (nt) PRES(32, true); else PRES(32, false); }
+#undef PRES
+        LAUNCH_CHECK("k_pee_embed_res");
+        if (P->H & 1) HIP_TRY(pee_copy_last_rows(P, cover, stego, st));
+        return 0;
+    }
     ProfScope prof(st, CODEC_K_PEE_EMBED_SS_AUTO);
 #define PEA(NTV, IP, DD) hipLaunchKernelGGL((k_pee_embed_ss<uint16_t, NTV, IP, DD, true, true>), dim3((unsigned)P->B), \
             dim3(SS_THREADS), 0, st, static_cast<const uint16_t*>(cover), static_cast<uint16_t*>(stego), P->H, P->W, \

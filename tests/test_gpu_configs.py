@@ -96,14 +96,17 @@ def test_c3_lsb_256x512():
     _lsb_batch_check(covers, msgs, sample=range(0, B, 16))
 
 
-@pytest.mark.parametrize("ss", ["auto", "0", "unfused"])
+@pytest.mark.parametrize("ss", ["auto", "res0", "0", "unfused"])
 def test_c3_pee_256x512(ss, monkeypatch):
     """1 KB per 512^2 ct12 slice needs T ~ 4-5 (T = 2 holds ~4.4 kbit): capacity control.
-    "auto": the default launch, capacity fused into the slice-serial embed
-    (codec_pee_embed_auto); "unfused": capacity pass + slice-serial embed as two launches;
+    "auto": the default launch, the resident embed (k_pee_embed_res: the slice read once and
+    kept on the CU while T is chosen); "res0": capacity fused into the two-phase slice-serial
+    embed (CODEC_PEE_RES=0); "unfused": capacity pass + slice-serial embed as two launches;
     "0": capacity pass + look-back embed."""
     if ss == "unfused":
         monkeypatch.setenv("CODEC_PEE_AUTO_FUSED", "0")
+    elif ss == "res0":
+        monkeypatch.setenv("CODEC_PEE_RES", "0")
     elif ss != "auto":
         monkeypatch.setenv("CODEC_PEE_SS", ss)
     _pee_batch_check(_batch(256, 512, 512, seed=2000), sample=range(3, 256, 16), T="auto")

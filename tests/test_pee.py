@@ -430,21 +430,31 @@ def test_gpu_embed_auto_fused_edges(h, w, maxval, tmax, inplace, monkeypatch):
             int(curves[4][-1]) + 37, 5]
     payloads = [_bits(n, 700 + i) for i, n in enumerate(lens)]
     runs = {}
-    for fused in ("1", "0"):
+    # fused launch: the resident kernel out of place (k_pee_embed_res, the default) and the
+    # two-phase slice-serial one (CODEC_PEE_RES=0); "0": capacity pass + embed, two launches
+    for name, fused, res in (("res", "1", "1"), ("ss", "1", "0"), ("unfused", "0", "1")):
         monkeypatch.setenv("CODEC_PEE_AUTO_FUSED", fused)
+        monkeypatch.setenv("CODEC_PEE_RES", res)
         codec = PeeCodec(bsz, h, w, dtype="uint16", T="auto", tmax=tmax, maxval=maxval)
         dev = torch.from_numpy(covers.copy()).cuda()
         enc = codec.embed(dev, payloads, stego=dev if inplace else None)
-        runs[fused] = (codec, enc, enc.records(), enc.stego.cpu().numpy(), codec.t_slices.cpu().numpy())
-    codec, enc, recs, stego, t_dev = runs["1"]
-    _, enc0, recs0, stego0, t_dev0 = runs["0"]
-    np.testing.assert_array_equal(stego, stego0)
-    np.testing.assert_array_equal(t_dev, t_dev0)
+        runs[name] = (codec, enc, enc.records(), enc.stego.cpu().numpy(), codec.t_slices.cpu().numpy())
+    codec, enc, recs, stego, t_dev = runs["res"]
+    for other in ("ss", "unfused"):
+        _, enc0, recs0, stego0, t_dev0 = runs[other]
+        np.testing.assert_array_equal(stego, stego0)
+        np.testing.assert_array_equal(t_dev, t_dev0)
+        for i in range(bsz):
+            assert (recs[i].status, recs[i].end, recs[i].T) == (recs0[i].status, recs0[i].end, recs0[i].T), (other, i)
+            assert recs[i].lm_count == recs0[i].lm_count, (other, i)
+            np.testing.assert_array_equal(lm_bits(enc, i), lm_bits(enc0, i))
     for i in range(bsz):
         T = P.select_T(covers[i], lens[i], tmax, maxval)
         assert recs[i].T == T == t_dev[i], i
         st, side = P.pee_embed(covers[i], payloads[i], T, maxval=maxval, truncate=True)
-        assert (recs[i].status, recs[i].end) == (side["status"], side["end"]) == (recs0[i].status, recs0[i].end), i
+        assert (recs[i].status, recs[i].end) == (side["status"], side["end"]), i
+        if not (recs[i].flags & 1):   # the resident kernel counts the whole slice: exact capacity
+            assert recs[i].capacity == side["capacity"], i
         np.testing.assert_array_equal(stego[i], st)
         np.testing.assert_array_equal(lm_bits(enc, i), side["lm"])
     words, cover = codec.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words,
