@@ -88,6 +88,7 @@ _SIGS = {
     "codec_pee_workspace_bytes": (C.c_size_t, [C.POINTER(PeeParams)]),
     "codec_pee_extract_flag_offset": (C.c_size_t, [C.POINTER(PeeParams)]),
     "codec_pee_diag_offset": (C.c_size_t, [C.POINTER(PeeParams)]),
+    "codec_debug_res_trace": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     "codec_pee_embed": (C.c_int, [C.POINTER(PeeParams), _VP, _VP, _VP, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),
     "codec_pee_extract": (C.c_int, [C.POINTER(PeeParams), _VP, _VP, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),
     "codec_pee_embed_ts": (C.c_int, [C.POINTER(PeeParams), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),

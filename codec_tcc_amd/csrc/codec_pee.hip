@@ -2122,37 +2122,78 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
 #define RES_PAD_WORDS (24 * 1024)   // 96 KB static pad: one workgroup per CU
 #define RES_CNT_BASE(tmax) (RES_PAD_WORDS - (tmax) * RES_THREADS)
 
-// exclusive scan of n (0..7) over the RES_WAVES waves (ss_scan_small for 8 waves)
-__device__ __forceinline__ void res_scan_small(uint32_t n, uint32_t (*wtot)[RES_WAVES], int par, uint32_t* excl,
-                                               uint32_t* tot) {
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    uint32_t wt;
-    const uint32_t ex = wave_excl_small(n, &wt);
-    if (lane == 0) wtot[par][wv] = wt;
-    lds_barrier();
-    int x = (lane & 15) < RES_WAVES ? (int)wtot[par][lane & (RES_WAVES - 1)] : 0;
-    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);   // row_shr:1
-    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);   // row_shr:2
-    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);   // row_shr:4
-    const uint32_t t = (uint32_t)__builtin_amdgcn_readlane(x, RES_WAVES - 1);
-    const uint32_t wb = wv ? (uint32_t)__builtin_amdgcn_readlane(x, wv - 1) : 0u;
-    *excl = wb + ex;
-    *tot = t;
+#ifndef RES_G
+#define RES_G 4   // items per thread in flight ahead of the one processed (read phase)
+#endif
+// inclusive scan over the wave: 16-lane rows by row_shr, then rows by row_bcast:15 / :31
+__device__ __forceinline__ uint32_t wave_incl_dpp(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+// The resident embed's kept error byte per candidate: bits 0-5 the error clamped to
+// [-32, 30] (6-bit two's complement; exact wherever used: expansion needs |e| < T <= 16 and a
+// shift only the side of +-T, with room for the payload bit: e + 1 stays in 6 bits), bit 6
+// "near" (a shift of up to tmax towards e's side could leave [0, maxval]), bit 7 = the
+// expansion stays in [0, maxval - 1] (both independent of T).  The embed phase works on the
+// four bytes of an item at once (SWAR) with masks in the bytes' bit 7.
+__device__ __forceinline__ uint32_t res_opaque(uint32_t x) {   // keeps shift/add forms: left
+    asm("" : "+v"(x));                                         // free, hipcc folded them into
+    return x;                                                  // quarter-rate multiplies
+}
+// expandable: folded error u = e >= 0 ? e : -e - 1 (XOR of the low 5 bits with the sign) < T
+// (bit 7 of (u | 0x80) - T: no borrow between bytes, u <= 31, T <= 16)
+__device__ __forceinline__ uint32_t res_ex_bytes(uint32_t ep, int T) {
+    const uint32_t s5 = ep & 0x20202020u;
+    const uint32_t m = res_opaque(s5) - (s5 >> 5);                  // sign ? 0x1F : 0 per byte
+    const uint32_t u = ((ep ^ m) & 0x1F1F1F1Fu) | 0x80808080u;
+    return ~(u - (uint32_t)T * 0x01010101u) & 0x80808080u;
+}
+// bytes' bit 7 -> byte q = number of set bits in bytes below q (0..3)
+__device__ __forceinline__ uint32_t res_prefix(uint32_t b7) {
+    const uint32_t e1 = b7 >> 7;
+    const uint32_t i1 = res_opaque(e1 << 8) + e1;
+    const uint32_t incl = res_opaque(i1 << 16) + i1;
+    return incl << 8;
+}
+__device__ __forceinline__ uint32_t res_nibble(uint32_t b7) {           // bytes' bit 7 -> 4 bits
+    return ((b7 >> 7) & 1u) | ((b7 >> 14) & 2u) | ((b7 >> 21) & 4u) | ((b7 >> 28) & 8u);
+}
+__device__ __forceinline__ int res_med3(int x, int lo, int hi) {
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "v"(hi));
+    return r;
 }
 
-template <int NI, bool NT>
-__global__ __launch_bounds__(RES_THREADS) void k_pee_embed_res(const uint16_t* __restrict__ cover,
+// phase stamps (CODEC_PEE_RES_TRACE=1, diagnostics only): per workgroup wall_clock64() at
+// entry, end of the read phase, T chosen, end of the embed phase (codec_debug_res_trace)
+#define RES_TRACE_WG 1024
+__device__ unsigned long long g_res_trace[RES_TRACE_WG * 5];
+#define RES_STAMP(i)                                                                          \
+    do {                                                                                      \
+        if (trace && tid == 0 && b < RES_TRACE_WG) g_res_trace[b * 5 + (i)] = wall_clock64(); \
+    } while (0)
+
+template <int NI, bool NT, bool NTS, int NTH>
+__global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restrict__ cover,
                                                                uint16_t* __restrict__ stego, int H, int W, int maxval,
                                                                const int32_t* __restrict__ lengths,
                                                                const u64* __restrict__ payload_all, int pw,
                                                                codec_pee_meta* __restrict__ meta_all,
                                                                u64* __restrict__ lm_all, int lmw, char* __restrict__ sink,
-                                                               int tmax, int32_t* __restrict__ t_out) {
+                                                               int tmax, int32_t* __restrict__ t_out, int trace) {
     typedef uint4 V;
+    constexpr int NWV = NTH / 64;
+    static_assert(NWV <= 16, "wave totals are scanned along one DPP row");
     __shared__ uint32_t pad[RES_PAD_WORDS];
-    __shared__ uint32_t wtot[2][RES_WAVES];
-    __shared__ uint32_t red[RES_WAVES];
+    __shared__ uint32_t s_wt[NI / 2][NWV];   // embed phase: wave totals of the packed counters
+    __shared__ uint32_t s_wb[NI / 2][NWV];    // embed phase: wave bases of the packed counters
+    __shared__ uint32_t s_cb[NI];                   // embed phase: rank of each chunk's first candidate
+    __shared__ uint32_t red[NWV];
     __shared__ uint32_t s_bins[SS_AUTO_TMAX];
     __shared__ int s_end, s_T;
     __shared__ uint32_t s_cap;
@@ -2169,16 +2210,17 @@ __global__ __launch_bounds__(RES_THREADS) void k_pee_embed_res(const uint16_t* _
     u64* lm = lm_all + (size_t)b * lmw;
     V* sink_v = reinterpret_cast<V*>(sink + SS_SINK_SLOT(b, tid));
     uint32_t* sink_w = reinterpret_cast<uint32_t*>(sink + SS_SINK_SLOT(b, tid) + 32);
-    uint32_t* cnt = pad + RES_CNT_BASE(tmax);     // lane-private capacity counters [tmax][512]
+    RES_STAMP(0);
+    uint32_t* cnt = pad + (RES_PAD_WORDS - tmax * NTH);     // lane-private capacity counters [tmax][512]
     const u64* payload = payload_all + (size_t)b * pw;
     u64* pay = reinterpret_cast<u64*>(pad);       // the slice's payload words
-    for (int u = 0; u < tmax; ++u) cnt[u * RES_THREADS + tid] = 0u;
+    for (int u = 0; u < tmax; ++u) cnt[u * NTH + tid] = 0u;
     if (tid == 0) s_end = -1;
     {   // the payload into LDS now (its loads overlap the read phase)
         const int nw = min(pw, (int)((L + 63u) >> 6));
-        for (int w = tid; w < nw; w += RES_THREADS) pay[w] = payload[w];
+        for (int w = tid; w < nw; w += NTH) pay[w] = payload[w];
     }
-    const uint32_t dq = RES_THREADS / (uint32_t)CR, dr = RES_THREADS % (uint32_t)CR;
+    const uint32_t dq = NTH / (uint32_t)CR, dr = NTH % (uint32_t)CR;
     const uint32_t ostep = 2u * (uint32_t)W * dq + 8u * dr, owrap = 2u * (uint32_t)W - 8u * (uint32_t)CR;
     lds_barrier();   // counters zeroed before any lane adds
 
@@ -2186,67 +2228,66 @@ __global__ __launch_bounds__(RES_THREADS) void k_pee_embed_res(const uint16_t* _
     V r1[NI];
     uint32_t re[NI];
     {
-        constexpr int G = 4;   // items per thread whose loads are in flight ahead of use
-        static_assert(NI % G == 0, "NI must be a multiple of G");
-        V v0[2][G];
-        uint32_t oo[2][G];
+        // G items per thread in flight ahead of the one processed: item k + G is issued just
+        // before item k is processed (a ring of G + 1 even-row vectors)
+        constexpr int G = NTH == 1024 ? 2 : RES_G;   // 4 waves per SIMD: half the registers, as many loads in flight per CU
+        V v0[G + 1];
+        uint32_t oo[G + 1];
         SsCursor cur;
         cur.init((uint32_t)tid, (uint32_t)CR, (uint32_t)W);
-        auto issue = [&](int g, int s) {
-#pragma unroll
-            for (int i = 0; i < G; ++i) {
-                const int k = g * G + i;
-                const bool in = (uint32_t)(k * RES_THREADS + tid) < items;
-                const uint32_t o = in ? cur.o : 0u;
-                oo[s][i] = in ? cur.o : 0xFFFFFFFFu;
-                v0[s][i] = ldv<NT>(reinterpret_cast<const V*>(src + o));
-                r1[k] = ldv<NT>(reinterpret_cast<const V*>(src + o + W));
-                cur.step(dr, (uint32_t)CR, ostep, owrap);
-            }
+        auto issue = [&](int k) {
+            uint32_t itv = (uint32_t)(k * NTH + tid);
+            asm volatile("" : "+v"(itv));   // no lane mask computed ahead (see the embed phase)
+            const bool in = itv < items;
+            const uint32_t o = in ? cur.o : 0u;
+            oo[k % (G + 1)] = in ? cur.o : 0xFFFFFFFFu;
+            v0[k % (G + 1)] = ldv<NT>(reinterpret_cast<const V*>(src + o));
+            r1[k] = ldv<NT>(reinterpret_cast<const V*>(src + o + W));
+            cur.step(dr, (uint32_t)CR, ostep, owrap);
         };
-        issue(0, 0);
 #pragma unroll
-        for (int g = 0; g < NI / G; ++g) {
-            const int s = g & 1;
-            // the next group's loads go out here and no earlier: left free, hipcc hoisted every
-            // load of the slice to the top (2 x NI vectors live at once: spills at NI = 16)
+        for (int k = 0; k < G && k < NI; ++k) issue(k);
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            // the next load goes out here and no earlier: left free, hipcc hoisted every load of
+            // the slice to the top (2 x NI vectors live at once: spills at NI = 16)
             asm volatile("" ::: "memory");
-            if (g + 1 < NI / G) issue(g + 1, s ^ 1);
+            if (k + G < NI) issue(k + G);
             asm volatile("" ::: "memory");
+            V& a0 = v0[k % (G + 1)];
+            V& a1 = r1[k];
+            // one item at a time: left free, hipcc interleaved several items' unpacked pixels
+            // and masks (~25 VGPRs each) for ILP and spilled the kept rows at NI = 16
+            asm volatile("" : "+v"(a0.x), "+v"(a0.y), "+v"(a0.z), "+v"(a0.w), "+v"(a1.x), "+v"(a1.y), "+v"(a1.z),
+                         "+v"(a1.w));
+            const bool in = oo[k % (G + 1)] != 0xFFFFFFFFu;
+            int x[4], a[4], bb[4], cc[4];
+            uint32_t ep = 0;
 #pragma unroll
-            for (int i = 0; i < G; ++i) {
-                const int k = g * G + i;
-                V& a0 = v0[s][i];
-                V& a1 = r1[k];
-                // one item at a time: left free, hipcc interleaved the G items' unpacked pixels
-                // and masks (~25 VGPRs each) for ILP and spilled the kept rows at NI = 16
-                asm volatile("" : "+v"(a0.x), "+v"(a0.y), "+v"(a0.z), "+v"(a0.w), "+v"(a1.x), "+v"(a1.y), "+v"(a1.z),
-                             "+v"(a1.w));
-                const bool in = oo[s][i] != 0xFFFFFFFFu;
-                int x[4], a[4], bb[4], cc[4];
-                uint32_t ep = 0;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    x[q] = (int)get_px(a1, 2 * q + 1); a[q] = (int)get_px(a1, 2 * q);
-                    bb[q] = (int)get_px(a0, 2 * q + 1); cc[q] = (int)get_px(a0, 2 * q);
-                    const int e = x[q] - med3(a[q], bb[q], cc[q]);
-                    ep |= ((uint32_t)min(127, max(-128, e)) & 0xFFu) << (8 * q);
-                }
-                // computed here, in the read phase: left free, hipcc sank it into the embed phase
-                // and kept the even row's pixels alive for it (spills at NI = 16)
-                asm volatile("" : "+v"(ep));
-                re[k] = ep;
-                ehist_add4<RES_THREADS>(cnt, tid, x, a, bb, cc, in ? 4 : 0, tmax, maxval);
-                stv<NT>(in ? reinterpret_cast<V*>(dst + oo[s][i]) : sink_v, a0);
+            for (int q = 0; q < 4; ++q) {
+                x[q] = (int)get_px(a1, 2 * q + 1); a[q] = (int)get_px(a1, 2 * q);
+                bb[q] = (int)get_px(a0, 2 * q + 1); cc[q] = (int)get_px(a0, 2 * q);
+                const int e = x[q] - med3(a[q], bb[q], cc[q]);
+                // byte q (res_ex_bytes): the clamped error, near, expansion safe (p + 2e = x + e)
+                const uint32_t sfe = (unsigned)(x[q] + e) < (unsigned)maxval ? 0x80u : 0u;
+                const uint32_t nr = (e >= 0 ? x[q] + tmax > maxval : x[q] < tmax) ? 0x40u : 0u;
+                ep |= (((uint32_t)min(30, max(-32, e)) & 0x3Fu) | nr | sfe) << (8 * q);
             }
+            // computed here, in the read phase: left free, hipcc sank it into the embed phase
+            // and kept the even row's pixels alive for it (spills at NI = 16)
+            asm volatile("" : "+v"(ep));
+            re[k] = ep;
+            ehist_add4<NTH>(cnt, tid, x, a, bb, cc, in ? 4 : 0, tmax, maxval);
+            stv<NTS>(in ? reinterpret_cast<V*>(dst + oo[k % (G + 1)]) : sink_v, a0);
         }
     }
     lds_barrier();
+    RES_STAMP(1);
     // ---- T: the smallest T <= tmax whose capacity holds L (pee_select_slice's rule)
-    for (int u = wv; u < tmax; u += RES_WAVES) {
+    for (int u = wv; u < tmax; u += NWV) {
         uint32_t s = 0;
 #pragma unroll
-        for (int j = 0; j < RES_THREADS / 64; ++j) s += cnt[u * RES_THREADS + j * 64 + lane];
+        for (int j = 0; j < NTH / 64; ++j) s += cnt[u * NTH + j * 64 + lane];
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
         if (lane == 0) s_bins[u] = s;
@@ -2265,88 +2306,153 @@ __global__ __launch_bounds__(RES_THREADS) void k_pee_embed_res(const uint16_t* _
     }
     lds_barrier();
     const int Tthr = s_T;
+    RES_STAMP(2);
 
-    // ---- embed phase: the odd rows from registers, in item order (no loads)
-    uint32_t running = 0, unsafe_n = 0;
-    int par = 0;
-    bool live = L > 0;
+    // ---- embed phase: the odd rows from registers, in item order (no loads).  Every rank is
+    // known before any candidate moves: pass A counts each item's expandable candidates, ONE
+    // block scan (the NI chunks' counters packed two per word, 16-bit fields) gives every
+    // item its exclusive rank, pass B embeds every item with no further barrier.  A block
+    // scan per chunk (or per 2-4 chunks) left this phase latency-bound: a barrier and its LDS
+    // round trips per chunk with two waves per SIMD, 20 of 60 us at C3 (tools/res_trace.py)
+    const uint32_t* pay32 = reinterpret_cast<const uint32_t*>(pay);
+    // the field's two words: ranks < L lie in the staged words; larger ranks (unused bits)
+    // only need an address inside the pad
+    const uint32_t pmax = RES_PAD_WORDS - 2;
+    const bool embed = trace != 2;   // trace 2: timing diagnostics only (no embedding: wrong stego)
+    // pass A: each item's expandable+safe candidates counted from its error bytes (SWAR,
+    // res_ex_bytes): items 2i, 2i+1 in 16-bit fields, wave-exclusive ranks to LDS (the
+    // counters' words, free once T is chosen; the registers are full of kept rows)
+    uint32_t* s_ex = pad + RES_PAD_WORDS - (NI / 2) * NTH;
+#pragma unroll
+    for (int i = 0; i < NI / 2; ++i) {
+        uint32_t itv[2], ep[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            itv[h] = (uint32_t)(2 * i + h) * NTH + (uint32_t)tid;
+            ep[h] = re[2 * i + h];
+        }
+        asm volatile("" : "+v"(itv[0]), "+v"(itv[1]), "+v"(ep[0]), "+v"(ep[1]));   // nothing of pass B ahead
+        uint32_t c = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t esm = res_ex_bytes(ep[h], Tthr) & ep[h];
+            c |= (itv[h] < items ? (uint32_t)__popc(esm) : 0u) << (16 * h);
+        }
+        const uint32_t inc = wave_incl_dpp(c);
+        if (lane == 63) s_wt[i][wv] = inc;
+        s_ex[i * NTH + tid] = inc - c;
+    }
+    lds_barrier();
+    {   // per word i: this wave's base over the waves before it, the chunks' bases over all
+        const bool inr = (lane & 15) < NWV;
+        uint32_t cb = 0;
+#pragma unroll
+        for (int i = 0; i < NI / 2; ++i) {
+            int x = inr ? (int)s_wt[i][lane & (NWV - 1)] : 0;
+            x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);   // row_shr:1
+            x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);   // row_shr:2
+            x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);   // row_shr:4
+            if constexpr (NWV > 8) x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);   // row_shr:8
+            const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane(x, NWV - 1);
+            const uint32_t wb = wv ? (uint32_t)__builtin_amdgcn_readlane(x, wv - 1) : 0u;
+            if (lane == 0) s_wb[i][wv] = wb;   // per-field add later: a chunk's total < 2^16
+            if (tid == 0) { s_cb[2 * i] = cb; s_cb[2 * i + 1] = cb + (tot & 0xFFFFu); }
+            cb += (tot & 0xFFFFu) + (tot >> 16);
+        }
+    }
+    lds_barrier();   // chunk bases
+    RES_STAMP(3);
+    uint32_t unsafe_n = 0;
     SsCursor cur;
     cur.init((uint32_t)tid, (uint32_t)CR, (uint32_t)W);
-    const uint32_t* pay32 = reinterpret_cast<const uint32_t*>(pay);
-    const uint32_t pmax = (uint32_t)max(2 * pw - 2, 0);
+    // item k's rank and payload field are read from LDS one item ahead (during item k - 1), so
+    // their two LDS round trips are off the item's own dependency chain
+    auto rank_of = [&](int k) {
+        const uint32_t e2 = s_ex[(k / 2) * NTH + tid] + s_wb[k / 2][wv];
+        return s_cb[k] + ((e2 >> (16 * (k & 1))) & 0xFFFFu);
+    };
+    auto field_at = [&](uint32_t rs) {
+        const uint32_t w = min(rs >> 5, pmax);
+        return __builtin_amdgcn_alignbit(pay32[w + 1], pay32[w], rs & 31u);
+    };
+    uint32_t rs_n = rank_of(0);
+    uint32_t field_n = field_at(rs_n);
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
-        const uint32_t it = (uint32_t)k * RES_THREADS + tid;
-        const bool ok = it < items;
-        V& v1 = r1[k];
+        uint32_t itv = (uint32_t)k * NTH + (uint32_t)tid;
         uint32_t ep = re[k];
-        // this chunk's values enter here: nothing derived from them (unpacked pixels, errors,
-        // the store offset) is computed ahead for all chunks at once
-        asm volatile("" : "+v"(v1.x), "+v"(v1.y), "+v"(v1.z), "+v"(v1.w), "+v"(ep), "+v"(cur.o), "+v"(cur.cc));
+        V& v1 = r1[k];
+        const uint32_t rs = rs_n, field = field_n;
+        if (k + 1 < NI) {
+            rs_n = rank_of(k + 1);
+            field_n = field_at(rs_n);
+        }
+        // this item's values enter here: nothing derived from them is computed ahead for all
+        // items at once (registers), no lane mask is kept across items (SGPRs)
+        asm volatile("" : "+v"(v1.x), "+v"(v1.y), "+v"(v1.z), "+v"(v1.w), "+v"(ep), "+v"(itv), "+v"(cur.o),
+                     "+v"(cur.cc));
         const uint32_t o1 = cur.o + (uint32_t)W;
         cur.step(dr, (uint32_t)CR, ostep, owrap);
-        uint32_t wm = 0;
-        if (live) {   // uniform; no vector memory instruction inside
-            uint32_t esm = 0, safem = 0, rightm = 0, expm = 0;
+        const bool ok = itv < items;
+        uint32_t ns_b = 0;   // processed candidates left unchanged as unsafe (the location map)
+        if (embed && rs < L) {   // divergent only at the lane holding `end`; no memory op inside
+            const uint32_t ex_b = res_ex_bytes(ep, Tthr);
+            const uint32_t esm_b = ex_b & ep;   // expandable + safe: carry payload bits
+            const uint32_t m = ok ? min(L - rs, 4u) : 0u;
+            const uint32_t pre_b = res_prefix(esm_b);
+            // processed: fewer than m payload carriers before the candidate in the item
+            const uint32_t proc_b = ~((pre_b | 0x80808080u) - __builtin_amdgcn_perm(m, m, 0u)) & 0x80808080u;
+            // safe: expandable -> the kept bit; shifted -> not near (else checked exactly below)
+            uint32_t safe_b = ((ex_b & ep) | (~ex_b & ~(ep << 1))) & 0x80808080u;
+            const uint32_t nr_b = ~ex_b & (ep << 1) & proc_b;
+            if (__builtin_amdgcn_ballot_w64(nr_b != 0u)) {   // wave-uniform; rare on smooth data
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t w = q == 0 ? v1.x : q == 1 ? v1.y : q == 2 ? v1.z : v1.w;
+                    const int y = (int)(w >> 16) + res_med3(__builtin_amdgcn_sbfe((int)ep, 8 * q, 6), -Tthr, Tthr);
+                    if (((nr_b >> (8 * q + 7)) & 1u) && (unsigned)y <= (unsigned)maxval) safe_b |= 0x80u << (8 * q);
+                }
+            }
+            const uint32_t sel_b = proc_b & safe_b;
+            // a moved candidate: y = x + clamp(e + bit, -T, T); the bit (field bit pre_q) is
+            // absorbed by the clamp for a shifted one (e >= T or e < -T)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int x = (int)get_px(v1, 2 * q + 1);
-                const int e = (int)(int8_t)(uint8_t)(ep >> (8 * q));
-                const bool expand = (unsigned)(e + Tthr) < (unsigned)(2 * Tthr);
-                const bool right = e >= Tthr;
-                const bool ok_e = (unsigned)(x + e) < (unsigned)maxval, ok_r = x <= maxval - Tthr, ok_l = x >= Tthr;
-                const bool safe = (expand & ok_e) | (!expand & right & ok_r) | (!expand & !right & ok_l);
-                safem |= safe ? 1u << q : 0u;
-                rightm |= right ? 1u << q : 0u;
-                expm |= expand ? 1u << q : 0u;
-                esm |= (expand & safe) ? 1u << q : 0u;
+                uint32_t& w = q == 0 ? v1.x : q == 1 ? v1.y : q == 2 ? v1.z : v1.w;
+                const int bit = q == 0 ? (int)(field & 1u) : (int)__builtin_amdgcn_ubfe(field, pre_b >> (8 * q), 1);
+                int d = res_med3(__builtin_amdgcn_sbfe((int)ep, 8 * q, 6) + bit, -Tthr, Tthr);
+                d &= __builtin_amdgcn_sbfe((int)sel_b, 8 * q + 7, 1);
+                w += (uint32_t)d << 16;
             }
-            if (!ok) esm = 0u;
-            const uint32_t n = (uint32_t)__popc(esm);
-            uint32_t ex, tot;
-            res_scan_small(n, wtot, par, &ex, &tot);
-            par ^= 1;
-            const uint32_t rs = running + ex;
-            const uint32_t m = (ok & (L > rs)) ? min(L - rs, 4u) : 0u;
-            const uint32_t w = min(rs >> 5, pmax);
-            const uint32_t field = __builtin_amdgcn_alignbit(pay32[w + 1], pay32[w], rs & 31u);
-            uint32_t procm = 0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {   // branch-free
-                const uint32_t bit = 1u << q;
-                const uint32_t pre = (uint32_t)__popc(esm & (bit - 1u));
-                const bool proc = pre < m;
-                procm |= proc ? bit : 0u;
-                const int x = (int)get_px(v1, 2 * q + 1);
-                const int e = (int)(int8_t)(uint8_t)(ep >> (8 * q));
-                const int nv_e = x + e + (int)((field >> pre) & 1u);   // p + 2e + bit
-                const int nv_s = (rightm & bit) ? x + Tthr : x - Tthr;
-                const int nv = (proc & ((safem & bit) != 0u)) ? ((expm & bit) ? nv_e : nv_s) : x;
-                set_px(v1, 2 * q + 1, (uint32_t)nv);
-            }
-            if (m != 0 && L - rs <= n) s_end = (int)(4 * it) + 31 - __clz(procm & esm);
-            const uint32_t nib = procm & ~safem;
+            if (m != 0 && L - rs <= (uint32_t)__popc(esm_b))
+                s_end = (int)(4 * itv) + ((31 - __clz(proc_b & esm_b)) >> 3);
+            ns_b = proc_b & ~safe_b;
+        }
+        uint32_t wm = 0;
+        if (__builtin_amdgcn_ballot_w64(ns_b != 0u)) {   // wave-uniform; rare
+            const uint32_t nib = res_nibble(ns_b);
             unsafe_n += (uint32_t)__popc(nib);
             wm = nib << (4 * (lane & 7));
             wm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
             wm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
             wm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0x141, 0xF, 0xF, false);   // row_half_mirror
-            running += tot;
-            if (running >= L) live = false;
         }
         // stores, unconditional: the map word halves (zeros past `end`), the odd row
-        const uint32_t wix = (4 * it) >> 6;
-        *(ok && (lane & 7) == 0 && (int)wix < lmw ? reinterpret_cast<uint32_t*>(lm + wix) + ((lane >> 3) & 1) : sink_w) = wm;
-        stv<NT>(ok ? reinterpret_cast<V*>(dst + o1) : sink_v + 1, v1);
+        const uint32_t wix = (4 * itv) >> 6;
+        *(ok && (lane & 7) == 0 && (int)wix < lmw ? reinterpret_cast<uint32_t*>(lm + wix) + ((lane >> 3) & 1) : sink_w) =
+            wm;
+        stv<NTS>(ok ? reinterpret_cast<V*>(dst + o1) : sink_v + 1, v1);
     }
+    const uint32_t running = s_cap;   // expandable candidates of the slice at T
     // lm_count: one block reduction
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) unsafe_n += __shfl_xor(unsafe_n, o, 64);
     if (lane == 0) red[wv] = unsafe_n;
     lds_barrier();
+    RES_STAMP(4);
     if (tid == 0) {
         uint32_t un = 0;
-        for (int w = 0; w < RES_WAVES; ++w) un += red[w];
+        for (int w = 0; w < NWV; ++w) un += red[w];
         codec_pee_meta* M = meta_all + b;
         M->T = Tthr; M->maxval = maxval; M->L = (int)L; M->nc = nc; M->ntiles = ntiles; M->h = H; M->w = W;
         M->lm_count = (int)un;
@@ -2653,6 +2759,10 @@ int codec_debug_lb_trace(unsigned long long* out, int n) {   // diagnostic build
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lb_trace), (size_t)n * 8) == hipSuccess ? n : -1;
 }
 #endif
+int codec_debug_res_trace(unsigned long long* out, int n) {   // CODEC_PEE_RES_TRACE=1 runs only
+    if (n > RES_TRACE_WG * 5) n = RES_TRACE_WG * 5;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_res_trace), (size_t)n * 8) == hipSuccess ? n : -1;
+}
 #ifdef PEE_SS_TRACE
 int codec_debug_ss_trace(unsigned long long* out, int n) {   // diagnostic build only
     if (n > SS_TRACE_N) n = SS_TRACE_N;
@@ -2913,16 +3023,28 @@ int codec_pee_embed_auto(const codec_pee_params* P, const void* cover, void* ste
     const bool nt = knob("CODEC_NT", 1) != 0;
     // resident variant (out of place, slices of <= 512 x 32 items, e.g. C3 / C4's 512^2): the
     // cover is read once and kept on the CU between the capacity and the embed phase
-    const long long nres = (items + RES_THREADS - 1) / RES_THREADS;
-    if (!inplace && knob("CODEC_PEE_RES", 1) != 0 && nres <= 32 && 2LL * P->payload_words <= RES_CNT_BASE(tmax)) {
+    // threads of the resident workgroup: 512 (two waves per SIMD, up to 32 items per lane in
+    // 256 registers) or 1024 (four waves per SIMD, up to 16 items per lane in 128)
+    const int nth = (int)knob("CODEC_PEE_RES_THREADS", 512) == 1024 ? 1024 : 512;
+    const long long nres = (items + nth - 1) / nth;
+    if (!inplace && knob("CODEC_PEE_RES", 1) != 0 && nres <= (nth == 512 ? 32 : 16) && tmax <= SS_AUTO_TMAX &&
+        2LL * P->payload_words + 2 <= RES_PAD_WORDS - 16LL * nth) {   // payload below the counters / ranks
         ProfScope prof(st, CODEC_K_PEE_EMBED_RES);
-#define PRES(NI, NTV) hipLaunchKernelGGL((k_pee_embed_res<NI, NTV>), dim3((unsigned)P->B), dim3(RES_THREADS), 0, st, \
+#define PRES(NI, NTV, NTS, NTH) hipLaunchKernelGGL((k_pee_embed_res<NI, NTV, NTS, NTH>), dim3((unsigned)P->B), dim3(NTH), 0, st, \
             static_cast<const uint16_t*>(cover), static_cast<uint16_t*>(stego), P->H, P->W, P->maxval, lengths, \
             reinterpret_cast<const u64*>(payload), P->payload_words, meta, reinterpret_cast<u64*>(lm), P->lm_words, \
-            static_cast<char*>(workspace) + L.sink, (int)tmax, t_out)
-        if (nres <= 8) { if (nt) PRES(8, true); else PRES(8, false); }
-        else if (nres <= 16) { if (nt) PRES(16, true); else PRES(16, false); }
-        else { if (nt) PRES(32, true); else PRES(32, false); }
+            static_cast<char*>(workspace) + L.sink, (int)tmax, t_out, trace)
+        const int trace = (int)knob("CODEC_PEE_RES_TRACE", 0);
+        // non-temporal loads, plain stores (nt stores: read phase 29.6 -> 32.5 us at C3);
+        // CODEC_PEE_RES_NTS=1 / CODEC_NT=0 for A/B
+        const bool nts = knob("CODEC_PEE_RES_NTS", 0) != 0;
+#define PRESN(NI, NTH) do { if (!nt) PRES(NI, false, false, NTH); else if (nts) PRES(NI, true, true, NTH); \
+                            else PRES(NI, true, false, NTH); } while (0)
+        if (nth == 1024) { if (nres <= 8) PRESN(8, 1024); else PRESN(16, 1024); }
+        else if (nres <= 8) PRESN(8, 512);
+        else if (nres <= 16) PRESN(16, 512);
+        else PRESN(32, 512);
+#undef PRESN
 #undef PRES
         LAUNCH_CHECK("k_pee_embed_res");
         if (P->H & 1) HIP_TRY(pee_copy_last_rows(P, cover, stego, st));

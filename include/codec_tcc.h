@@ -239,6 +239,11 @@ size_t codec_pee_extract_flag_offset(const codec_pee_params* P);
  * counting the missing predecessors from pixels (exact results), [2] embed / [3] extract
  * in-place chunks whose look-back timed out unrecovered.  0 on bad parameters. */
 size_t codec_pee_diag_offset(const codec_pee_params* P);
+/* Diagnostics: phase stamps of the last k_pee_embed_res launch run with the env knob
+ * CODEC_PEE_RES_TRACE=1 (wall_clock64 at entry / end of the read phase / T chosen / ranks
+ * known / end of the embed phase, 5 per workgroup, first 1024 workgroups); returns the count
+ * copied or -1. */
+int codec_debug_res_trace(unsigned long long* out, int n);
 /* cover -> stego (full copy + expansion/shifting of candidates 0..end), lm, meta.
  * lengths[B] (device int32) = payload bits per slice.
  * stego == cover is allowed (in place): only the items up to `end` are read and

@@ -143,3 +143,67 @@ def test_bench_launches_its_own_ranks():
     bad = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2"],
                          env=dict(env, WORLD_SIZE="1", RANK="0"), cwd=repo, capture_output=True, text=True, timeout=120)
     assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr
+
+
+def _rccl_worker(port, q):
+    """One rank over the nccl (= RCCL) backend: the exchanges' RCCL branches
+    (all_gather_into_tensor, all_reduce) on real kernel records."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        assert dist.get_backend() == "nccl"
+        import codec_tcc_amd as ct
+        from codec_tcc_amd import framing, synth
+        from codec_tcc_amd import distributed as D
+        from codec_tcc_amd.pee import PeeCodec
+        n, H, W = 3, 256, 256
+        allc = _covers(n, H, W, dev)
+        codec = PeeCodec(n, H, W, dtype="uint16", T=2, device=dev)
+        enc = codec.embed(allc, [framing.to_bits(synth.payload(96, 40 + g)) for g in range(n)])
+        xch = D.PeeRecordExchange(n, 1, dev)
+        ok = True
+        for _ in range(3):                      # first call agrees the width; later ones carry it
+            xch.mark()
+            xch.start(enc.meta, enc.lm)
+            gmeta, glm = xch.join()
+            torch.cuda.synchronize()
+            ok &= bool(torch.equal(gmeta, enc.meta))
+            ok &= bool(torch.equal(glm, D.map_prefix(enc.meta, enc.lm, xch.lm_words)))
+        ok &= xch.overflows() == 0 and D.agree_max(7, device=dev) == 7
+        lcodec = ct.Codec(n, H, W, dtype="uint16", beta=0.4, block=16, device=dev)
+        pl = ct.make_payloads([synth.payload(96, 70 + g) for g in range(n)], dev)
+        lenc = lcodec.encode(allc, pl)
+        rx = D.RecordExchange(n, pl.map_words, 1, dev)
+        rx.mark()
+        rx.start(lenc.meta, lenc.maps)
+        allrec = rx.join()
+        torch.cuda.synchronize()
+        ok &= bool(torch.equal(allrec, D.pack_records(lenc.meta, lenc.maps)))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - reported through the queue
+        q.put((False, repr(e)))
+        return
+    q.put((bool(ok), ""))
+
+
+def test_exchanges_over_rccl_world1():
+    """The RCCL code path of the record exchanges (the 8-GPU bench's collectives) with one
+    rank on the box's one GPU: RCCL refuses two ranks on one device, so this is the only RCCL
+    run possible here; the multi-rank path is covered over gloo above."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    try:
+        ok, err = q.get(timeout=110)
+    finally:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+            p.join(timeout=10)
+    assert ok, err
