@@ -2168,6 +2168,21 @@ __device__ __forceinline__ int res_med3(int x, int lo, int hi) {
     asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "v"(hi));
     return r;
 }
+// the capacity histogram from an item's kept bytes: lane-private counters [tmax][NTH] (no
+// bank conflicts), bin min(u, tmax - 1) += (u < tmax) & expansion safe, one LDS add per
+// candidate (no return; candidates of one item sharing a bin need no merge)
+template <int NTH>
+__device__ __forceinline__ void res_hist4(uint32_t* cnt, int tid, uint32_t ep, bool in, int tmax) {
+    const uint32_t s5 = ep & 0x20202020u;
+    const uint32_t u_b = (ep ^ (res_opaque(s5) - (s5 >> 5))) & 0x1F1F1F1Fu;
+    const uint32_t c_b = ~((u_b | 0x80808080u) - (uint32_t)tmax * 0x01010101u) & ep & (in ? 0x80808080u : 0u);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t u = min(__builtin_amdgcn_ubfe(u_b, 8 * q, 5), (uint32_t)tmax - 1u);
+        __hip_atomic_fetch_add(cnt + u * NTH + tid, __builtin_amdgcn_ubfe(c_b, 8 * q + 7, 1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
 
 // phase stamps (CODEC_PEE_RES_TRACE=1, diagnostics only): per workgroup wall_clock64() at
 // entry, end of the read phase, T chosen, end of the embed phase (codec_debug_res_trace)
@@ -2270,14 +2285,14 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
                 const int e = x[q] - med3(a[q], bb[q], cc[q]);
                 // byte q (res_ex_bytes): the clamped error, near, expansion safe (p + 2e = x + e)
                 const uint32_t sfe = (unsigned)(x[q] + e) < (unsigned)maxval ? 0x80u : 0u;
-                const uint32_t nr = (e >= 0 ? x[q] + tmax > maxval : x[q] < tmax) ? 0x40u : 0u;
-                ep |= (((uint32_t)min(30, max(-32, e)) & 0x3Fu) | nr | sfe) << (8 * q);
+                const uint32_t nr = (unsigned)(x[q] + (e >= 0 ? tmax : -tmax)) > (unsigned)maxval ? 0x40u : 0u;
+                ep |= (((uint32_t)res_med3(e, -32, 30) & 0x3Fu) | nr | sfe) << (8 * q);
             }
             // computed here, in the read phase: left free, hipcc sank it into the embed phase
             // and kept the even row's pixels alive for it (spills at NI = 16)
             asm volatile("" : "+v"(ep));
             re[k] = ep;
-            ehist_add4<NTH>(cnt, tid, x, a, bb, cc, in ? 4 : 0, tmax, maxval);
+            res_hist4<NTH>(cnt, tid, ep, in, tmax);
             stv<NTS>(in ? reinterpret_cast<V*>(dst + oo[k % (G + 1)]) : sink_v, a0);
         }
     }
