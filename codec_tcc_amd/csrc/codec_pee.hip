@@ -2204,10 +2204,12 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
     typedef uint4 V;
     constexpr int NWV = NTH / 64;
     static_assert(NWV <= 16, "wave totals are scanned along one DPP row");
+    static_assert(NI % 8 == 0, "pass A packs four items per word, the wave bases four word pairs per scan");
     __shared__ uint32_t pad[RES_PAD_WORDS];
     __shared__ uint32_t s_wt[NI / 2][NWV];   // embed phase: wave totals of the packed counters
     __shared__ uint32_t s_wb[NI / 2][NWV];    // embed phase: wave bases of the packed counters
     __shared__ uint32_t s_cb[NI];                   // embed phase: rank of each chunk's first candidate
+    __shared__ uint32_t s_tot[NI / 2];              // embed phase: chunk totals (16-bit pairs)
     __shared__ uint32_t red[NWV];
     __shared__ uint32_t s_bins[SS_AUTO_TMAX];
     __shared__ int s_end, s_T;
@@ -2334,48 +2336,56 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
     // only need an address inside the pad
     const uint32_t pmax = RES_PAD_WORDS - 2;
     const bool embed = trace != 2;   // trace 2: timing diagnostics only (no embedding: wrong stego)
-    // pass A: each item's expandable+safe candidates counted from its error bytes (SWAR,
-    // res_ex_bytes): items 2i, 2i+1 in 16-bit fields, wave-exclusive ranks to LDS (the
-    // counters' words, free once T is chosen; the registers are full of kept rows)
-    uint32_t* s_ex = pad + RES_PAD_WORDS - (NI / 2) * NTH;
+    // pass A: each item's expandable+safe candidates counted from its kept bytes (SWAR,
+    // res_ex_bytes), items 4j .. 4j + 3 in the bytes of one word, one wave scan per word: the
+    // lane-exclusive prefixes (<= 63 x 4) never overflow a byte, only lane 63's inclusive sum
+    // (never read by another lane); they go to LDS (the counters' words, free once T is
+    // chosen; the registers are full of kept rows), the wave totals (<= 256) as 16-bit pairs
+    uint32_t* s_ex = pad + RES_PAD_WORDS - (NI / 4) * NTH;
 #pragma unroll
-    for (int i = 0; i < NI / 2; ++i) {
-        uint32_t itv[2], ep[2];
+    for (int j = 0; j < NI / 4; ++j) {
+        uint32_t itv[4], ep[4];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            itv[h] = (uint32_t)(2 * i + h) * NTH + (uint32_t)tid;
-            ep[h] = re[2 * i + h];
+        for (int h = 0; h < 4; ++h) {
+            itv[h] = (uint32_t)(4 * j + h) * NTH + (uint32_t)tid;
+            ep[h] = re[4 * j + h];
         }
-        asm volatile("" : "+v"(itv[0]), "+v"(itv[1]), "+v"(ep[0]), "+v"(ep[1]));   // nothing of pass B ahead
+        asm volatile("" : "+v"(itv[0]), "+v"(itv[1]), "+v"(itv[2]), "+v"(itv[3]), "+v"(ep[0]), "+v"(ep[1]),
+                     "+v"(ep[2]), "+v"(ep[3]));   // nothing of pass B ahead
         uint32_t c = 0;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t esm = res_ex_bytes(ep[h], Tthr) & ep[h];
-            c |= (itv[h] < items ? (uint32_t)__popc(esm) : 0u) << (16 * h);
+        for (int h = 0; h < 4; ++h)
+            c |= (uint32_t)__popc(res_ex_bytes(ep[h], Tthr) & ep[h] & (itv[h] < items ? ~0u : 0u)) << (8 * h);
+        const uint32_t ex = wave_incl_dpp(c) - c;
+        s_ex[j * NTH + tid] = ex;
+        if (lane == 63) {   // chunk totals: fields 0 and 2 / 1 and 3 as 16-bit halves
+            const uint32_t lo = (ex & 0x00FF00FFu) + (c & 0x00FF00FFu);
+            const uint32_t hi = ((ex >> 8) & 0x00FF00FFu) + ((c >> 8) & 0x00FF00FFu);
+            s_wt[2 * j][wv] = (lo & 0xFFFFu) | (hi << 16);
+            s_wt[2 * j + 1][wv] = (lo >> 16) | (hi & 0xFFFF0000u);
         }
-        const uint32_t inc = wave_incl_dpp(c);
-        if (lane == 63) s_wt[i][wv] = inc;
-        s_ex[i * NTH + tid] = inc - c;
     }
     lds_barrier();
-    {   // per word i: this wave's base over the waves before it, the chunks' bases over all
-        const bool inr = (lane & 15) < NWV;
-        uint32_t cb = 0;
+    if (wv == 0) {   // wave bases per pair of chunks (four pairs at once, one per DPP row), then
+                     // the chunks' bases over the whole slice
+        const int r = lane >> 4, j = lane & 15;
 #pragma unroll
-        for (int i = 0; i < NI / 2; ++i) {
-            int x = inr ? (int)s_wt[i][lane & (NWV - 1)] : 0;
-            x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);   // row_shr:1
-            x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);   // row_shr:2
-            x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);   // row_shr:4
-            if constexpr (NWV > 8) x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);   // row_shr:8
-            const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane(x, NWV - 1);
-            const uint32_t wb = wv ? (uint32_t)__builtin_amdgcn_readlane(x, wv - 1) : 0u;
-            if (lane == 0) s_wb[i][wv] = wb;   // per-field add later: a chunk's total < 2^16
-            if (tid == 0) { s_cb[2 * i] = cb; s_cb[2 * i + 1] = cb + (tot & 0xFFFFu); }
-            cb += (tot & 0xFFFFu) + (tot >> 16);
+        for (int it = 0; it < NI / 8; ++it) {
+            const int i = 4 * it + r;
+            const int x = j < NWV ? (int)s_wt[i][j] : 0;
+            int y = x;
+            y += __builtin_amdgcn_update_dpp(0, y, 0x111, 0xF, 0xF, true);   // row_shr:1
+            y += __builtin_amdgcn_update_dpp(0, y, 0x112, 0xF, 0xF, true);   // row_shr:2
+            y += __builtin_amdgcn_update_dpp(0, y, 0x114, 0xF, 0xF, true);   // row_shr:4
+            if constexpr (NWV > 8) y += __builtin_amdgcn_update_dpp(0, y, 0x118, 0xF, 0xF, true);   // row_shr:8
+            if (j < NWV) s_wb[i][j] = (uint32_t)(y - x);   // per-field: a chunk's total < 2^16
+            if (j == NWV - 1) s_tot[i] = (uint32_t)y;
         }
+        const uint32_t t = lane < NI ? (s_tot[lane >> 1] >> (16 * (lane & 1))) & 0xFFFFu : 0u;
+        const uint32_t cb = wave_incl_dpp(t) - t;
+        if (lane < NI) s_cb[lane] = cb;
     }
-    lds_barrier();   // chunk bases
+    lds_barrier();   // wave and chunk bases
     RES_STAMP(3);
     uint32_t unsafe_n = 0;
     SsCursor cur;
@@ -2383,8 +2393,8 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
     // item k's rank and payload field are read from LDS one item ahead (during item k - 1), so
     // their two LDS round trips are off the item's own dependency chain
     auto rank_of = [&](int k) {
-        const uint32_t e2 = s_ex[(k / 2) * NTH + tid] + s_wb[k / 2][wv];
-        return s_cb[k] + ((e2 >> (16 * (k & 1))) & 0xFFFFu);
+        const uint32_t ex = s_ex[(k / 4) * NTH + tid], wb = s_wb[k / 2][wv];
+        return s_cb[k] + ((wb >> (16 * (k & 1))) & 0xFFFFu) + ((ex >> (8 * (k & 3))) & 0xFFu);
     };
     auto field_at = [&](uint32_t rs) {
         const uint32_t w = min(rs >> 5, pmax);
