@@ -2120,6 +2120,10 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
 #define RES_THREADS 512
 #define RES_WAVES (RES_THREADS / 64)
 #define RES_PAD_WORDS (24 * 1024)   // 96 KB static pad: one workgroup per CU
+// LIN (1024 threads): the kept error words live in LDS ([NI][1024] below the counters, which
+// are 16-bit pairs [8][1024]): 16 VGPRs fewer per lane -- at 128 VGPRs the register-kept
+// words spilled, and each scratch reload made the embed phase wait for every store in flight
+#define RES_PAD_WORDS_LIN (28 * 1024)
 #define RES_CNT_BASE(tmax) (RES_PAD_WORDS - (tmax) * RES_THREADS)
 
 #ifndef RES_G
@@ -2171,7 +2175,7 @@ __device__ __forceinline__ int res_med3(int x, int lo, int hi) {
 // the capacity histogram from an item's kept bytes: lane-private counters [tmax][NTH] (no
 // bank conflicts), bin min(u, tmax - 1) += (u < tmax) & expansion safe, one LDS add per
 // candidate (no return; candidates of one item sharing a bin need no merge)
-template <int NTH>
+template <int NTH, bool PACK = false>
 __device__ __forceinline__ void res_hist4(uint32_t* cnt, int tid, uint32_t ep, bool in, int tmax) {
     const uint32_t s5 = ep & 0x20202020u;
     const uint32_t u_b = (ep ^ (res_opaque(s5) - (s5 >> 5))) & 0x1F1F1F1Fu;
@@ -2179,8 +2183,12 @@ __device__ __forceinline__ void res_hist4(uint32_t* cnt, int tid, uint32_t ep, b
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const uint32_t u = min(__builtin_amdgcn_ubfe(u_b, 8 * q, 5), (uint32_t)tmax - 1u);
-        __hip_atomic_fetch_add(cnt + u * NTH + tid, __builtin_amdgcn_ubfe(c_b, 8 * q + 7, 1), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        if constexpr (PACK)   // bins 2i and 2i + 1 as the halves of word i (a lane counts <= 64 per bin)
+            __hip_atomic_fetch_add(cnt + (u >> 1) * NTH + tid, __builtin_amdgcn_ubfe(c_b, 8 * q + 7, 1) << (16 * (u & 1)),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else
+            __hip_atomic_fetch_add(cnt + u * NTH + tid, __builtin_amdgcn_ubfe(c_b, 8 * q + 7, 1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
@@ -2193,7 +2201,13 @@ __device__ unsigned long long g_res_trace[RES_TRACE_WG * 5];
         if (trace && tid == 0 && b < RES_TRACE_WG) g_res_trace[b * 5 + (i)] = wall_clock64(); \
     } while (0)
 
-template <int NI, bool NT, bool NTS, int NTH>
+// LIN: every lane's items are in range and item k + 1 lies a fixed offset KS after item k
+// (NTH a multiple of the items per row pair, items a multiple of NTH: e.g. 512^2 at 1024
+// threads): no cursor, no lane masks, no sink; the location-map halves are zeroed in the read
+// phase by the lanes that may later write them (same lane, same address: ordered), so the
+// embed phase stores a map word only where a wave has an unsafe candidate (rare), and the
+// lane-exclusive ranks stay in registers
+template <int NI, bool NT, bool NTS, int NTH, bool LIN = false>
 __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restrict__ cover,
                                                                uint16_t* __restrict__ stego, int H, int W, int maxval,
                                                                const int32_t* __restrict__ lengths,
@@ -2205,7 +2219,8 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
     constexpr int NWV = NTH / 64;
     static_assert(NWV <= 16, "wave totals are scanned along one DPP row");
     static_assert(NI % 8 == 0, "pass A packs four items per word, the wave bases four word pairs per scan");
-    __shared__ uint32_t pad[RES_PAD_WORDS];
+    constexpr int PADW = LIN ? RES_PAD_WORDS_LIN : RES_PAD_WORDS;
+    __shared__ uint32_t pad[PADW];
     __shared__ uint32_t s_wt[NI / 2][NWV];   // embed phase: wave totals of the packed counters
     __shared__ uint32_t s_wb[NI / 2][NWV];    // embed phase: wave bases of the packed counters
     __shared__ uint32_t s_cb[NI];                   // embed phase: rank of each chunk's first candidate
@@ -2228,10 +2243,12 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
     V* sink_v = reinterpret_cast<V*>(sink + SS_SINK_SLOT(b, tid));
     uint32_t* sink_w = reinterpret_cast<uint32_t*>(sink + SS_SINK_SLOT(b, tid) + 32);
     RES_STAMP(0);
-    uint32_t* cnt = pad + (RES_PAD_WORDS - tmax * NTH);     // lane-private capacity counters [tmax][512]
+    const int crow = LIN ? (tmax + 1) / 2 : tmax;   // counter rows (LIN: 16-bit pairs)
+    uint32_t* cnt = pad + (PADW - crow * NTH);      // lane-private capacity counters [crow][NTH]
+    uint32_t* s_re = pad + (PADW - (8 + NI) * NTH);   // LIN: kept error words [NI][NTH]
     const u64* payload = payload_all + (size_t)b * pw;
     u64* pay = reinterpret_cast<u64*>(pad);       // the slice's payload words
-    for (int u = 0; u < tmax; ++u) cnt[u * NTH + tid] = 0u;
+    for (int u = 0; u < crow; ++u) cnt[u * NTH + tid] = 0u;
     if (tid == 0) s_end = -1;
     {   // the payload into LDS now (its loads overlap the read phase)
         const int nw = min(pw, (int)((L + 63u) >> 6));
@@ -2239,11 +2256,17 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
     }
     const uint32_t dq = NTH / (uint32_t)CR, dr = NTH % (uint32_t)CR;
     const uint32_t ostep = 2u * (uint32_t)W * dq + 8u * dr, owrap = 2u * (uint32_t)W - 8u * (uint32_t)CR;
+    // LIN: item k of this lane at o_lin + k KS (the host checked dr == 0, items % NTH == 0)
+    const uint32_t KS = ostep;
+    const uint32_t o_lin = 2u * ((uint32_t)tid / (uint32_t)CR) * (uint32_t)W + 8u * ((uint32_t)tid % (uint32_t)CR);
+    // LIN: this lane's location-map half for item k (lanes 8j own one 32-bit half; others: sink)
+    uint32_t* const lm_half = (lane & 7) == 0 ? reinterpret_cast<uint32_t*>(lm + (tid >> 4)) + ((lane >> 3) & 1) : sink_w;
+    const uint32_t lm_step = (lane & 7) == 0 ? (NTH / 16) * 2 : 0u;   // 32-bit words per k
     lds_barrier();   // counters zeroed before any lane adds
 
     // ---- read phase: every item once; even row -> stego now, odd row + errors kept
     V r1[NI];
-    uint32_t re[NI];
+    uint32_t re[LIN ? 1 : NI];
     {
         // G items per thread in flight ahead of the one processed: item k + G is issued just
         // before item k is processed (a ring of G + 1 even-row vectors)
@@ -2253,6 +2276,13 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
         SsCursor cur;
         cur.init((uint32_t)tid, (uint32_t)CR, (uint32_t)W);
         auto issue = [&](int k) {
+            if constexpr (LIN) {
+                const uint32_t o = o_lin + (uint32_t)k * KS;
+                oo[k % (G + 1)] = o;
+                v0[k % (G + 1)] = ldv<NT>(reinterpret_cast<const V*>(src + o));
+                r1[k] = ldv<NT>(reinterpret_cast<const V*>(src + o + W));
+                return;
+            }
             uint32_t itv = (uint32_t)(k * NTH + tid);
             asm volatile("" : "+v"(itv));   // no lane mask computed ahead (see the embed phase)
             const bool in = itv < items;
@@ -2293,9 +2323,15 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
             // computed here, in the read phase: left free, hipcc sank it into the embed phase
             // and kept the even row's pixels alive for it (spills at NI = 16)
             asm volatile("" : "+v"(ep));
-            re[k] = ep;
-            res_hist4<NTH>(cnt, tid, ep, in, tmax);
-            stv<NTS>(in ? reinterpret_cast<V*>(dst + oo[k % (G + 1)]) : sink_v, a0);
+            if constexpr (LIN) s_re[k * NTH + tid] = ep;
+            else re[k] = ep;
+            res_hist4<NTH, LIN>(cnt, tid, ep, LIN || in, tmax);
+            if constexpr (LIN) {
+                stv<NTS>(reinterpret_cast<V*>(dst + oo[k % (G + 1)]), a0);
+                lm_half[(uint32_t)k * lm_step] = 0u;   // cleared now; the embed phase ORs nothing in
+            } else {
+                stv<NTS>(in ? reinterpret_cast<V*>(dst + oo[k % (G + 1)]) : sink_v, a0);
+            }
         }
     }
     lds_barrier();
@@ -2304,7 +2340,8 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
     for (int u = wv; u < tmax; u += NWV) {
         uint32_t s = 0;
 #pragma unroll
-        for (int j = 0; j < NTH / 64; ++j) s += cnt[u * NTH + j * 64 + lane];
+        for (int j = 0; j < NTH / 64; ++j)
+            s += LIN ? (cnt[(u >> 1) * NTH + j * 64 + lane] >> (16 * (u & 1))) & 0xFFFFu : cnt[u * NTH + j * 64 + lane];
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
         if (lane == 0) s_bins[u] = s;
@@ -2334,21 +2371,26 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
     const uint32_t* pay32 = reinterpret_cast<const uint32_t*>(pay);
     // the field's two words: ranks < L lie in the staged words; larger ranks (unused bits)
     // only need an address inside the pad
-    const uint32_t pmax = RES_PAD_WORDS - 2;
+    const uint32_t pmax = PADW - 2;
     const bool embed = trace != 2;   // trace 2: timing diagnostics only (no embedding: wrong stego)
     // pass A: each item's expandable+safe candidates counted from its kept bytes (SWAR,
     // res_ex_bytes), items 4j .. 4j + 3 in the bytes of one word, one wave scan per word: the
     // lane-exclusive prefixes (<= 63 x 4) never overflow a byte, only lane 63's inclusive sum
     // (never read by another lane); they go to LDS (the counters' words, free once T is
     // chosen; the registers are full of kept rows), the wave totals (<= 256) as 16-bit pairs
-    uint32_t* s_ex = pad + RES_PAD_WORDS - (NI / 4) * NTH;
+    uint32_t* s_ex = pad + PADW - (NI / 4) * NTH;
+#ifndef RES_EXR
+#define RES_EXR 0
+#endif
+    constexpr bool EXR = LIN && RES_EXR;   // the lane-exclusive prefixes in registers (spills at 1024)
+    uint32_t exr[EXR ? NI / 4 : 1];
 #pragma unroll
     for (int j = 0; j < NI / 4; ++j) {
         uint32_t itv[4], ep[4];
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
             itv[h] = (uint32_t)(4 * j + h) * NTH + (uint32_t)tid;
-            ep[h] = re[4 * j + h];
+            ep[h] = LIN ? s_re[(4 * j + h) * NTH + tid] : re[4 * j + h];
         }
         asm volatile("" : "+v"(itv[0]), "+v"(itv[1]), "+v"(itv[2]), "+v"(itv[3]), "+v"(ep[0]), "+v"(ep[1]),
                      "+v"(ep[2]), "+v"(ep[3]));   // nothing of pass B ahead
@@ -2357,7 +2399,8 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
         for (int h = 0; h < 4; ++h)
             c |= (uint32_t)__popc(res_ex_bytes(ep[h], Tthr) & ep[h] & (itv[h] < items ? ~0u : 0u)) << (8 * h);
         const uint32_t ex = wave_incl_dpp(c) - c;
-        s_ex[j * NTH + tid] = ex;
+        if constexpr (EXR) exr[j] = ex;
+        else s_ex[j * NTH + tid] = ex;
         if (lane == 63) {   // chunk totals: fields 0 and 2 / 1 and 3 as 16-bit halves
             const uint32_t lo = (ex & 0x00FF00FFu) + (c & 0x00FF00FFu);
             const uint32_t hi = ((ex >> 8) & 0x00FF00FFu) + ((c >> 8) & 0x00FF00FFu);
@@ -2390,9 +2433,19 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
     uint32_t unsafe_n = 0;
     SsCursor cur;
     cur.init((uint32_t)tid, (uint32_t)CR, (uint32_t)W);
+    // LIN: lane k of every wave holds the wave's base rank for item k (read back by readlane)
+    uint32_t vb = 0;
+    if constexpr (LIN) {
+        const int kk = lane < NI ? lane : 0;
+        vb = s_cb[kk] + ((s_wb[kk / 2][wv] >> (16 * (kk & 1))) & 0xFFFFu);
+    }
     // item k's rank and payload field are read from LDS one item ahead (during item k - 1), so
     // their two LDS round trips are off the item's own dependency chain
     auto rank_of = [&](int k) {
+        if constexpr (EXR)
+            return (uint32_t)__builtin_amdgcn_readlane((int)vb, k) + ((exr[k / 4] >> (8 * (k & 3))) & 0xFFu);
+        if constexpr (LIN)
+            return (uint32_t)__builtin_amdgcn_readlane((int)vb, k) + ((s_ex[(k / 4) * NTH + tid] >> (8 * (k & 3))) & 0xFFu);
         const uint32_t ex = s_ex[(k / 4) * NTH + tid], wb = s_wb[k / 2][wv];
         return s_cb[k] + ((wb >> (16 * (k & 1))) & 0xFFFFu) + ((ex >> (8 * (k & 3))) & 0xFFu);
     };
@@ -2405,7 +2458,7 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
         uint32_t itv = (uint32_t)k * NTH + (uint32_t)tid;
-        uint32_t ep = re[k];
+        uint32_t ep = LIN ? s_re[k * NTH + tid] : re[k];
         V& v1 = r1[k];
         const uint32_t rs = rs_n, field = field_n;
         if (k + 1 < NI) {
@@ -2416,9 +2469,11 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
         // items at once (registers), no lane mask is kept across items (SGPRs)
         asm volatile("" : "+v"(v1.x), "+v"(v1.y), "+v"(v1.z), "+v"(v1.w), "+v"(ep), "+v"(itv), "+v"(cur.o),
                      "+v"(cur.cc));
-        const uint32_t o1 = cur.o + (uint32_t)W;
-        cur.step(dr, (uint32_t)CR, ostep, owrap);
-        const bool ok = itv < items;
+        uint32_t ob = o_lin;
+        asm volatile("" : "+v"(ob));   // LIN: the address is formed here (hoisted: 16 spilled pointers)
+        const uint32_t o1 = LIN ? ob + (uint32_t)k * KS + (uint32_t)W : cur.o + (uint32_t)W;
+        if constexpr (!LIN) cur.step(dr, (uint32_t)CR, ostep, owrap);
+        const bool ok = LIN || itv < items;
         uint32_t ns_b = 0;   // processed candidates left unchanged as unsafe (the location map)
         if (embed && rs < L) {   // divergent only at the lane holding `end`; no memory op inside
             const uint32_t ex_b = res_ex_bytes(ep, Tthr);
@@ -2461,6 +2516,15 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
             wm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
             wm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
             wm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0x141, 0xF, 0xF, false);   // row_half_mirror
+            if constexpr (LIN) {   // over the read phase's zero (address formed here, not CSE'd with it)
+                uint32_t ls = lm_step;
+                asm volatile("" : "+v"(ls));
+                lm_half[(uint32_t)k * ls] = wm;
+            }
+        }
+        if constexpr (LIN) {
+            stv<NTS>(reinterpret_cast<V*>(dst + o1), v1);
+            continue;
         }
         // stores, unconditional: the map word halves (zeros past `end`), the odd row
         const uint32_t wix = (4 * itv) >> 6;
@@ -3049,13 +3113,24 @@ int codec_pee_embed_auto(const codec_pee_params* P, const void* cover, void* ste
     // resident variant (out of place, slices of <= 512 x 32 items, e.g. C3 / C4's 512^2): the
     // cover is read once and kept on the CU between the capacity and the embed phase
     // threads of the resident workgroup: 512 (two waves per SIMD, up to 32 items per lane in
-    // 256 registers) or 1024 (four waves per SIMD, up to 16 items per lane in 128)
-    const int nth = (int)knob("CODEC_PEE_RES_THREADS", 512) == 1024 ? 1024 : 512;
+    // 256 registers) or 1024 (four waves per SIMD, up to 16 items per lane in 128); 1024 where
+    // it holds the slice (C3's 512^2, phase trace: last workgroup done at 55.4 -> 52.4 us, embed
+    // phase 14.4 -> 12.8 us), else 512
+    const long long kth = knob("CODEC_PEE_RES_THREADS", 0);
+    auto res_fits = [&](int n) {   // items per lane in registers; payload below the counters / ranks
+        return (items + n - 1) / n <= (n == 512 ? 32 : 16) && 2LL * P->payload_words + 2 <= RES_PAD_WORDS - 16LL * n;
+    };
+    auto lin_fits = [&]() {   // LIN layout: payload below the error words and the counters
+        return 2LL * P->payload_words + 2 <= RES_PAD_WORDS_LIN - 24LL * 1024;
+    };
+    const int nth = kth == 512 ? 512 : kth == 1024 ? 1024 : res_fits(1024) ? 1024 : 512;
     const long long nres = (items + nth - 1) / nth;
-    if (!inplace && knob("CODEC_PEE_RES", 1) != 0 && nres <= (nth == 512 ? 32 : 16) && tmax <= SS_AUTO_TMAX &&
-        2LL * P->payload_words + 2 <= RES_PAD_WORDS - 16LL * nth) {   // payload below the counters / ranks
+    const long long CRl = P->W / 8;
+    const bool lin = nth == 1024 && (items == 8 * 1024 || items == 16 * 1024) && 1024 % CRl == 0 && lin_fits() &&
+                     knob("CODEC_PEE_RES_LIN", 1) != 0;
+    if (!inplace && knob("CODEC_PEE_RES", 1) != 0 && res_fits(nth) && tmax <= SS_AUTO_TMAX) {
         ProfScope prof(st, CODEC_K_PEE_EMBED_RES);
-#define PRES(NI, NTV, NTS, NTH) hipLaunchKernelGGL((k_pee_embed_res<NI, NTV, NTS, NTH>), dim3((unsigned)P->B), dim3(NTH), 0, st, \
+#define PRES(NI, NTV, NTS, NTH, LN) hipLaunchKernelGGL((k_pee_embed_res<NI, NTV, NTS, NTH, LN>), dim3((unsigned)P->B), dim3(NTH), 0, st, \
             static_cast<const uint16_t*>(cover), static_cast<uint16_t*>(stego), P->H, P->W, P->maxval, lengths, \
             reinterpret_cast<const u64*>(payload), P->payload_words, meta, reinterpret_cast<u64*>(lm), P->lm_words, \
             static_cast<char*>(workspace) + L.sink, (int)tmax, t_out, trace)
@@ -3063,12 +3138,16 @@ int codec_pee_embed_auto(const codec_pee_params* P, const void* cover, void* ste
         // non-temporal loads, plain stores (nt stores: read phase 29.6 -> 32.5 us at C3);
         // CODEC_PEE_RES_NTS=1 / CODEC_NT=0 for A/B
         const bool nts = knob("CODEC_PEE_RES_NTS", 0) != 0;
-#define PRESN(NI, NTH) do { if (!nt) PRES(NI, false, false, NTH); else if (nts) PRES(NI, true, true, NTH); \
-                            else PRES(NI, true, false, NTH); } while (0)
-        if (nth == 1024) { if (nres <= 8) PRESN(8, 1024); else PRESN(16, 1024); }
-        else if (nres <= 8) PRESN(8, 512);
-        else if (nres <= 16) PRESN(16, 512);
-        else PRESN(32, 512);
+#define PRESN(NI, NTH, LN) do { if (!nt) PRES(NI, false, false, NTH, LN); else if (nts) PRES(NI, true, true, NTH, LN); \
+                                else PRES(NI, true, false, NTH, LN); } while (0)
+        if (nth == 1024) {
+            if (lin) { if (nres <= 8) PRESN(8, 1024, true); else PRESN(16, 1024, true); }
+            else if (nres <= 8) PRESN(8, 1024, false);
+            else PRESN(16, 1024, false);
+        }
+        else if (nres <= 8) PRESN(8, 512, false);
+        else if (nres <= 16) PRESN(16, 512, false);
+        else PRESN(32, 512, false);
 #undef PRESN
 #undef PRES
         LAUNCH_CHECK("k_pee_embed_res");

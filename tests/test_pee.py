@@ -412,7 +412,11 @@ def test_gpu_capacity_control(kind, h, w, bsz, inplace, pee_path):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("inplace", [False, True])
-@pytest.mark.parametrize("h,w,maxval,tmax", [(65, 64, 4095, 16), (128, 96, None, 5), (66, 128, 4095, 1)])
+@pytest.mark.parametrize("h,w,maxval,tmax", [(65, 64, 4095, 16), (128, 96, None, 5), (66, 128, 4095, 1),
+                                             # the resident kernel's LIN launch (1024 threads, 8 or 16 items
+                                             # per lane, fixed item stride): C3's shape with an odd
+                                             # extra row, and other row widths
+                                             (513, 512, 4095, 16), (256, 1024, None, 5), (1024, 128, 4095, 16)])
 def test_gpu_embed_auto_fused_edges(h, w, maxval, tmax, inplace, monkeypatch):
     """codec_pee_embed_auto's fused launch (slice-serial forced on a small batch) on the
     shapes it must get right: an odd height (last row copied, never a candidate), a
@@ -432,15 +436,21 @@ def test_gpu_embed_auto_fused_edges(h, w, maxval, tmax, inplace, monkeypatch):
     runs = {}
     # fused launch: the resident kernel out of place (k_pee_embed_res, the default) and the
     # two-phase slice-serial one (CODEC_PEE_RES=0); "0": capacity pass + embed, two launches
-    for name, fused, res in (("res", "1", "1"), ("ss", "1", "0"), ("unfused", "0", "1")):
+    # "res_nolin" / "res512": the resident kernel's other launches (CODEC_PEE_RES_LIN=0: the
+    # cursor-stepped 1024-thread one; CODEC_PEE_RES_THREADS=512)
+    for name, fused, res, lin, nth in (("res", "1", "1", "1", "0"), ("ss", "1", "0", "1", "0"),
+                                       ("unfused", "0", "1", "1", "0"), ("res_nolin", "1", "1", "0", "0"),
+                                       ("res512", "1", "1", "1", "512")):
         monkeypatch.setenv("CODEC_PEE_AUTO_FUSED", fused)
         monkeypatch.setenv("CODEC_PEE_RES", res)
+        monkeypatch.setenv("CODEC_PEE_RES_LIN", lin)
+        monkeypatch.setenv("CODEC_PEE_RES_THREADS", nth)
         codec = PeeCodec(bsz, h, w, dtype="uint16", T="auto", tmax=tmax, maxval=maxval)
         dev = torch.from_numpy(covers.copy()).cuda()
         enc = codec.embed(dev, payloads, stego=dev if inplace else None)
         runs[name] = (codec, enc, enc.records(), enc.stego.cpu().numpy(), codec.t_slices.cpu().numpy())
     codec, enc, recs, stego, t_dev = runs["res"]
-    for other in ("ss", "unfused"):
+    for other in ("ss", "unfused", "res_nolin", "res512"):
         _, enc0, recs0, stego0, t_dev0 = runs[other]
         np.testing.assert_array_equal(stego, stego0)
         np.testing.assert_array_equal(t_dev, t_dev0)
