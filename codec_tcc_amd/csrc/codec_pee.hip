@@ -2342,21 +2342,20 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
 #pragma unroll
         for (int j = 0; j < NTH / 64; ++j)
             s += LIN ? (cnt[(u >> 1) * NTH + j * 64 + lane] >> (16 * (u & 1))) & 0xFFFFu : cnt[u * NTH + j * 64 + lane];
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-        if (lane == 0) s_bins[u] = s;
+        s = wave_incl_dpp(s);   // DPP, not shuffles: lane 63 holds the bin's total
+        if (lane == 63) s_bins[u] = s;
     }
     lds_barrier();
-    if (tid == 0) {
-        long long run = 0, cap = 0;
-        int tsel = 0;
-        for (int t = 1; t <= tmax; ++t) {
-            run += (long long)s_bins[t - 1];
-            if (!tsel && run >= (long long)L) { tsel = t; cap = run; }
+    if (wv == 0) {   // lane t - 1: capacity(t) = bins 0..t-1; T = the first t with capacity >= L
+        const uint32_t run = wave_incl_dpp(lane < tmax ? s_bins[lane] : 0u);   // <= 4 x items: no overflow
+        const u64 hit = __ballot(lane < tmax && run >= L);
+        const int tsel = hit ? (int)__builtin_ctzll(hit) + 1 : 0;
+        const uint32_t cap = (uint32_t)__builtin_amdgcn_readlane((int)run, (tsel ? tsel : tmax) - 1);
+        if (lane == 0) {
+            s_T = tsel ? tsel : tmax;
+            s_cap = cap;   // the exact capacity at T over the whole slice
+            if (t_out) t_out[b] = s_T;
         }
-        s_T = tsel ? tsel : tmax;
-        s_cap = (uint32_t)(tsel ? cap : run);   // the exact capacity at T over the whole slice
-        if (t_out) t_out[b] = s_T;
     }
     lds_barrier();
     const int Tthr = s_T;
