@@ -2217,6 +2217,131 @@ __global__ __launch_bounds__(1024) void k_restore_ss(const T* __restrict__ stego
     }
 }
 
+// Inline variant of k_restore_ss (round 3): the same register-ring copy of one slice per
+// 1024-thread workgroup, but the window hull is restored and the payload gathered in the
+// stream, from the vectors already in registers: the slice's location map is staged in LDS
+// first, a vector inside the hull XORs its map bits back (LDS reads only, so the ring's loads
+// and stores stay straight-line and hipcc's vmcnt counting exact) and ORs its payload bits into
+// an LDS buffer.  No gather before the copy (its loads queued behind the ring's), no hull
+// pass after it (a full vmcnt(0) drain, then a dependent load + store).  Bits as gather_body:
+// bit j = stego bit p of the j-th window pixel in segment order, j = cat[p] + (q - off[p]) mod npx.
+#define RIL_WORDS 4096   // 32-bit LDS words each for the map and the payload (host-checked)
+template <typename T, bool NT, int D, int G>
+__global__ __launch_bounds__(1024) void k_restore_il(const T* __restrict__ stego, T* __restrict__ cover, uint32_t npx,
+                                                     const codec_slice_meta* __restrict__ meta,
+                                                     const u64* __restrict__ maps_all, int mw,
+                                                     u64* __restrict__ payload_out, int pw) {
+    typedef typename Vec8<T>::type V;
+    __shared__ uint32_t s_map[RIL_WORDS], s_pay[RIL_WORDS];
+    __shared__ int s_n[16], s_off[16], s_cat[16];
+    const int b = blockIdx.x;
+    const uint32_t t = threadIdx.x;
+    const uint32_t nv = npx / 8;   // a multiple of 1024 * D * G (host check)
+    const codec_slice_meta* M = meta + b;
+    // the slice's windows and location map first: their loads are ahead of the ring's
+    const int s = M->s;
+    const uint32_t lo = (uint32_t)M->span_lo, len = (uint32_t)M->span_len;
+    if (t < 16) {
+        const bool on = (int)t < s;
+        s_n[t] = on ? M->n[t] : 0;
+        s_off[t] = on ? M->off[t] : 0;
+        s_cat[t] = on ? M->cat[t] : 0;
+    }
+    const u64* maps = maps_all + (size_t)b * mw;
+    for (uint32_t w = t; w < (uint32_t)mw; w += 1024u) {
+        const u64 m = maps[w];
+        s_map[2 * w] = (uint32_t)m;
+        s_map[2 * w + 1] = (uint32_t)(m >> 32);
+    }
+    if (payload_out)
+        for (uint32_t w = t; w < 2u * (uint32_t)pw; w += 1024u) s_pay[w] = 0u;
+    const V* src = reinterpret_cast<const V*>(stego + (size_t)b * npx);
+    V* dst = reinterpret_cast<V*>(cover + (size_t)b * npx);
+    V r[D][G];
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int g = 0; g < G; ++g) r[d][g] = ldv<NT>(src + (uint32_t)(d * G + g) * 1024u + t);
+    lds_barrier();
+    const uint32_t hi = lo + len;   // <= 2 npx - 1 < 2^32
+    const bool wrap = len > 0 && hi > npx;
+    // a vector (8 pixels from q0) inside the hull: per plane, its in-window pixels form one run
+    // [e0, e1) whose bits j0 .. j0 + (e1 - e0) - 1 are consecutive in the map and the payload
+    auto fix = [&](V& v, uint32_t q0) {
+        uint32_t px[8];
+        if constexpr (sizeof(T) == 2) {
+            px[0] = v.x & 0xFFFFu; px[1] = v.x >> 16; px[2] = v.y & 0xFFFFu; px[3] = v.y >> 16;
+            px[4] = v.z & 0xFFFFu; px[5] = v.z >> 16; px[6] = v.w & 0xFFFFu; px[7] = v.w >> 16;
+        } else {
+            for (int e = 0; e < 4; ++e) { px[e] = (v.x >> (8 * e)) & 0xFFu; px[4 + e] = (v.y >> (8 * e)) & 0xFFu; }
+        }
+        for (int p = 0; p < s; ++p) {
+            const int n = s_n[p];
+            if (n <= 0) continue;
+            int i0 = (int)q0 - s_off[p];   // window index of pixel e = i0 + e (mod npx)
+            if (i0 < -7) i0 += (int)npx;
+            int e0 = 8, e1 = 0;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                int i = i0 + e;
+                if (i < 0) i += (int)npx;
+                if (i < n) { e0 = min(e0, e); e1 = e + 1; }
+            }
+            if (e0 >= e1) continue;
+            int ia = i0 + e0;
+            if (ia < 0) ia += (int)npx;
+            const uint32_t j0 = (uint32_t)(s_cat[p] + ia);
+            const uint32_t wd = j0 >> 5, sh = j0 & 31u;
+            const uint32_t mf = __builtin_amdgcn_alignbit(s_map[min(wd + 1, (uint32_t)RIL_WORDS - 1)], s_map[wd], sh);
+            uint32_t bits = 0;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                if (e < e0 || e >= e1) continue;
+                bits |= ((px[e] >> p) & 1u) << (e - e0);
+                px[e] ^= ((mf >> (e - e0)) & 1u) << p;
+            }
+            if (payload_out && bits) {
+                atomicOr(&s_pay[wd], bits << sh);
+                if (sh + (uint32_t)(e1 - e0) > 32u) atomicOr(&s_pay[wd + 1], bits >> (32u - sh));
+            }
+        }
+        if constexpr (sizeof(T) == 2) {
+            v.x = px[0] | (px[1] << 16); v.y = px[2] | (px[3] << 16);
+            v.z = px[4] | (px[5] << 16); v.w = px[6] | (px[7] << 16);
+        } else {
+            v.x = px[0] | (px[1] << 8) | (px[2] << 16) | (px[3] << 24);
+            v.y = px[4] | (px[5] << 8) | (px[6] << 16) | (px[7] << 24);
+        }
+    };
+    auto put = [&](uint32_t idx, V& v) {
+        const uint32_t q0 = idx * 8u;
+        if (len > 0 && ((q0 + 8u > lo && q0 < hi) || (wrap && q0 < hi - npx))) fix(v, q0);
+        stv<NT>(dst + idx, v);
+    };
+    const uint32_t step = 1024u * D * G;
+    uint32_t base = 0;
+    for (; base + step < nv; base += step) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const uint32_t idx = base + (uint32_t)(d * G + g) * 1024u + t;
+                put(idx, r[d][g]);
+                r[d][g] = ldv<NT>(src + idx + step);   // refill from the next group
+            }
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int g = 0; g < G; ++g) put(base + (uint32_t)(d * G + g) * 1024u + t, r[d][g]);
+    if (payload_out) {
+        lds_barrier();   // every payload OR done
+        for (uint32_t w = t; w < (uint32_t)pw; w += 1024u)
+            payload_out[(size_t)b * pw + w] = (u64)s_pay[2 * w] | ((u64)s_pay[2 * w + 1] << 32);
+    }
+}
+
 // scalar variant for slices whose rows are not 8-pixel aligned
 template <typename T>
 __global__ __launch_bounds__(256) void k_restore_scalar(const T* __restrict__ stego, T* __restrict__ cover,
@@ -2893,7 +3018,23 @@ int codec_extract(const codec_params* P, const void* stego, const uint64_t* maps
                 static_cast<const TT*>(stego), static_cast<TT*>(cover_out), (uint32_t)npx, meta, mp, P->map_words, po, \
                 P->payload_words, glate)
             const int glate = (int)knob("CODEC_RESTORE_SS_GLATE", 0);   // payload gather after the copy (A/B)
-            if (P->in_bytes == 2 && ntg && dep == 16 && npx % 131072 == 0) RSS(uint16_t, true, 8);
+            // inline hull restore + gather (k_restore_il) where the map and payload fit its LDS
+            // buffers; CODEC_RESTORE_IL=0 for the copy-then-hull kernel
+            const bool il = knob("CODEC_RESTORE_IL", 1) != 0 && 2LL * P->map_words <= RIL_WORDS &&
+                            (!payload_out || 2LL * P->payload_words <= RIL_WORDS) && dep == 8 && !glate;
+#define RIL(TT, NTV, DD) hipLaunchKernelGGL((k_restore_il<TT, NTV, DD, 2>), dim3((unsigned)P->B), dim3(1024), 0, st, \
+                static_cast<const TT*>(stego), static_cast<TT*>(cover_out), (uint32_t)npx, meta, mp, P->map_words, po, \
+                P->payload_words)
+            // vectors in flight per thread (A/B knob CODEC_RESTORE_IL_DEPTH: 4, 8 or 16)
+            const long long idep = knob("CODEC_RESTORE_IL_DEPTH", 8);
+            if (il) {
+                if (P->in_bytes == 2 && ntg && idep == 16 && npx % 131072 == 0) RIL(uint16_t, true, 8);
+                else if (P->in_bytes == 2 && ntg && idep == 4 && npx % 32768 == 0) RIL(uint16_t, true, 2);
+                else if (P->in_bytes == 2) { if (ntg) RIL(uint16_t, true, 4); else RIL(uint16_t, false, 4); }
+                else { if (ntg) RIL(uint8_t, true, 4); else RIL(uint8_t, false, 4); }
+            }
+#undef RIL
+            else if (P->in_bytes == 2 && ntg && dep == 16 && npx % 131072 == 0) RSS(uint16_t, true, 8);
             else if (P->in_bytes == 2 && ntg && dep == 4 && npx % 32768 == 0) RSS(uint16_t, true, 2);
             else if (P->in_bytes == 2) { if (ntg) RSS(uint16_t, true, 4); else RSS(uint16_t, false, 4); }
             else { if (ntg) RSS(uint8_t, true, 4); else RSS(uint8_t, false, 4); }

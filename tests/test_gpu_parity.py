@@ -364,15 +364,19 @@ def test_workspace_reuse_stays_clean(dtype, kinds, monkeypatch):
             np.testing.assert_array_equal(stego[i], exp["stego"])
 
 
-@pytest.mark.parametrize("restore", ["ss", "ss_d4", "ss_d16", "ss_late", "gs"])
+@pytest.mark.parametrize("restore", ["ss", "ss_copy_hull", "ss_d4", "ss_d16", "ss_late", "gs"])
 @pytest.mark.parametrize("kind,h,w,bsz,chars", [("ct12", 512, 512, 5, 1024), ("u8", 256, 256, 3, 2500),
                                                 ("u16", 256, 512, 2, 4000), ("ct12", 256, 256, 4, 3000)])
 def test_restore_paths_vs_oracle(kind, h, w, bsz, chars, restore, monkeypatch):
-    """codec_extract's out-of-place restore through the slice-serial pass (k_restore_ss: ring
-    copy + window-hull rewrite + fused payload gather; forced here, the default for batches of
-    >= one slice per CU) and the grid-stride pass: payload bits and restored cover exact,
-    stego vs the oracle; long payloads make windows wrap past the slice end."""
+    """codec_extract's out-of-place restore through the slice-serial pass (forced here, the
+    default for batches of >= one slice per CU) -- "ss": k_restore_il (ring copy with the hull
+    restored and the payload gathered inline from LDS-staged maps), "ss_copy_hull" and the
+    depth / late-gather variants: k_restore_ss (ring copy, then the window-hull rewrite; gather
+    first or last) -- and the grid-stride pass: payload bits and restored cover exact, stego vs
+    the oracle; long payloads make windows wrap past the slice end."""
     monkeypatch.setenv("CODEC_RESTORE_SS", "0" if restore == "gs" else "1")
+    if restore == "ss_copy_hull":
+        monkeypatch.setenv("CODEC_RESTORE_IL", "0")
     if restore in ("ss_d4", "ss_d16"):   # ring depths other than the default 8 vectors per thread
         monkeypatch.setenv("CODEC_RESTORE_SS_DEPTH", restore[4:])
     if restore == "ss_late":             # payload gather after the copy instead of before it
