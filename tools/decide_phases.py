@@ -22,7 +22,7 @@ def main():
     from codec_tcc_amd import synth
     kind = sys.argv[1] if len(sys.argv) > 1 else "ct12"
     B = int(os.environ.get("DTS_B", "64"))
-    H = W = 2048
+    H = W = int(os.environ.get("DTS_SIZE", "2048"))
     dev = torch.device("cuda", 0)
     covers = bench.make_covers(torch, kind, B, H, W, dev, 0)
     codec = ct.Codec(B, H, W, dtype="uint16", device=dev)
@@ -67,6 +67,10 @@ def main():
     for n, v in zip(names, med):
         print(f"  {n:16s} {v:8.0f} ticks = {v * 0.01:7.2f} us")
     print(f"  total            {np.median(t[:, -1] - t[:, 0]) * 0.01:7.2f} us")
+    t00 = t[:, 0].min()
+    print("slices' entry stamps: median %.2f, max %.2f us after the first; last decision done %.2f us, last embed "
+          "done %.2f us after the first entry" % (np.median(t[:, 0] - t00) * 0.01, (t[:, 0].max() - t00) * 0.01,
+                                                  (t[:, -1].max() - t00) * 0.01, (raw[:, 11].max() - t00) * 0.01))
     print("embed (fused): load_win %.2f us, embed loop %.2f us" % (np.median(raw[:, 10] - raw[:, 5]) * 0.01,
                                                                 np.median(raw[:, 11] - raw[:, 10]) * 0.01))
 
