@@ -1039,6 +1039,9 @@ struct ExtractCount {
 #ifndef LB_WIN
 #define LB_WIN 4
 #endif
+#ifndef PEE_LB_PARTIAL
+#define PEE_LB_PARTIAL 1   // embed: a partial sum of the published words may end the wait (past `end`)
+#endif
 template <typename F>
 __device__ uint32_t lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, uint32_t spin_max, const F& count,
                                  uint32_t* done = nullptr, uint32_t sat = 0) {
@@ -1066,6 +1069,15 @@ __device__ uint32_t lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, 
             const u64 need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);  // lanes 0..first
             if (notready & need) {
                 if (done && ld_agent(done)) return sat;
+                if (done && (PEE_LB_PARTIAL)) {
+                    // the published words already bound the prefix from below (aggregates of
+                    // disjoint chunks, or an inclusive prefix): reaching `sat` (= L) places this
+                    // chunk past `end` without waiting for the missing ones
+                    uint32_t lo = (lane <= first && fl != 0u) ? (uint32_t)w : 0u;
+#pragma unroll
+                    for (int o = 32; o >= 1; o >>= 1) lo += __shfl_xor(lo, o, 64);
+                    if (excl + lo >= sat) return excl + lo;
+                }
                 if (++spins <= spin_max) {
                     __builtin_amdgcn_s_sleep(PEE_LB_SLEEP);
                     p = pr;                  // reload from this window
