@@ -499,7 +499,8 @@ def bench_lsb(args, torch, dist, world, rank, dev, covers, B, H, W, *, exchange=
                               "kernels_only_value": round(B * H * W * world / t_k / 1e6, 1)}
     kern = _profile(_lib.load(), _lib, kernels, steps) if not args.no_profile else {}
     res["kernels_ms"] = {k: round(v, 4) for k, v in kern.items()}
-    sk = next((k for k in ("k_scan_rows", "k_scan_fast") if k in kern), None)
+    # the copying scan (fused with the decision and embed at C3-like shapes: k_scan_decide)
+    sk = next((k for k in ("k_scan_rows", "k_scan_fast", "k_scan_decide") if k in kern), None)
     if sk:   # read cover + write stego (uint16)
         res["roofline"] = _roof(sk, B * H * W * 4, kern[sk], pmc_traffic(sk, B, H, W, kind))
     res["_stego"] = stego

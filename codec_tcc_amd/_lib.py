@@ -107,7 +107,7 @@ KERNEL_TAGS = {1: "k_scan_fast", 2: "k_scan_generic", 3: "k_block_exact", 4: "k_
                15: "k_pee_embed1", 16: "k_pee_extract1", 17: "k_scan_read", 18: "k_unxor",
                19: "k_scan_rows", 20: "k_scan_rows_read", 21: "k_quality", 22: "k_decide_embed",
                23: "k_pee_capacity", 24: "k_pee_embed_ss", 25: "k_pee_extract_ss",
-               26: "k_pee_embed_ss_auto", 27: "k_pee_embed_res"}
+               26: "k_pee_embed_ss_auto", 27: "k_pee_embed_res", 28: "k_scan_decide"}
 EXPORTS = tuple(_SIGS)
 
 _lib = None

@@ -586,7 +586,7 @@ __device__ __noinline__ void hist16_fix(uint32_t* ghist, uint32_t v, uint32_t cn
 // their returned values are checked for 16-bit wraps only afterwards, so the adds
 // pipeline instead of each waiting for its return.
 template <typename T, typename V>
-__device__ __forceinline__ void hist_add8(uint32_t* lds, uint32_t* ghist, const V& vec) {
+__device__ __forceinline__ void hist_add8(uint32_t* lds, uint32_t* ghist, const V& vec, uint32_t* wrapf = nullptr) {
     uint32_t px[8];
     if constexpr (sizeof(T) == 2) {
         px[0] = vec.x & 0xFFFFu; px[1] = vec.x >> 16; px[2] = vec.y & 0xFFFFu; px[3] = vec.y >> 16;
@@ -618,6 +618,7 @@ __device__ __forceinline__ void hist_add8(uint32_t* lds, uint32_t* ghist, const 
             wrap |= (field + cnt[k]) > 0xFFFFu;
         }
         if (wrap) {
+            if (wrapf) *wrapf = 1u;   // fused scan: the slice's counts are no longer all in LDS
 #pragma unroll
             for (int k = 0; k < 8; ++k)
                 if (cnt[k]) hist16_fix(ghist, px[k], cnt[k], old[k]);
@@ -775,8 +776,20 @@ __global__ __launch_bounds__(1024) void k_scan_read(const T* __restrict__ cover,
 // kernel 0.800 ms, no histogram 0.762, bare region copy 0.757 -- the histogram, block
 // counts and key costs 5 % over the copy in this order.  U (vectors per thread per
 // iteration) = 4; U = 2 or 8 (pipelined or not) measured 0.83-0.84 ms.
-template <typename T, int SB, bool NT, bool STORE, int DIAG = 0, bool PIPE = true, int U = 4>
-__device__ __forceinline__ void scan_rows_body(const T* __restrict__ cover, T* __restrict__ stego,
+// k_scan_rows' LDS (a struct so that k_scan_decide can overlay k_decide's on it); `wor` and
+// `wrap` serve the fused kernel only: the workgroup's OR of pixels and "a 16-bit field wrapped"
+template <typename T>
+struct ScanRowsSmem {
+    uint32_t lds[HistCfg<T>::kLdsWords];
+    uint32_t cnt[SCAN_ROWS_CNT_WORDS];
+    u64 wkey;
+    uint32_t wor, wrap;
+};
+
+// FUSED (k_scan_decide: the workgroup is its slice's only one): no histogram flush, and the
+// OR word and block key stay in LDS for the decision that follows in the same workgroup
+template <typename T, int SB, bool NT, bool STORE, int DIAG = 0, bool PIPE = true, int U = 4, bool FUSED = false>
+__device__ __forceinline__ void scan_rows_body(ScanRowsSmem<T>& SS, const T* __restrict__ cover, T* __restrict__ stego,
                                                int H, int W, int bands_per_wg,
                                                uint32_t* __restrict__ ghist_all,
                                                u64* __restrict__ gkey, uint32_t* __restrict__ gor) {
@@ -786,9 +799,9 @@ __device__ __forceinline__ void scan_rows_body(const T* __restrict__ cover, T* _
     constexpr int LSB_ = SB == 8 ? 3 : SB == 16 ? 4 : SB == 32 ? 5 : 6;
     constexpr uint32_t NPB = (uint32_t)SB * SB;
     constexpr int NT_ = 1024;
-    __shared__ uint32_t lds[HistCfg<T>::kLdsWords];
-    __shared__ uint32_t cnt[SCAN_ROWS_CNT_WORDS];
-    __shared__ u64 wkey;
+    uint32_t* lds = SS.lds;
+    uint32_t* cnt = SS.cnt;
+    u64& wkey = SS.wkey;
     const int b = blockIdx.y;
     const size_t npx = (size_t)H * W;
     const T* src = cover + (size_t)b * npx;
@@ -805,7 +818,7 @@ __device__ __forceinline__ void scan_rows_body(const T* __restrict__ cover, T* _
     const int nfull = max(0, fb1 - band0) * fullbx;        // host guarantees nfull <= 2*CNT_WORDS
     for (int i = threadIdx.x; i < HistCfg<T>::kLdsWords; i += NT_) lds[i] = 0;
     for (int i = threadIdx.x; i < (nfull + 1) / 2; i += NT_) cnt[i] = 0;
-    if (threadIdx.x == 0) wkey = 0;
+    if (threadIdx.x == 0) { wkey = 0; SS.wor = 0u; SS.wrap = 0u; }
     __syncthreads();
 
     const long long nvec = (long long)max(0, row1 - row0) * CR;
@@ -888,7 +901,7 @@ __device__ __forceinline__ void scan_rows_body(const T* __restrict__ cover, T* _
             const bool ok = whole || i < nvec;
             if (DIAG == 4) { vor ^= v[u].x; continue; }
             if (DIAG == 0)
-                if (ok) hist_add8<T>(lds, ghist, v[u]);
+                if (ok) hist_add8<T>(lds, ghist, v[u], FUSED ? &SS.wrap : nullptr);
         }
     };
     const long long step = (long long)NT_ * U;
@@ -931,7 +944,10 @@ __device__ __forceinline__ void scan_rows_body(const T* __restrict__ cover, T* _
     else vor = (vor | (vor >> 8) | (vor >> 16) | (vor >> 24)) & 0xFFu;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) vor |= __shfl_xor(vor, o, 64);
-    if (lane == 0 && vor) atomicOr(&gor[b], vor);
+    if (lane == 0 && vor) {
+        if constexpr (FUSED) atomicOr(&SS.wor, vor);
+        else atomicOr(&gor[b], vor);
+    }
     __syncthreads();
     // block keys: score c(n-c) (exact variance numerator of a full pow2 block), first
     // maximal block in raster order wins (~index in the low word)
@@ -950,9 +966,9 @@ __device__ __forceinline__ void scan_rows_body(const T* __restrict__ cover, T* _
         best = best > other ? best : other;
     }
     if (lane == 0 && best) atomicMax(&wkey, best);
-    if (DIAG == 0) hist_flush<T>(lds, ghist);
+    if (DIAG == 0 && !FUSED) hist_flush<T>(lds, ghist);
     __syncthreads();
-    if (threadIdx.x == 0 && wkey) atomicMax(&gkey[b], wkey);
+    if (!FUSED && threadIdx.x == 0 && wkey) atomicMax(&gkey[b], wkey);
 }
 
 template <typename T, int SB, bool NT, bool STORE, int DIAG = 0, bool PIPE = true, int U = 4>
@@ -960,7 +976,8 @@ __global__ __launch_bounds__(1024) void k_scan_rows(const T* __restrict__ cover,
                                                     int H, int W, int bands_per_wg,
                                                     uint32_t* __restrict__ ghist_all,
                                                     u64* __restrict__ gkey, uint32_t* __restrict__ gor) {
-    scan_rows_body<T, SB, NT, STORE, DIAG, PIPE, U>(cover, stego, H, W, bands_per_wg, ghist_all, gkey, gor);
+    __shared__ ScanRowsSmem<T> SS;
+    scan_rows_body<T, SB, NT, STORE, DIAG, PIPE, U>(SS, cover, stego, H, W, bands_per_wg, ghist_all, gkey, gor);
 }
 
 // ------------------------------------------------------------------ K1': scan + copy (generic)
@@ -1189,41 +1206,78 @@ struct EmbedArgs {
     uint32_t keep;
 };
 
-template <typename T, bool EMBED = false>
-__global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __restrict__ ghist_all,
-                                                 uint32_t* __restrict__ gor, double* __restrict__ gterms,
-                                                 u64* __restrict__ gkey, const double* __restrict__ exact,
-                                                 int exact_cap, int exact_edge_only, int fast_blocks,
-                                                 const double* __restrict__ lut, long long lut_len,
-                                                 const codec_layout* __restrict__ table,
-                                                 const int32_t* __restrict__ slice_class,
-                                                 codec_slice_meta* __restrict__ meta_all, EmbedArgs E,
-                                                 u64* __restrict__ plane_slots, int nsplit, uint32_t spin_max,
-                                                 int dbg_late) {
-    constexpr int R = HistCfg<T>::kBins;
+// k_decide's LDS, one struct so that the fused scan + decision kernel (k_scan_decide) can
+// overlay it on the scan's (a union: `list` over the histogram, `vals` over the block counters)
+template <typename T, bool EMBED>
+struct DecideSmem {
+    static constexpr int R = HistCfg<T>::kBins;
+    static constexpr bool kWideT = sizeof(T) == 2;
     // `list` doubles as the wave-parallel path's arena: terms (8m B), rank -> value (2m B),
     // one joint-order list per plane in flight (2m B each)
-    __shared__ __align__(16) uint16_t list[R];
-    __shared__ double vals[sizeof(T) == 2 ? 2048 : 1024];   // 2048: the walk path's two orders
-    __shared__ uint32_t sh[20];
-    __shared__ u64 sh64[17];
-    __shared__ uint32_t pops_sh[16];
-    __shared__ double mis_sh[16];
-    __shared__ double best_sc[16];
-    __shared__ int best_ix[16];
-    __shared__ double hxy_sh[16], hx_sh[16], hy_sh;
-    __shared__ int ctl_sh[4];
+    __align__(16) uint16_t list[R];
+    double vals[sizeof(T) == 2 ? 2048 : 1024];   // 2048: the walk path's two orders
+    uint32_t sh[20];
+    u64 sh64[17];
+    uint32_t pops_sh[16];
+    double mis_sh[16];
+    double best_sc[16];
+    int best_ix[16];
+    double hxy_sh[16], hx_sh[16], hy_sh;
+    int ctl_sh[4];
     // walk path (wide 16-bit slices): non-zero masks per 64-bin group, terms by count
-    constexpr bool kWideT = sizeof(T) == 2;
-    __shared__ u64 nzs[kWideT ? R / 64 : 1];
-    __shared__ double tcs[kWideT ? kTermCodes : 1];
+    u64 nzs[kWideT ? R / 64 : 1];
+    double tcs[kWideT ? kTermCodes : 1];
+    u64 pay_sh[EMBED ? 256 : 1];
+    u64 slot_sh[16];
+    int slot_to;
+    int32_t lay_sh[sizeof(codec_layout) / 4];
+    SliceWin Wsh;
+    int seg_end[16], seg_p[16], seg_q0[16], seg_s0[16];
+};
 
-    const int b = blockIdx.x;
+// what the fused kernel hands the decision: the slice's OR word and block key, and -- when the
+// slice's counts fit (no 16-bit field wrapped, values < 4096) -- its histogram in the scan's
+// LDS (16-bit halves), read by pass 1 instead of the global histogram
+struct FusedScan {
+    const uint32_t* lds;
+    uint32_t orv;
+    u64 key;
+    bool lds_ok;
+};
+
+template <typename T, bool EMBED>
+__device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const FusedScan* fz, const int b, const int role,
+                                            codec_params P,
+                                            uint32_t* __restrict__ ghist_all, uint32_t* __restrict__ gor,
+                                            double* __restrict__ gterms, u64* __restrict__ gkey,
+                                            const double* __restrict__ exact, int exact_cap, int exact_edge_only,
+                                            int fast_blocks, const double* __restrict__ lut, long long lut_len,
+                                            const codec_layout* __restrict__ table,
+                                            const int32_t* __restrict__ slice_class,
+                                            codec_slice_meta* __restrict__ meta_all, EmbedArgs E,
+                                            u64* __restrict__ plane_slots, int nsplit, uint32_t spin_max,
+                                            int dbg_late) {
+    constexpr int R = HistCfg<T>::kBins;
+    auto& list = S.list;
+    auto& vals = S.vals;
+    auto& sh = S.sh;
+    auto& sh64 = S.sh64;
+    auto& pops_sh = S.pops_sh;
+    auto& mis_sh = S.mis_sh;
+    auto& best_sc = S.best_sc;
+    auto& best_ix = S.best_ix;
+    auto& hxy_sh = S.hxy_sh;
+    auto& hx_sh = S.hx_sh;
+    double& hy_sh = S.hy_sh;
+    auto& ctl_sh = S.ctl_sh;
+    constexpr bool kWideT = sizeof(T) == 2;
+    auto& nzs = S.nzs;
+    auto& tcs = S.tcs;
+
     const int t = threadIdx.x;
     // split decision (small batches, nsplit > 0): blockIdx.y = 0 is the slice's main
     // workgroup; blockIdx.y = 1 + i computes plane i's joint entropy on its own CU and
     // publishes it in plane_slots[16 b + i] (see the plane branch below)
-    const int role = blockIdx.y;
     const uint32_t* hist = ghist_all + (size_t)b * R;
     double* terms = gterms + (size_t)b * R;
     const long long npx = (long long)P.H * P.W;
@@ -1233,7 +1287,8 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
     DTS(0);
     if (role > 0) PTS(0);
     // the scan's block key, loaded now (used by the offset argmax after the decision)
-    const u64 key0 = (t == 0 && role == 0 && fast_blocks && P.fixed_offset < 0 && P.mode == CODEC_MODE_HYBRID) ? gkey[b] : 0ull;
+    const bool keyed = t == 0 && role == 0 && fast_blocks && P.fixed_offset < 0 && P.mode == CODEC_MODE_HYBRID;
+    const u64 key0 = keyed ? (fz ? fz->key : gkey[b]) : 0ull;
     // the slice's layout class (its layout for s is loaded once s is known)
     constexpr int kLayW = (int)(sizeof(codec_layout) / 4);
     static_assert(16 * kLayW <= 1024, "one int of the class's layouts per thread");
@@ -1242,13 +1297,15 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
     // fused embed: the slice's payload words (<= 2 KiB) go to LDS now, read by the embed
     // loop after the decision instead of one dependent global load per bit
     constexpr int kPaySh = EMBED ? 256 : 1;
-    __shared__ u64 pay_sh[kPaySh];
+    auto& pay_sh = S.pay_sh;
     const bool pay_in_lds = EMBED && E.pw <= kPaySh;
     if (EMBED && pay_in_lds && role == 0)
         for (int w = t; w < E.pw; w += 1024) pay_sh[w] = E.payload[(size_t)b * E.pw + w];
     // ---- bins that can be non-zero: [0, Rp), Rp = next power of two above OR(pixels)
-    const uint32_t orv = gor[b];
+    const uint32_t orv = fz ? fz->orv : gor[b];
     int Rp = orv ? (1 << (32 - __clz((int)orv))) : 1;
+    // fused (k_scan_decide): pass 1 reads the counts from the scan's LDS histogram
+    const uint32_t* flds = (fz && fz->lds_ok) ? fz->lds : nullptr;
     if (Rp > R) Rp = R;
     const int bpt = Rp > 1024 ? Rp / 1024 : 1;     // <= 64 bins per thread
     const int v0 = t * bpt;
@@ -1308,7 +1365,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
 #pragma unroll
         for (int u = 0; u < 16; ++u) {            // 16 loads in flight, then the adds
             const int v = v0 + k0 + u;
-            cc[u] = (k0 + u < bpt && v < Rp) ? hist[v] : 0u;
+            cc[u] = (k0 + u < bpt && v < Rp) ? (flds ? (flds[v >> 1] >> (16 * (v & 1))) & 0xFFFFu : hist[v]) : 0u;
         }
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
@@ -1433,8 +1490,8 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
     // the histogram this workgroup clears at the end); the slots are cleared for the next
     // call at the end, with the histogram (a store here would be waited for by the next
     // vmcnt wait of the wave, ~2 us)
-    __shared__ u64 slot_sh[16];
-    __shared__ int slot_to;
+    auto& slot_sh = S.slot_sh;
+    int& slot_to = S.slot_to;
     bool collected = false;
     bool abandoned = false;   // thread t < nsplit: slot t was given up (the late writer clears it)
     auto collect = [&]() {
@@ -1735,7 +1792,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
 
     // the slice's segment layout for its s (64 ints), loaded by one wave in one round trip
     // while the offset is found, instead of thread 0's dependent loads in the windows loop
-    __shared__ int32_t lay_sh[kLayW];
+    auto& lay_sh = S.lay_sh;
     if (t == 0) ctl_sh[1] = s;
     __syncthreads();
     {
@@ -1747,10 +1804,13 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
     DTS(3);
     if (!offset_done) find_offset();
 
-    __shared__ SliceWin Wsh;   // the fused embed's window cache, filled by thread 0 below
+    SliceWin& Wsh = S.Wsh;   // the fused embed's window cache, filled by thread 0 below
     // ... and its segments in perm order: bit j belongs to the first k with j < seg_end[k];
     // pixel = seg_q0[k] + j (mod npx), payload bit = seg_s0[k] + j
-    __shared__ int seg_end[16], seg_p[16], seg_q0[16], seg_s0[16];
+    auto& seg_end = S.seg_end;
+    auto& seg_p = S.seg_p;
+    auto& seg_q0 = S.seg_q0;
+    auto& seg_s0 = S.seg_s0;
     __syncthreads();   // lay_sh
     DTS(4);
     if (t < 64) {   // ---- windows and the slice record (wave 0: lane j = segment j in perm order)
@@ -1889,7 +1949,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
     // slice's block key and OR word.  All reads of them precede this barrier.
     __syncthreads();
     if (t < nsplit && !abandoned) plane_slots[16 * (size_t)b + t] = 0ull;
-    {
+    if (!flds) {   // fused with the LDS histogram: the global one was never written
         const int zr = Rp < 2 ? 2 : Rp;
         uint32_t* hz = ghist_all + (size_t)b * R;
         if ((zr & 3) == 0) {
@@ -1898,8 +1958,65 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
         } else {
             for (int v = t; v < zr; v += 1024) hz[v] = 0u;
         }
-        if (t == 0) { gkey[b] = 0ull; gor[b] = 0u; }
     }
+    if (t == 0) { gkey[b] = 0ull; gor[b] = 0u; }
+}
+
+template <typename T, bool EMBED = false>
+__global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __restrict__ ghist_all,
+                                                 uint32_t* __restrict__ gor, double* __restrict__ gterms,
+                                                 u64* __restrict__ gkey, const double* __restrict__ exact,
+                                                 int exact_cap, int exact_edge_only, int fast_blocks,
+                                                 const double* __restrict__ lut, long long lut_len,
+                                                 const codec_layout* __restrict__ table,
+                                                 const int32_t* __restrict__ slice_class,
+                                                 codec_slice_meta* __restrict__ meta_all, EmbedArgs E,
+                                                 u64* __restrict__ plane_slots, int nsplit, uint32_t spin_max,
+                                                 int dbg_late) {
+    __shared__ DecideSmem<T, EMBED> S;
+    decide_body<T, EMBED>(S, nullptr, (int)blockIdx.x, (int)blockIdx.y, P, ghist_all, gor, gterms, gkey, exact, exact_cap, exact_edge_only, fast_blocks,
+                          lut, lut_len, table, slice_class, meta_all, E, plane_slots, nsplit, spin_max, dbg_late);
+}
+
+// ------------------------------------------------------------------ K1 + K3 fused: scan + decide
+// For batches whose slices each fit one scan workgroup (C3's 256 x 512^2: the row sweep runs one
+// workgroup per slice anyway) the workgroup that scanned slice b decides it too, with codec_encode's
+// embed, in the same launch: the histogram is still in its LDS (read by pass 1 instead of a global
+// flush + reload), there is no kernel boundary, and each slice's decision starts as soon as its own
+// scan ends, overlapping other slices' streaming.  The two LDS layouts are overlaid (a union: the
+// decision's arena over the histogram, its `vals` over the block counters; both are dead by then).
+// A slice whose counts left LDS (a 16-bit field wrapped) or whose values reach 4096 and beyond
+// flushes the histogram to global memory as k_scan_rows would and decides from there.
+template <typename T, int SB, bool NT>
+__global__ __launch_bounds__(1024) void k_scan_decide(const T* __restrict__ cover, T* __restrict__ stego,
+                                                      int bands_per_wg, codec_params P, uint32_t* __restrict__ ghist_all,
+                                                      uint32_t* __restrict__ gor, double* __restrict__ gterms,
+                                                      u64* __restrict__ gkey, const double* __restrict__ exact,
+                                                      int exact_cap, int exact_edge_only, const double* __restrict__ lut,
+                                                      long long lut_len, const codec_layout* __restrict__ table,
+                                                      const int32_t* __restrict__ slice_class,
+                                                      codec_slice_meta* __restrict__ meta_all, EmbedArgs E) {
+    union FusedSmem {
+        ScanRowsSmem<T> s;
+        DecideSmem<T, true> d;
+    };
+    __shared__ FusedSmem U;
+    const int b = blockIdx.y;
+    scan_rows_body<T, SB, NT, true, 0, true, 4, true>(U.s, cover, stego, P.H, P.W, bands_per_wg, ghist_all, gkey, gor);
+    // scan_rows_body ended with a barrier after its last LDS write (the block key)
+    FusedScan fz;
+    fz.lds = U.s.lds;
+    fz.orv = U.s.wor;
+    fz.key = U.s.wkey;
+    const int Rp = fz.orv ? (1 << (32 - __clz((int)fz.orv))) : 1;
+    fz.lds_ok = sizeof(T) == 2 && U.s.wrap == 0u && Rp <= 4096;
+    if (!fz.lds_ok) {   // uniform: the global histogram path (wrap fix-ups are already there)
+        hist_flush<T>(U.s.lds, ghist_all + (size_t)b * HistCfg<T>::kBins);
+        __threadfence();
+    }
+    __syncthreads();   // every read of the scan's LDS words above precedes the decision's writes
+    decide_body<T, true>(U.d, &fz, b, 0, P, ghist_all, gor, gterms, gkey, exact, exact_cap, exact_edge_only, 1, lut,
+                         lut_len, table, slice_class, meta_all, E, nullptr, 0, 0u, -1);
 }
 
 // ------------------------------------------------------------------ K4: embed (window writes)
@@ -2862,6 +2979,31 @@ static int plan_impl(const codec_params* P, const void* cover, void* stego, cons
     if (stego == cover && P->in_bytes != P->out_bytes)
         return set_err(CODEC_EINVAL, "codec_plan: in place (stego == cover) needs one pixel dtype");
     const bool fast = use_fast_scan(P, cover, stego ? stego : cover);
+    const bool need_blocks0 = P->mode == CODEC_MODE_HYBRID && P->fixed_offset < 0;
+    // fused scan + decide (k_scan_decide): codec_encode out of place, uint16, 16x16 blocks, a
+    // chip-filling batch (or CODEC_FUSED_DECIDE=2) whose slices' block counters fit one scan
+    // workgroup and need no exact edge blocks
+    {
+        const long long fk = knob("CODEC_FUSED_DECIDE", 1);
+        const int nbands = (P->H + 15) / 16;
+        const bool shape_ok = E && fast && stego && stego != cover && P->in_bytes == 2 && P->out_bytes == 2 &&
+                              P->block == 16 && (long long)nbands * (P->W / 16) <= 2LL * SCAN_ROWS_CNT_WORDS &&
+                              (!need_blocks0 || host_exact_count(P, true) == 0);
+        if (fk != 0 && shape_ok && (fk == 2 || (long long)P->B >= device_cu_count())) {
+            codec_params Pv = *P;
+            Pv.reserved = (knob("CODEC_DECIDE_WAVES", 1) ? 0 : 1) | (knob("CODEC_DECIDE_WALK", 1) ? 0 : 2);
+            ProfScope prof(st, CODEC_K_SCAN_DECIDE);
+            const bool nt = knob("CODEC_NT", 1) != 0;
+#define SD(NTV) hipLaunchKernelGGL((k_scan_decide<uint16_t, 16, NTV>), dim3(1, P->B), dim3(1024), 0, st, \
+                static_cast<const uint16_t*>(cover), static_cast<uint16_t*>(stego), nbands, Pv, hist, orv, terms, keys, \
+                exact, L.exact_cap, 1, log2_lut, (long long)lut_len, table, slice_class, meta, *E)
+            if (nt) SD(true); else SD(false);
+#undef SD
+            const hipError_t ef = hipGetLastError();
+            if (ef != hipSuccess) return reclear(set_err(-(int)ef, "launch k_scan_decide: %s", hipGetErrorString(ef)));
+            return 0;
+        }
+    }
     if (fast) {
         // in place the stego copy is the cover itself: the scan only reads
         void* sdst = stego == cover ? nullptr : stego;

@@ -324,6 +324,7 @@ int codec_quality_moments(int32_t B, int32_t H, int32_t W, int32_t bytes, const 
 #define CODEC_K_PEE_EXTRACT_SS 25
 #define CODEC_K_PEE_EMBED_SS_AUTO 26
 #define CODEC_K_PEE_EMBED_RES 27   /* resident auto embed: slice read once, kept on the CU */
+#define CODEC_K_SCAN_DECIDE 28     /* fused scan + decide + embed (one workgroup per slice)  */
 int codec_profile_begin(int32_t capacity);
 /* after the stream has been synchronised: fills ms[i], tag[i] for the recorded pairs and
  * returns their count (closes the window and frees the events). */

@@ -31,13 +31,18 @@ def _run_case(case):
     return codec, enc
 
 
-@pytest.fixture(params=["split", "waves", "block"])
+@pytest.fixture(params=["split", "waves", "block", "fused"])
 def decide_path(request, monkeypatch):
     """k_decide's split decision (default for small batches: one plane workgroup per MI
     plane), its one-workgroup wave-parallel MI path (CODEC_DECIDE_SPLIT=0; the default for
     big batches when the joint orders fit in LDS) and the block-sequential one
     (CODEC_DECIDE_WAVES=0; also what large-m slices use).  The block variant also runs
-    codec_encode unfused (codec_plan then the separate k_embed launch)."""
+    codec_encode unfused (codec_plan then the separate k_embed launch).  "fused": the scan,
+    decision and embed in one launch (k_scan_decide, CODEC_FUSED_DECIDE=2 forces it on these
+    one-slice batches; cases it does not take -- uint8, other block sizes, edge blocks -- run
+    the separate kernels)."""
+    if request.param == "fused":
+        monkeypatch.setenv("CODEC_FUSED_DECIDE", "2")
     if request.param == "waves":
         monkeypatch.setenv("CODEC_DECIDE_SPLIT", "0")
     if request.param == "block":
