@@ -2247,7 +2247,6 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
     const uint32_t items = (uint32_t)(H / 2) * (uint32_t)CR;
     const int nc = (H / 2) * (W / 2);
     const int ntiles = (nc + PEE_TILE - 1) / PEE_TILE;
-    const uint32_t L = (uint32_t)max(0, lengths[b]);
     const size_t npx = (size_t)H * W;
     const uint16_t* src = cover + b * npx;
     uint16_t* dst = stego + b * npx;
@@ -2260,12 +2259,6 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
     uint32_t* s_re = pad + (PADW - (8 + NI) * NTH);   // LIN: kept error words [NI][NTH]
     const u64* payload = payload_all + (size_t)b * pw;
     u64* pay = reinterpret_cast<u64*>(pad);       // the slice's payload words
-    for (int u = 0; u < crow; ++u) cnt[u * NTH + tid] = 0u;
-    if (tid == 0) s_end = -1;
-    {   // the payload into LDS now (its loads overlap the read phase)
-        const int nw = min(pw, (int)((L + 63u) >> 6));
-        for (int w = tid; w < nw; w += NTH) pay[w] = payload[w];
-    }
     const uint32_t dq = NTH / (uint32_t)CR, dr = NTH % (uint32_t)CR;
     const uint32_t ostep = 2u * (uint32_t)W * dq + 8u * dr, owrap = 2u * (uint32_t)W - 8u * (uint32_t)CR;
     // LIN: item k of this lane at o_lin + k KS (the host checked dr == 0, items % NTH == 0)
@@ -2274,9 +2267,9 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
     // LIN: this lane's location-map half for item k (lanes 8j own one 32-bit half; others: sink)
     uint32_t* const lm_half = (lane & 7) == 0 ? reinterpret_cast<uint32_t*>(lm + (tid >> 4)) + ((lane >> 3) & 1) : sink_w;
     const uint32_t lm_step = (lane & 7) == 0 ? (NTH / 16) * 2 : 0u;   // 32-bit words per k
-    lds_barrier();   // counters zeroed before any lane adds
 
     // ---- read phase: every item once; even row -> stego now, odd row + errors kept
+    uint32_t L;   // the slice's payload bits: read once the first loads are out
     V r1[NI];
     uint32_t re[LIN ? 1 : NI];
     {
@@ -2306,6 +2299,18 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
         };
 #pragma unroll
         for (int k = 0; k < G && k < NI; ++k) issue(k);
+        // the slice's first loads go out before the setup below: the payload's copy into LDS
+        // is a dependent round trip (load -> LDS write -> barrier), and in front of them it
+        // held them back by one memory latency (C3 embed 0.0553 -> 0.0538 ms)
+        asm volatile("" ::: "memory");
+        L = (uint32_t)max(0, lengths[b]);
+        for (int u = 0; u < crow; ++u) cnt[u * NTH + tid] = 0u;
+        if (tid == 0) s_end = -1;
+        {   // the payload into LDS (read by the embed phase, after the barriers below)
+            const int nw = min(pw, (int)((L + 63u) >> 6));
+            for (int w = tid; w < nw; w += NTH) pay[w] = payload[w];
+        }
+        lds_barrier();   // counters zeroed before any lane adds
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
             // the next load goes out here and no earlier: left free, hipcc hoisted every load of
