@@ -770,6 +770,12 @@ __global__ __launch_bounds__(1024) void k_scan_read(const T* __restrict__ cover,
 // block of the region, pre-combined across the SB/8 lanes of a block row when W % SB == 0)
 // and are turned into argmax keys once the region is done.
 #define SCAN_ROWS_CNT_WORDS 7168   // 28 KiB of LDS = 14 336 block counters per workgroup
+// the region's first loads go out before the LDS zeroing (build-time A/B knob; 256 x 2048^2
+// k_scan_rows 0.7944 -> 0.7874 ms, profiles/r03/lockstep_ab.log).  A barrier per iteration
+// (waves in lockstep, as the restore wants) made the sweep slower: 0.79 -> 0.89 ms.
+#ifndef SCAN_EARLY_LOAD
+#define SCAN_EARLY_LOAD 1
+#endif
 // DIAG (timing diagnostics only, decisions are wrong): 1 = no histogram adds, 4 = copy with
 // the sweep's bookkeeping only, 5 = bare region copy (tools/ubench_stagger.hip's loop).
 // Measured in one process at 256 x 2048^2 (profiles/r01/ubench/scan_rows_diag.txt): full
@@ -816,14 +822,28 @@ __device__ __forceinline__ void scan_rows_body(ScanRowsSmem<T>& SS, const T* __r
     // full blocks of this region: bands [band0, min(band1, fullby)) x [0, fullbx)
     const int fb1 = min(fullby, band0 + bands_per_wg);
     const int nfull = max(0, fb1 - band0) * fullbx;        // host guarantees nfull <= 2*CNT_WORDS
-    for (int i = threadIdx.x; i < HistCfg<T>::kLdsWords; i += NT_) lds[i] = 0;
-    for (int i = threadIdx.x; i < (nfull + 1) / 2; i += NT_) cnt[i] = 0;
-    if (threadIdx.x == 0) { wkey = 0; SS.wor = 0u; SS.wrap = 0u; }
-    __syncthreads();
-
     const long long nvec = (long long)max(0, row1 - row0) * CR;
     const V* s = reinterpret_cast<const V*>(src + (size_t)row0 * W);
     V* d = STORE ? reinterpret_cast<V*>(dst + (size_t)row0 * W) : nullptr;
+    const long long step = (long long)NT_ * U;
+    const long long nwhole = nvec / step * step;   // iterations with every vector in range
+    V v[U], vn[U];
+#if SCAN_EARLY_LOAD
+    // the region's first loads go out before the LDS zeroing (they touch no LDS), and the
+    // barrier after it is LDS-only (__syncthreads' fence would wait for them)
+    if (PIPE && DIAG != 5 && nwhole > 0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = ldv<NT>(s + (long long)u * NT_ + threadIdx.x);
+    }
+#endif
+    for (int i = threadIdx.x; i < HistCfg<T>::kLdsWords; i += NT_) lds[i] = 0;
+    for (int i = threadIdx.x; i < (nfull + 1) / 2; i += NT_) cnt[i] = 0;
+    if (threadIdx.x == 0) { wkey = 0; SS.wor = 0u; SS.wrap = 0u; }
+#if SCAN_EARLY_LOAD
+    lds_barrier();
+#else
+    __syncthreads();
+#endif
     const int lane = threadIdx.x & 63;
     const bool grouped = (CR % G) == 0;                     // G-lane groups share a block row
     // (row, column-vector) of this thread's first vector, advanced incrementally
@@ -904,16 +924,15 @@ __device__ __forceinline__ void scan_rows_body(ScanRowsSmem<T>& SS, const T* __r
                 if (ok) hist_add8<T>(lds, ghist, v[u], FUSED ? &SS.wrap : nullptr);
         }
     };
-    const long long step = (long long)NT_ * U;
-    const long long nwhole = nvec / step * step;   // iterations with every vector in range
     if constexpr (PIPE) {
         // software pipelined: the next iteration's loads are issued before this iteration's
         // stores and histogram adds
-        V v[U], vn[U];
+#if !SCAN_EARLY_LOAD
         if (nwhole > 0) {
 #pragma unroll
             for (int u = 0; u < U; ++u) v[u] = ldv<NT>(s + (long long)u * NT_ + threadIdx.x);
         }
+#endif
         for (long long base = 0; base < nwhole; base += step) {
             if (base + step < nwhole) {
 #pragma unroll
@@ -2343,6 +2362,13 @@ __global__ __launch_bounds__(1024) void k_restore_ss(const T* __restrict__ stego
 // pass after it (a full vmcnt(0) drain, then a dependent load + store).  Bits as gather_body:
 // bit j = stego bit p of the j-th window pixel in segment order, j = cat[p] + (q - off[p]) mod npx.
 #define RIL_WORDS 4096   // 32-bit LDS words each for the map and the payload (host-checked)
+// LDS-only barriers in the ring loop keep the 16 waves in step: without them the oldest waves
+// ran ahead and the slice's tail was streamed by the youngest alone (as in k_pee_embed_ss).
+// 2 = one barrier per ring slot (G vectors): C3 restore 0.0519 -> 0.0486 ms
+// (profiles/r03/c3_ril_lockstep_ab.log); 1 = per ring group, 3 = per vector, 0 = none
+#ifndef RIL_LOCKSTEP
+#define RIL_LOCKSTEP 2
+#endif
 template <typename T, bool NT, int D, int G>
 __global__ __launch_bounds__(1024) void k_restore_il(const T* __restrict__ stego, T* __restrict__ cover, uint32_t npx,
                                                      const codec_slice_meta* __restrict__ meta,
@@ -2445,7 +2471,13 @@ __global__ __launch_bounds__(1024) void k_restore_il(const T* __restrict__ stego
                 const uint32_t idx = base + (uint32_t)(d * G + g) * 1024u + t;
                 put(idx, r[d][g]);
                 r[d][g] = ldv<NT>(src + idx + step);   // refill from the next group
+#if RIL_LOCKSTEP == 3
+                lds_barrier();
+#endif
             }
+#if RIL_LOCKSTEP == 1 || RIL_LOCKSTEP == 2
+            if (RIL_LOCKSTEP == 2 || d == D - 1) lds_barrier();
+#endif
         }
     }
 #pragma unroll

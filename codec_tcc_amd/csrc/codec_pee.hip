@@ -2138,6 +2138,12 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
 #define RES_PAD_WORDS_LIN (28 * 1024)
 #define RES_CNT_BASE(tmax) (RES_PAD_WORDS - (tmax) * RES_THREADS)
 
+// read phase: an LDS-only barrier every RES_LOCKSTEP items keeps the waves in step (without
+// it the oldest ran ahead and the slice's last items were streamed by a few waves): C3 embed
+// 0.0540 -> 0.0494 ms at 1 or 2 (profiles/r03/lockstep_ab.log); 0 = none
+#ifndef RES_LOCKSTEP
+#define RES_LOCKSTEP 1
+#endif
 #ifndef RES_G
 #define RES_G 4   // items per thread in flight ahead of the one processed (read phase)
 #endif
@@ -2349,6 +2355,9 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
             } else {
                 stv<NTS>(in ? reinterpret_cast<V*>(dst + oo[k % (G + 1)]) : sink_v, a0);
             }
+#if RES_LOCKSTEP
+            if ((k % RES_LOCKSTEP) == RES_LOCKSTEP - 1) lds_barrier();
+#endif
         }
     }
     lds_barrier();
