@@ -2144,6 +2144,9 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
 #ifndef RES_LOCKSTEP
 #define RES_LOCKSTEP 1
 #endif
+#ifndef RES_ELOCK
+#define RES_ELOCK 0   // embed phase: the same every RES_ELOCK items (build-time A/B)
+#endif
 #ifndef RES_G
 #define RES_G 4   // items per thread in flight ahead of the one processed (read phase)
 #endif
@@ -2549,6 +2552,9 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
         }
         if constexpr (LIN) {
             stv<NTS>(reinterpret_cast<V*>(dst + o1), v1);
+#if RES_ELOCK
+            if ((k % RES_ELOCK) == RES_ELOCK - 1) lds_barrier();
+#endif
             continue;
         }
         // stores, unconditional: the map word halves (zeros past `end`), the odd row
@@ -2556,6 +2562,9 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
         *(ok && (lane & 7) == 0 && (int)wix < lmw ? reinterpret_cast<uint32_t*>(lm + wix) + ((lane >> 3) & 1) : sink_w) =
             wm;
         stv<NTS>(ok ? reinterpret_cast<V*>(dst + o1) : sink_v + 1, v1);
+#if RES_ELOCK
+        if ((k % RES_ELOCK) == RES_ELOCK - 1) lds_barrier();
+#endif
     }
     const uint32_t running = s_cap;   // expandable candidates of the slice at T
     // lm_count: one block reduction
