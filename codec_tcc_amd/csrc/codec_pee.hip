@@ -2147,6 +2147,10 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
 #ifndef RES_ELOCK
 #define RES_ELOCK 0   // embed phase: the same every RES_ELOCK items (build-time A/B)
 #endif
+#ifndef RES_G1024
+#define RES_G1024 2   // the same at 1024 threads (build-time A/B: 1 ties, 3 and 4 are slower once the
+                      // read phase runs in lockstep, profiles/r03/c3_res_depth_ab.log)
+#endif
 #ifndef RES_G
 #define RES_G 4   // items per thread in flight ahead of the one processed (read phase)
 #endif
@@ -2284,7 +2288,7 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
     {
         // G items per thread in flight ahead of the one processed: item k + G is issued just
         // before item k is processed (a ring of G + 1 even-row vectors)
-        constexpr int G = NTH == 1024 ? 2 : RES_G;   // 4 waves per SIMD: half the registers, as many loads in flight per CU
+        constexpr int G = NTH == 1024 ? RES_G1024 : RES_G;   // 4 waves per SIMD: half the registers, as many loads in flight per CU
         V v0[G + 1];
         uint32_t oo[G + 1];
         SsCursor cur;
