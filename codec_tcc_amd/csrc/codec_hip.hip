@@ -549,18 +549,21 @@ __device__ __forceinline__ void hist_add<uint8_t>(uint32_t* lds, uint32_t*, uint
     atomicAdd(&lds[((threadIdx.x >> 6) << 8) + v], cnt);
 }
 
+// `vmax` bounds every value the workgroup counted (its OR of pixels: a value's bits are a
+// subset of it), so LDS words past vmax / 2 are zero and are not read (ct12: 2 048 of 32 768)
 template <typename T>
-__device__ void hist_flush(uint32_t* lds, uint32_t* ghist);
+__device__ void hist_flush(uint32_t* lds, uint32_t* ghist, uint32_t vmax = 0xFFFFu);
 template <>
-__device__ void hist_flush<uint16_t>(uint32_t* lds, uint32_t* ghist) {
+__device__ void hist_flush<uint16_t>(uint32_t* lds, uint32_t* ghist, uint32_t vmax) {
     u64* g64 = reinterpret_cast<u64*>(ghist);
-    for (int w = threadIdx.x; w < 32768; w += blockDim.x) {
+    const int nw = (int)min((vmax & 0xFFFFu) >> 1, 32767u) + 1;
+    for (int w = threadIdx.x; w < nw; w += blockDim.x) {
         const uint32_t x = lds[w];
         if (x) atomicAdd(&g64[w], (u64)(x & 0xFFFFu) | ((u64)(x >> 16) << 32));
     }
 }
 template <>
-__device__ void hist_flush<uint8_t>(uint32_t* lds, uint32_t* ghist) {
+__device__ void hist_flush<uint8_t>(uint32_t* lds, uint32_t* ghist, uint32_t) {
     for (int v = threadIdx.x; v < 256; v += blockDim.x) {
         uint32_t acc = 0;
         for (int c = 0; c < 16; ++c) acc += lds[(c << 8) + v];
@@ -736,7 +739,7 @@ __device__ __forceinline__ void scan_fast_body(const T* __restrict__ cover, T* _
     // one global OR per workgroup (a same-address global atomic per wave serialised)
     if (lane == 0 && vor) atomicOr(&wor, vor);
     __syncthreads();
-    hist_flush<T>(lds, ghist);
+    hist_flush<T>(lds, ghist, wor);
     if (threadIdx.x == 0) {
         if (wkey) atomicMax(&gkey[b], wkey);
         if (wor) atomicOr(&gor[b], wor);
@@ -963,10 +966,7 @@ __device__ __forceinline__ void scan_rows_body(ScanRowsSmem<T>& SS, const T* __r
     else vor = (vor | (vor >> 8) | (vor >> 16) | (vor >> 24)) & 0xFFu;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) vor |= __shfl_xor(vor, o, 64);
-    if (lane == 0 && vor) {
-        if constexpr (FUSED) atomicOr(&SS.wor, vor);
-        else atomicOr(&gor[b], vor);
-    }
+    if (lane == 0 && vor) atomicOr(&SS.wor, vor);   // the workgroup's OR (bounds the flush)
     __syncthreads();
     // block keys: score c(n-c) (exact variance numerator of a full pow2 block), first
     // maximal block in raster order wins (~index in the low word)
@@ -985,9 +985,10 @@ __device__ __forceinline__ void scan_rows_body(ScanRowsSmem<T>& SS, const T* __r
         best = best > other ? best : other;
     }
     if (lane == 0 && best) atomicMax(&wkey, best);
-    if (DIAG == 0 && !FUSED) hist_flush<T>(lds, ghist);
+    if (DIAG == 0 && !FUSED) hist_flush<T>(lds, ghist, SS.wor);
     __syncthreads();
     if (!FUSED && threadIdx.x == 0 && wkey) atomicMax(&gkey[b], wkey);
+    if (!FUSED && threadIdx.x == 0 && SS.wor) atomicOr(&gor[b], SS.wor);
 }
 
 template <typename T, int SB, bool NT, bool STORE, int DIAG = 0, bool PIPE = true, int U = 4>
