@@ -645,7 +645,7 @@ template <typename T, int SB, bool NT, bool HIST>
 __device__ __forceinline__ void scan_fast_body(const T* __restrict__ cover, T* __restrict__ stego,
                                                int H, int W, int bands_per_wg,
                                                uint32_t* __restrict__ ghist_all,
-                                               u64* __restrict__ gkey, uint32_t* __restrict__ gor) {
+                                               u64* __restrict__ gkey, uint32_t* __restrict__ gor, int csplit) {
     typedef typename Vec8<T>::type V;
     constexpr int G = SB / 8;
     constexpr uint32_t NPB = (uint32_t)SB * SB;
@@ -663,13 +663,18 @@ __device__ __forceinline__ void scan_fast_body(const T* __restrict__ cover, T* _
     __syncthreads();
 
     const int nbands = (H + SB - 1) / SB;
-    const int band0 = blockIdx.x * bands_per_wg;
+    // csplit > 1 (small batches: fewer bands than CUs): workgroup x takes column segment
+    // x % csplit of the bands of group x / csplit; segments are whole block columns (G chunks)
+    const int band0 = (int)(blockIdx.x / (unsigned)csplit) * bands_per_wg;
     const int band1 = min(nbands, band0 + bands_per_wg);
     const int CR = W / 8;
     const int CRp = (CR + G - 1) / G * G;
+    const int seg = (int)(blockIdx.x % (unsigned)csplit);
+    const int CRs = (CRp / G + csplit - 1) / csplit * G;   // chunks per segment, a multiple of G
+    const int c0 = min(CRp, seg * CRs), CRw = min(CRp, c0 + CRs) - c0;
     const int nbx = (W + SB - 1) / SB;
     const int fullbx = W / SB, fullby = H / SB;
-    const int nitems = max(0, band1 - band0) * CRp;
+    const int nitems = max(0, band1 - band0) * CRw;
     const int lane = threadIdx.x & 63;
     u64 best = 0;
     uint32_t vor = 0;   // OR of every pixel: bounds the histogram range the decision scans
@@ -677,8 +682,8 @@ __device__ __forceinline__ void scan_fast_body(const T* __restrict__ cover, T* _
     for (int base = (threadIdx.x & ~63); base < nitems; base += 1024) {
         const int it = base + lane;
         const bool valid = it < nitems;
-        const int band = band0 + (valid ? it / CRp : 0);
-        const int c = valid ? it % CRp : CRp;
+        const int band = band0 + (valid ? it / CRw : 0);
+        const int c = valid ? c0 + it % CRw : CRp;
         const bool inrow = valid && c < CR;
         uint32_t ones = 0;
         if (inrow) {
@@ -750,8 +755,8 @@ template <typename T, int SB, bool NT, bool HIST = true>
 __global__ __launch_bounds__(1024) void k_scan_fast(const T* __restrict__ cover, T* __restrict__ stego,
                                                     int H, int W, int bands_per_wg,
                                                     uint32_t* __restrict__ ghist_all,
-                                                    u64* __restrict__ gkey, uint32_t* __restrict__ gor) {
-    scan_fast_body<T, SB, NT, HIST>(cover, stego, H, W, bands_per_wg, ghist_all, gkey, gor);
+                                                    u64* __restrict__ gkey, uint32_t* __restrict__ gor, int csplit) {
+    scan_fast_body<T, SB, NT, HIST>(cover, stego, H, W, bands_per_wg, ghist_all, gkey, gor, csplit);
 }
 
 // read-only variant (plan only, or in place where the stego copy is the cover itself); a
@@ -759,8 +764,8 @@ __global__ __launch_bounds__(1024) void k_scan_fast(const T* __restrict__ cover,
 template <typename T, int SB>
 __global__ __launch_bounds__(1024) void k_scan_read(const T* __restrict__ cover, int H, int W, int bands_per_wg,
                                                     uint32_t* __restrict__ ghist_all,
-                                                    u64* __restrict__ gkey, uint32_t* __restrict__ gor) {
-    scan_fast_body<T, SB, true, true>(cover, nullptr, H, W, bands_per_wg, ghist_all, gkey, gor);
+                                                    u64* __restrict__ gkey, uint32_t* __restrict__ gor, int csplit) {
+    scan_fast_body<T, SB, true, true>(cover, nullptr, H, W, bands_per_wg, ghist_all, gkey, gor, csplit);
 }
 
 // ------------------------------------------------------------------ K1 (row-major): scan + copy
@@ -2883,19 +2888,30 @@ static int launch_scan_fast(const codec_params* P, const void* cover, void* steg
     // so small regions cost more than they stream: measured 256 x 512^2 0.066 ms at one
     // workgroup per slice vs 0.108 at four; 256 x 2048^2 best at four)
     const long long slice_bytes = (long long)P->H * P->W * sizeof(T);
-    // batches under 128 MiB (e.g. 1..8 slices of 2048^2): 128 workgroups in the band order
-    // measured best (1 x 2048^2: 0.020 ms vs 0.032 for the row sweep; 8 x 2048^2: 0.056 vs
-    // 0.074 at 256 workgroups)
+    // batches under 128 MiB (e.g. 1..8 slices of 2048^2): the band order (1 x 2048^2: 0.020 ms
+    // vs 0.032 for the row sweep) with 256 workgroups since the flush reads only the counted
+    // range (2 / 4 / 8 x 2048^2: 0.0193 / 0.025 / 0.036 ms vs 0.0205 / 0.029 / 0.046 at 128 and
+    // 0.019 / 0.034 / 0.044 at 512, profiles/r03/scan_small_sweep.log; a lone slice has 128 bands)
     const bool small = (long long)P->B * slice_bytes < (128LL << 20);
-    const int per_slice = small ? (128 + P->B - 1) / P->B
+    const int per_slice = small ? (256 + P->B - 1) / P->B
                                 : (int)std::max<long long>((256 + P->B - 1) / P->B, (slice_bytes + (2 << 20) - 1) / (2 << 20));
     const int target = (int)knob("CODEC_SCAN_WGS", (long long)per_slice * P->B);   // tools/tune.py
     const bool nt = knob("CODEC_NT", 1) != 0;
     int wgps = (target + P->B - 1) / P->B;
+    // column-band sweep of a batch with fewer bands than the target (a lone 2048^2 slice has
+    // 128 bands for 256 CUs): each band's columns are split over csplit workgroups
+    // (CODEC_SCAN_CSPLIT; whole block columns per segment)
+    const int want = wgps;
     wgps = wgps < 1 ? 1 : (wgps > nb ? nb : wgps);
     const int bpw = (nb + wgps - 1) / wgps;
     wgps = (nb + bpw - 1) / bpw;
-    dim3 grid(wgps, P->B);
+    const int gcols = (P->W / 8 + sb / 8 - 1) / (sb / 8);   // block columns (G chunks each)
+    // off by default: a lone 2048^2 slice scans slower split (256 workgroups 0.0191 vs 128
+    // 0.0167 ms: every workgroup's flush adds to the same slice's words, profiles/r03/c2_csplit.log)
+    int csplit = (int)knob("CODEC_SCAN_CSPLIT", 1);
+    (void)want;
+    csplit = csplit < 1 ? 1 : (csplit > gcols ? gcols : (csplit > 8 ? 8 : csplit));
+    dim3 grid(wgps * csplit, P->B);
     const T* c = static_cast<const T*>(cover);
     T* s = static_cast<T*>(stego);
     // the row sweep needs one band's full blocks to fit its LDS counters; wider images
@@ -2940,25 +2956,25 @@ static int launch_scan_fast(const codec_params* P, const void* cover, void* steg
     if (!s) {
         ProfScope prof(st, CODEC_K_SCAN_READ);
         switch (sb) {
-            case 8: hipLaunchKernelGGL((k_scan_read<T, 8>), grid, dim3(1024), 0, st, c, P->H, P->W, bpw, hist, keys, orv); break;
-            case 16: hipLaunchKernelGGL((k_scan_read<T, 16>), grid, dim3(1024), 0, st, c, P->H, P->W, bpw, hist, keys, orv); break;
-            case 32: hipLaunchKernelGGL((k_scan_read<T, 32>), grid, dim3(1024), 0, st, c, P->H, P->W, bpw, hist, keys, orv); break;
-            default: hipLaunchKernelGGL((k_scan_read<T, 64>), grid, dim3(1024), 0, st, c, P->H, P->W, bpw, hist, keys, orv); break;
+            case 8: hipLaunchKernelGGL((k_scan_read<T, 8>), grid, dim3(1024), 0, st, c, P->H, P->W, bpw, hist, keys, orv, csplit); break;
+            case 16: hipLaunchKernelGGL((k_scan_read<T, 16>), grid, dim3(1024), 0, st, c, P->H, P->W, bpw, hist, keys, orv, csplit); break;
+            case 32: hipLaunchKernelGGL((k_scan_read<T, 32>), grid, dim3(1024), 0, st, c, P->H, P->W, bpw, hist, keys, orv, csplit); break;
+            default: hipLaunchKernelGGL((k_scan_read<T, 64>), grid, dim3(1024), 0, st, c, P->H, P->W, bpw, hist, keys, orv, csplit); break;
         }
         LAUNCH_CHECK("k_scan_read");
         return 0;
     }
     ProfScope prof(st, CODEC_K_SCAN_FAST);
     switch (sb) {
-        case 8: if (nt) hipLaunchKernelGGL((k_scan_fast<T, 8, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv);
-                else hipLaunchKernelGGL((k_scan_fast<T, 8, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
-        case 16: if (knob("CODEC_DIAG_NOHIST", 0)) hipLaunchKernelGGL((k_scan_fast<T, 16, true, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv);   // timing diagnostics only: s is wrong
-                else if (nt) hipLaunchKernelGGL((k_scan_fast<T, 16, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv);
-                else hipLaunchKernelGGL((k_scan_fast<T, 16, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
-        case 32: if (nt) hipLaunchKernelGGL((k_scan_fast<T, 32, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv);
-                else hipLaunchKernelGGL((k_scan_fast<T, 32, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
-        default: if (nt) hipLaunchKernelGGL((k_scan_fast<T, 64, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv);
-                 else hipLaunchKernelGGL((k_scan_fast<T, 64, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv); break;
+        case 8: if (nt) hipLaunchKernelGGL((k_scan_fast<T, 8, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv, csplit);
+                else hipLaunchKernelGGL((k_scan_fast<T, 8, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv, csplit); break;
+        case 16: if (knob("CODEC_DIAG_NOHIST", 0)) hipLaunchKernelGGL((k_scan_fast<T, 16, true, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv, csplit);   // timing diagnostics only: s is wrong
+                else if (nt) hipLaunchKernelGGL((k_scan_fast<T, 16, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv, csplit);
+                else hipLaunchKernelGGL((k_scan_fast<T, 16, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv, csplit); break;
+        case 32: if (nt) hipLaunchKernelGGL((k_scan_fast<T, 32, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv, csplit);
+                else hipLaunchKernelGGL((k_scan_fast<T, 32, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv, csplit); break;
+        default: if (nt) hipLaunchKernelGGL((k_scan_fast<T, 64, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv, csplit);
+                 else hipLaunchKernelGGL((k_scan_fast<T, 64, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv, csplit); break;
     }
     LAUNCH_CHECK("k_scan_fast");
     return 0;
