@@ -614,14 +614,55 @@ def _free_port() -> int:
     return port
 
 
+PR_SET_PDEATHSIG = 1      # <linux/prctl.h>
+
+
+def _die_with_parent(parent_pid: int):
+    """preexec_fn of a rank (runs in the child between fork and exec, before any GPU call):
+    SIGKILL this process when the launcher dies, however it dies (the flag survives the
+    exec).  If the launcher is already gone, exit at once."""
+    import ctypes
+    import signal
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.prctl(PR_SET_PDEATHSIG, int(signal.SIGKILL), 0, 0, 0)
+    if os.getppid() != parent_pid:
+        os._exit(1)
+
+
+def _stop_ranks(procs, grace_s: float = 5.0):
+    """SIGTERM every live rank, SIGKILL what is still alive after `grace_s`, reap all."""
+    for p in procs:
+        if p.poll() is None:
+            try:
+                p.terminate()
+            except ProcessLookupError:
+                pass
+    t_end = time.monotonic() + grace_s
+    for p in procs:
+        try:
+            p.wait(timeout=max(0.0, t_end - time.monotonic()))
+        except Exception:   # subprocess.TimeoutExpired
+            pass
+    for p in procs:
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+
+
 def launch_ranks(args) -> int:
     """`bench.py --gpus N` without a launcher: start N fresh rank processes of this script
     (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, as torchrun sets them),
     wait for all of them and forward rank 0's JSON line.  This process never touches the GPU
-    (no HIP call, no torch.cuda query) and never execs: the ranks are child processes, and a
-    rank that fails stops the others (exit status of the first failure)."""
+    (no HIP call, no torch.cuda query) and never execs: the ranks are child processes.
+
+    Fail-safe: the ranks stay in this process group (a signal to the
+    group reaches them) and get PR_SET_PDEATHSIG = SIGKILL (a killed launcher never leaves
+    ranks holding GPUs); SIGTERM/SIGINT here stop every rank and exit non-zero; rank 0's
+    output is drained on a thread while every rank is polled, so the first rank that exits
+    non-zero -- whichever it is -- stops the others at once (exit status of that failure)."""
     import signal
     import subprocess
+    import threading
     n = int(args.gpus)
     env0 = dict(os.environ)
     env0.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -630,45 +671,69 @@ def launch_ranks(args) -> int:
     env0["LOCAL_WORLD_SIZE"] = str(n)
     env0.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC (RCCL / cross-process tensors)
     cmd = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+    me = os.getpid()
     procs = []
-    for r in range(n):
-        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r), GROUP_RANK="0")
-        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else None,
-                                      start_new_session=True, text=True))
-    line = None
-    rc = 0
+
+    def on_signal(signum, _frame):
+        _stop_ranks(procs, grace_s=2.0)
+        sys.stderr.write(f"bench.py: launcher got signal {signum}; stopped {len(procs)} ranks\n")
+        os._exit(128 + signum)
+
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
+    lines = []
     try:
-        for raw in procs[0].stdout:          # rank 0's output: forward the JSON line, echo the rest
-            if raw.startswith("{"):
-                line = raw.strip()
-            else:
-                sys.stderr.write(raw)
-        while procs:
-            for p in list(procs):
+        for r in range(n):
+            env = dict(env0, RANK=str(r), LOCAL_RANK=str(r), GROUP_RANK="0")
+            procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else None, text=True,
+                                          preexec_fn=lambda: _die_with_parent(me)))
+        sys.stderr.write("bench.py: rank pids " + " ".join(str(p.pid) for p in procs) + "\n")
+        sys.stderr.flush()
+
+        def drain(stream):               # rank 0's output: keep the JSON line, echo the rest
+            for raw in stream:
+                if raw.startswith("{"):
+                    lines.append(raw.strip())
+                else:
+                    sys.stderr.write(raw)
+        reader = threading.Thread(target=drain, args=(procs[0].stdout,), daemon=True)
+        reader.start()
+        rc = 0
+        live = list(procs)
+        while live and rc == 0:
+            for p in list(live):
                 code = p.poll()
                 if code is None:
                     continue
-                procs.remove(p)
-                if code != 0 and rc == 0:
+                live.remove(p)
+                if code != 0:
                     rc = code if code > 0 else 128 - code
-                    for q in procs:          # one rank failed: the others would wait forever
-                        try:
-                            os.killpg(q.pid, signal.SIGTERM)
-                        except ProcessLookupError:
-                            pass
+                    sys.stderr.write(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the others\n")
+                    break
             time.sleep(0.05)
+        reader.join(timeout=10)
     finally:
-        for q in procs:
-            try:
-                os.killpg(q.pid, signal.SIGKILL)
-            except ProcessLookupError:
-                pass
+        _stop_ranks(procs)
+        for s, h in old.items():
+            signal.signal(s, h)
+    line = lines[-1] if lines else None
     if rc == 0 and line:
         print(line, flush=True)
     elif rc == 0:
         sys.stderr.write("bench.py: rank 0 printed no JSON line\n")
         rc = 1
     return rc
+
+
+def _rank_fault_knob(rank: int):
+    """CODEC_BENCH_FAIL_RANK=k (tests of the launcher only): rank k exits 3 right after
+    joining the process group; CODEC_BENCH_STALL_RANK=k: rank k sleeps forever there."""
+    if os.environ.get("CODEC_BENCH_FAIL_RANK") == str(rank):
+        sys.stderr.write(f"bench.py: rank {rank} failing on request (CODEC_BENCH_FAIL_RANK)\n")
+        sys.stderr.flush()
+        os._exit(3)
+    if os.environ.get("CODEC_BENCH_STALL_RANK") == str(rank):
+        while True:
+            time.sleep(1)
 
 
 def main():
@@ -696,11 +761,20 @@ def main():
         sys.exit(f"bench.py: {world} ranks over RCCL need {world} GPUs, {ndev} visible "
                  "(--backend gloo rehearses the multi-rank path with several ranks per GPU)")
     if world > 1:
-        torch.cuda.set_device(local % ndev)
+        # a collective that waits longer than this (a dead or stuck peer) raises instead of
+        # hanging the job; rank 0's solo legs (C3, quality) stay far below it
+        from datetime import timedelta
+        pg_timeout = timedelta(seconds=float(os.environ.get("CODEC_BENCH_PG_TIMEOUT", "180")))
+        if ndev:
+            torch.cuda.set_device(local % ndev)
         if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local % ndev))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local % ndev), timeout=pg_timeout)
         else:   # rehearsal of the multi-rank path on fewer GPUs (e.g. gloo, 2 ranks on 1 GPU)
-            dist.init_process_group(args.backend)
+            dist.init_process_group(args.backend, timeout=pg_timeout)
+        _rank_fault_knob(rank)
+        dist.barrier()                        # every rank is up before any GPU work
+    if ndev == 0:
+        sys.exit("bench.py: no GPU visible (the benchmark runs the HIP kernels; there is no CPU path)")
     dev = torch.device("cuda", local % ndev if world > 1 else torch.cuda.current_device())
     B, H, W = args.batch, args.size, args.size
     covers = make_covers(torch, args.kind, B, H, W, dev, seed=rank * B)

@@ -10,7 +10,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # CODEC_TCC_LIB: an alternative build of the same library (A/B benchmarking, tools/ab_bench.sh)
-LIB_PATH = os.environ.get("CODEC_TCC_LIB") or os.path.join(_HERE, "libcodec_hip.so")
+_DEFAULT_PATH = os.path.join(_HERE, "libcodec_hip.so")
+LIB_PATH = os.environ.get("CODEC_TCC_LIB") or _DEFAULT_PATH
 
 MAX_PLANES = 16
 MODE_HYBRID = 0
@@ -71,6 +72,7 @@ LAYOUT_BYTES = C.sizeof(Layout)
 _VP = C.c_void_p
 _SIGS = {
     "codec_abi_version": (C.c_int, []),
+    "codec_build_digest": (C.c_char_p, []),
     "codec_last_error": (C.c_char_p, []),
     "codec_workspace_bytes": (C.c_size_t, [C.POINTER(Params)]),
     "codec_plan": (C.c_int, [C.POINTER(Params), _VP, _VP, _VP, C.c_int64, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),
@@ -126,19 +128,38 @@ def load(path: str = LIB_PATH):
     if not os.path.exists(path):
         raise RuntimeError(f"libcodec_hip.so not found at {path}: build it with "
                            f"`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback)")
+    in_tree = os.path.abspath(path) == os.path.abspath(_DEFAULT_PATH)
+    if in_tree:
+        _check_digest(path)
     try:
         lib = C.CDLL(path)
     except OSError as e:  # pragma: no cover - environment specific
         _load_error = e
         raise RuntimeError(f"cannot load {path}: {e}") from e
     for name, (res, args) in _SIGS.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if name == "codec_build_digest" and not in_tree:   # a diagnostic build (tools/)
+                continue
+            raise RuntimeError(f"{path} does not export {name}")
         fn.restype = res
         fn.argtypes = args
     if lib.codec_abi_version() != 1:
         raise RuntimeError("libcodec_hip.so ABI mismatch")
     _lib = lib
     return lib
+
+
+def _check_digest(path: str):
+    """Refuse an in-tree library not built from the tree's sources: its
+    embedded digest (build.library_digest, read from the file before loading it) must equal
+    the digest of csrc/*, include/codec_tcc.h and the build flags.  No rebuild here: on the
+    GPU box the prebuilt library is the product, and a mismatch there is an error."""
+    from . import build
+    have, want = build.library_digest(path), build.source_digest()
+    if have != want:
+        raise RuntimeError(f"{path} was not built from these sources (library digest {have}, sources {want}): "
+                           "rebuild it with `python -c 'import __graft_entry__ as g; g.build()'`")
 
 
 def check(rc: int, what: str):

@@ -251,6 +251,21 @@ static long long knob(const char* name, long long dflt) {
     return (v && *v) ? atoll(v) : dflt;
 }
 
+// fault-injection and spin-bound knobs (tests only): live only in a -DCODEC_DEBUG_KNOBS build
+// or with the master switch CODEC_DEBUG=1, so a leaked CODEC_PEE_DEBUG_SKIP cannot make a
+// production launch skip a publish
+static inline bool debug_knobs_enabled() {
+#ifdef CODEC_DEBUG_KNOBS
+    return true;
+#else
+    const char* v = getenv("CODEC_DEBUG");
+    return v && v[0] == '1' && v[1] == 0;
+#endif
+}
+static long long debug_knob(const char* name, long long dflt) {
+    return debug_knobs_enabled() ? knob(name, dflt) : dflt;
+}
+
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // CUs of the current device (cached per device): slice-serial dispatch decisions

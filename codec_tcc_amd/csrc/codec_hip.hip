@@ -3095,8 +3095,8 @@ static int plan_impl(const codec_params* P, const void* cover, void* stego, cons
     // workgroups are co-resident by construction, so it only trips on a broken launch --
     // CODEC_DECIDE_SPINS / CODEC_DECIDE_DEBUG_LATE=i+1 (plane i of slice 0 publishes only
     // after the main workgroup gave up) exist to test that path
-    const uint32_t spin_max = (uint32_t)knob("CODEC_DECIDE_SPINS", 1 << 24);
-    const int dbg_late = (int)knob("CODEC_DECIDE_DEBUG_LATE", 0) - 1;
+    const uint32_t spin_max = (uint32_t)debug_knob("CODEC_DECIDE_SPINS", 1 << 24);
+    const int dbg_late = (int)debug_knob("CODEC_DECIDE_DEBUG_LATE", 0) - 1;
     ProfScope prof(st, E ? CODEC_K_DECIDE_EMBED : CODEC_K_DECIDE);
     const EmbedArgs Ev = E ? *E : EmbedArgs{nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
 #define DEC(TT, EM) hipLaunchKernelGGL((k_decide<TT, EM>), dim3(P->B, 1 + nsplit), dim3(1024), 0, st, Pv, hist, orv, terms, keys, exact, \

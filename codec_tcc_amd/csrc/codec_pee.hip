@@ -2916,7 +2916,7 @@ int codec_pee_capacity(const codec_pee_params* P, const void* cover, int32_t tma
     ProfScope prof(st, CODEC_K_PEE_CAPACITY);
     {   // launched even when there is nothing to count: the last workgroup writes caps / t_out
         const long long per = knob("CODEC_PEE_EHIST_PER_WG", 4096);
-        const int dbg_delay = (int)knob("CODEC_PEE_EHIST_DEBUG_DELAY", 0) - 1;
+        const int dbg_delay = (int)debug_knob("CODEC_PEE_EHIST_DEBUG_DELAY", 0) - 1;
         dim3 grid((unsigned)max(1LL, (units + per - 1) / per), (unsigned)P->B);
         const size_t lds = (size_t)tmax * 256 * 4;   // lane-private counters
         uint32_t* arrivals = hist + (size_t)P->B * PEE_TMAX_MAX;
@@ -3034,8 +3034,8 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
         long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));
         if (g > total) g = total;
         g = (g + 7) / 8 * 8;   // keep every workgroup on one slot lane (pee_slot)
-        const uint32_t spin_max = (uint32_t)knob("CODEC_PEE_LB_SPINS", inplace ? (1 << 22) : (1 << 14));
-        const int dbg_skip = (int)knob("CODEC_PEE_DEBUG_SKIP", 0) - 1;
+        const uint32_t spin_max = (uint32_t)debug_knob("CODEC_PEE_LB_SPINS", inplace ? (1 << 22) : (1 << 14));
+        const int dbg_skip = (int)debug_knob("CODEC_PEE_DEBUG_SKIP", 0) - 1;
         uint32_t* diag = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.diag);
 #define PE1(TT, NTV, IP) hipLaunchKernelGGL((k_pee_embed1<TT, NTV, IP>), dim3((unsigned)g), dim3(256), 0, st, \
             static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, \
@@ -3266,8 +3266,8 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
         long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));
         if (g > total) g = total;
         g = (g + 7) / 8 * 8;
-        const uint32_t spin_max = (uint32_t)knob("CODEC_PEE_LB_SPINS", inplace ? (1 << 22) : (1 << 14));
-        const int dbg_skip = (int)knob("CODEC_PEE_DEBUG_SKIP", 0) - 1;
+        const uint32_t spin_max = (uint32_t)debug_knob("CODEC_PEE_LB_SPINS", inplace ? (1 << 22) : (1 << 14));
+        const int dbg_skip = (int)debug_knob("CODEC_PEE_DEBUG_SKIP", 0) - 1;
         uint32_t* diag = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.diag);
 #define PX1(TT, NTV, IP) hipLaunchKernelGGL((k_pee_extract1<TT, NTV, IP>), dim3((unsigned)g), dim3(256), 0, st, \
             static_cast<const TT*>(stego), static_cast<TT*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm), \

@@ -93,6 +93,10 @@ typedef struct codec_slice_meta {
 
 int codec_abi_version(void);
 const char* codec_last_error(void);
+/* SHA-256 (hex) of the sources, headers and compiler flags this library was built from
+ * (codec_tcc_amd/build.py); the Python loader refuses an in-tree library whose digest differs
+ * from the tree's.  No reference counterpart (build integrity only). */
+const char* codec_build_digest(void);
 
 /* Bytes of scratch `codec_plan` needs for these parameters.  Zero-initialise the workspace
  * once before its first use: codec_plan / codec_encode expect its histogram words clear and

@@ -72,6 +72,102 @@ def test_committed_pmc_summaries_resolve_every_bench_instance():
         assert bench.pmc_traffic(tag, 256, 512, 512, "ct12", ta) is not None, tag
 
 
+def _launcher(env_extra):
+    """bench.py --gpus 2 --backend gloo without a launcher, ranks driven by the fault knobs
+    (they act right after init_process_group, before any GPU call, so this runs on CPU)."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra)
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo", "--cpu-seconds", "0"]
+    return subprocess.Popen(cmd, env=env, cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+
+
+def _rank_pids(proc, timeout=120):
+    """Read the launcher's stderr until it names its rank pids."""
+    import time
+    t0 = time.monotonic()
+    seen = []
+    for line in proc.stderr:
+        seen.append(line)
+        if line.startswith("bench.py: rank pids "):
+            return [int(x) for x in line.split()[3:]], seen
+        assert time.monotonic() - t0 < timeout, "".join(seen)
+    raise AssertionError("launcher printed no rank pids:\n" + "".join(seen))
+
+
+def _gone(pids, timeout=20.0):
+    import time
+
+    import psutil
+    t_end = time.monotonic() + timeout
+    while time.monotonic() < t_end:
+        alive = []
+        for p in pids:
+            try:
+                if psutil.Process(p).status() != psutil.STATUS_ZOMBIE:
+                    alive.append(p)
+            except psutil.NoSuchProcess:
+                pass
+        if not alive:
+            return True
+        time.sleep(0.1)
+    return False
+
+
+def _kill_all(pids):
+    import signal
+    for p in pids:
+        try:
+            os.kill(p, signal.SIGKILL)
+        except (ProcessLookupError, PermissionError):
+            pass
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("fail,stall", [("1", "0"), ("0", "1")])
+def test_launcher_failed_rank_stops_the_others(fail, stall):
+    """one rank exits non-zero while the other is stuck (as in a collective
+    that will never complete): the launcher sees it whatever the failing rank's index, stops
+    the stuck rank, returns that failure's status within seconds and leaves no rank alive."""
+    import time
+    t0 = time.monotonic()
+    proc = _launcher({"CODEC_BENCH_FAIL_RANK": fail, "CODEC_BENCH_STALL_RANK": stall})
+    pids = []
+    try:
+        pids, _ = _rank_pids(proc)
+        rc = proc.wait(timeout=90)
+        err = proc.stderr.read()
+        assert rc == 3, err
+        assert f"rank {fail} exited with 3" in err
+        assert time.monotonic() - t0 < 90
+        assert _gone(pids), pids
+    finally:
+        if proc.poll() is None:
+            proc.kill()
+        _kill_all(pids)
+
+
+@pytest.mark.parametrize("sig", ["SIGTERM", "SIGKILL"])
+def test_launcher_killed_leaves_no_ranks(sig):
+    """A launcher that is terminated (its handler stops the ranks) or killed outright (the
+    ranks' parent-death signal) never leaves ranks behind."""
+    import signal
+    proc = _launcher({"CODEC_BENCH_STALL_RANK": "0", "CODEC_BENCH_FAIL_RANK": "none"})
+    pids = []
+    try:
+        pids, _ = _rank_pids(proc)
+        os.kill(proc.pid, getattr(signal, sig))
+        rc = proc.wait(timeout=60)
+        assert rc != 0
+        assert _gone(pids), pids
+    finally:
+        if proc.poll() is None:
+            proc.kill()
+        _kill_all(pids)
+
+
 def test_gpus_world_size_mismatch_is_refused():
     """bench.py --gpus N under a launcher that started a different number of ranks exits
     non-zero before touching the GPU."""

@@ -418,6 +418,7 @@ def test_split_decision_timeout_leaves_no_stale_slot(monkeypatch):
     ref = codec.encode(covers, msgs)
     rr = ref.records()
     assert all(r.status == 0 for r in rr)
+    monkeypatch.setenv("CODEC_DEBUG", "1")               # the fault-injection knobs' master switch
     monkeypatch.setenv("CODEC_DECIDE_SPINS", "200")
     monkeypatch.setenv("CODEC_DECIDE_DEBUG_LATE", "1")
     with pytest.raises(RuntimeError, match="timed out"):

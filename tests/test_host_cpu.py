@@ -90,6 +90,30 @@ def test_struct_layout_matches_header():
     assert sizes[8] == _lib.PeeMeta.lm_count.offset
 
 
+def test_library_digest_ties_binary_to_sources(monkeypatch, tmp_path):
+    """the in-tree library carries the digest of the sources it was built
+    from; the loader refuses it when the tree's digest differs (a stale or copied-in binary),
+    and a library without any digest is refused too."""
+    from codec_tcc_amd import build
+    if build.needs_build():
+        build.build()
+    assert build.library_digest() == build.source_digest()
+    monkeypatch.setattr(_lib, "_lib", None)                 # force a fresh load
+    monkeypatch.setattr(build, "source_digest", lambda: "0" * 64)
+    with pytest.raises(RuntimeError, match="not built from these sources"):
+        _lib.load()
+    monkeypatch.undo()
+    fake = tmp_path / "libcodec_hip.so"
+    fake.write_bytes(b"\x7fELF no digest here")
+    assert build.library_digest(str(fake)) is None
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "_DEFAULT_PATH", str(fake))
+    with pytest.raises(RuntimeError, match="not built from these sources"):
+        _lib.load(str(fake))
+    monkeypatch.undo()
+    assert _lib.load().codec_build_digest().decode() == build.source_digest()
+
+
 def test_library_exports_every_header_symbol():
     if not os.path.exists(_lib.LIB_PATH):
         from codec_tcc_amd import build

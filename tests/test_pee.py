@@ -300,6 +300,7 @@ def test_gpu_lookback_fallback_out_of_place(slots, monkeypatch):
     torch = pytest.importorskip("torch")
     from codec_tcc_amd import framing
     from codec_tcc_amd.pee import PeeCodec, lm_bits
+    monkeypatch.setenv("CODEC_DEBUG", "1")               # the fault-injection knobs' master switch
     monkeypatch.setenv("CODEC_PEE_ONEPASS", "1")
     monkeypatch.setenv("CODEC_PEE_DEBUG_SKIP", "2")
     monkeypatch.setenv("CODEC_PEE_LB_SPINS", "256")
@@ -327,6 +328,36 @@ def test_gpu_lookback_fallback_out_of_place(slots, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_gpu_fault_knobs_inert_without_master_switch(monkeypatch):
+    """a leaked CODEC_PEE_DEBUG_SKIP / CODEC_PEE_LB_SPINS has no effect
+    unless CODEC_DEBUG=1 is set: the in-place embed that the knob makes fail with the switch
+    (test below) succeeds without it, and no chunk needs the fallback out of place."""
+    torch = pytest.importorskip("torch")
+    from codec_tcc_amd.pee import PeeCodec
+    monkeypatch.delenv("CODEC_DEBUG", raising=False)
+    monkeypatch.setenv("CODEC_PEE_ONEPASS", "1")
+    monkeypatch.setenv("CODEC_PEE_SS", "0")                   # the look-back kernels read the knob
+    monkeypatch.setenv("CODEC_PEE_DEBUG_SKIP", "2")
+    monkeypatch.setenv("CODEC_PEE_LB_SPINS", "256")
+    bsz, h, w, T = 2, 256, 256, 2
+    covers = np.stack([synth.ct12(h, w, 520 + i) for i in range(bsz)])
+    payloads = [_bits(P.capacity(c, T) - 3, 80 + i) for i, c in enumerate(covers)]
+    codec = PeeCodec(bsz, h, w, T=T)
+    work = torch.from_numpy(covers).cuda()
+    enc = codec.embed(work, payloads, stego=work)             # would raise with CODEC_DEBUG=1
+    assert all(r.status == 0 for r in enc.records())
+    codec.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words, cover=enc.stego)
+    assert not codec.lookback_failed(enc.payload_words)
+    np.testing.assert_array_equal(enc.stego.cpu().numpy(), covers)
+    enc2 = codec.embed(torch.from_numpy(covers).cuda(), payloads)   # out of place
+    d = codec.diagnostics()
+    assert d["embed_fallback_chunks"] == 0 and d["extract_unrecovered_chunks"] == 0, d
+    for i in range(bsz):
+        st, _side = P.pee_embed(covers[i], payloads[i], T)
+        np.testing.assert_array_equal(enc2.stego[i].cpu().numpy(), st)
+
+
+@pytest.mark.gpu
 def test_gpu_lookback_timeout_in_place_raises(monkeypatch):
     """In place a predecessor may be rewriting its pixels, so there is no fallback: the
     slice gets the sticky status CODEC_PEE_ELOOKBACK and embed raises; an in-place extract
@@ -334,6 +365,7 @@ def test_gpu_lookback_timeout_in_place_raises(monkeypatch):
     torch = pytest.importorskip("torch")
     from codec_tcc_amd import _lib
     from codec_tcc_amd.pee import PeeCodec
+    monkeypatch.setenv("CODEC_DEBUG", "1")
     monkeypatch.setenv("CODEC_PEE_ONEPASS", "1")
     monkeypatch.setenv("CODEC_PEE_LB_SPINS", "256")
     bsz, h, w, T = 2, 256, 256, 2
@@ -644,6 +676,7 @@ def test_gpu_capacity_pass_forced_reorder(per_wg, delay, monkeypatch):
     from codec_tcc_amd.pee import PeeCodec
     monkeypatch.setenv("CODEC_PEE_EHIST_PER_WG", per_wg)
     if delay is not None:
+        monkeypatch.setenv("CODEC_DEBUG", "1")
         monkeypatch.setenv("CODEC_PEE_EHIST_DEBUG_DELAY", delay)
     monkeypatch.setenv("CODEC_PEE_AUTO_FUSED", "0")          # the standalone capacity pass
     tmax, bsz, h, w = 12, 4, 256, 256
