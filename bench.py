@@ -179,16 +179,41 @@ def _timed_loop(fn, budget_s):
     return px, n, t_work
 
 
-def cpu_baseline(args):
-    """The MED-PEE oracle (oracle/pee_cpu.py, vectorised numpy) on this host, 1 process, on
-    distinct synthetic slices of the benchmark's shape until the budget is used; beside it
-    the reference-path oracle (numpy restatement of src/codec.py, bit-identical to it)."""
+def _affinity():
+    """Host cores this process may run on (sorted)."""
+    try:
+        return sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):   # pragma: no cover - non-Linux
+        return list(range(os.cpu_count() or 1))
+
+
+_PIN_NEXT = None
+
+
+def _pin_worker(cores):
+    """Pool initializer: pin this worker to the next core of `cores` (one core each)."""
+    with _PIN_NEXT.get_lock():
+        i = _PIN_NEXT.value
+        _PIN_NEXT.value += 1
+    os.sched_setaffinity(0, {cores[i % len(cores)]})
+
+
+def _pinned_pool(workers, cores):
+    """A fork pool of `workers` processes, worker i pinned to cores[i]."""
+    import multiprocessing as mp
+    global _PIN_NEXT
+    ctx = mp.get_context("fork")
+    _PIN_NEXT = ctx.Value("i", 0)
+    return ctx.Pool(workers, initializer=_pin_worker, initargs=(list(cores),))
+
+
+def _cpu_baseline_work(args):
     size, kind, chars = args.size, args.kind, args.payload_chars
     px, n, t = _timed_loop(lambda s: _pee_cpu_slice(size, kind, chars, args.pee_T, s), args.cpu_seconds)
     out = {"value": round(px / t / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
            "sample": f"{n} x {size}x{size} {kind} uint16 slice runs ({CPU_DISTINCT} distinct covers, "
                      f"distinct {chars}-char payloads), T={args.pee_T}: oracle/pee_cpu.py embed + extract "
-                     f"(numpy), 1 process; seconds = timed oracle work",
+                     f"(numpy), 1 process pinned to one core; seconds = timed oracle work",
            "seconds": round(t, 2), "cpu_model": _cpu_model()}
     if args.cpu_ref_seconds > 0:
         px, n, t = _timed_loop(lambda s: _lsb_cpu_slice(size, kind, chars, s), args.cpu_ref_seconds)
@@ -196,8 +221,23 @@ def cpu_baseline(args):
             "value": round(px / t / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
             "sample": f"{n} x {size}x{size} {kind} slice runs ({CPU_DISTINCT} distinct covers): the reference's "
                       f"numpy loop (oracle/ref_cpu.py: decompose + hybrid embed + merge + "
-                      f"extract_local_planes + decode_message), 1 process",
+                      f"extract_local_planes + decode_message), 1 process pinned to one core",
             "seconds": round(t, 2)}
+    return out
+
+
+def cpu_baseline(args):
+    """The MED-PEE oracle (oracle/pee_cpu.py, vectorised numpy) on this host, ONE process
+    pinned to one core (SURVEY §8(d) / BASELINE.md: `taskset -c 0`; here a forked child with
+    sched_setaffinity to the first core this process may use), on distinct synthetic slices
+    of the benchmark's shape until the budget is used; beside it the reference-path oracle
+    (numpy restatement of src/codec.py, bit-identical to it).  Call before the GPU is
+    initialised (the child is forked)."""
+    cores = _affinity()
+    with _pinned_pool(1, cores[:1]) as pool:
+        out = pool.apply(_cpu_baseline_work, (args,))
+    out["pinned_core"] = cores[0]
+    out["cores_available"] = len(cores)
     return out
 
 
@@ -208,24 +248,28 @@ def _pool_job(job):
 
 def cpu_baseline_pool(args, which: str, per_worker: int = 0):
     """The same oracle work over a process pool (one worker per host core of
-    this GPU's share).  Forked BEFORE the GPU is initialised in this process; the covers are
-    generated in the parent first, so the wall clock holds the fork and the oracle work."""
-    import multiprocessing as mp
-    workers = args.cpu_pool
+    this GPU's share), each worker pinned to its own core.  The pool has
+    min(len(sched_getaffinity), --cpu-pool) workers: the affinity set on the GPU box can be
+    the whole machine while this GPU's share is 16 cores (--cpu-pool).  Forked BEFORE the GPU
+    is initialised in this process; the covers are generated in the parent first, so the
+    wall clock holds the fork and the oracle work."""
+    cores = _affinity()
+    workers = max(1, min(len(cores), int(args.cpu_pool)))
     per_worker = per_worker or (40 if which == "pee" else 4)   # ~2 s of oracle work per worker
     for i in range(CPU_DISTINCT):
         _cpu_img(args.size, args.kind, i)
     jobs = [(which, args.size, args.kind, args.payload_chars, args.pee_T, 2000 + i) for i in range(workers * per_worker)]
-    ctx = mp.get_context("fork")
     t0 = time.perf_counter()
-    with ctx.Pool(workers) as pool:
+    with _pinned_pool(workers, cores[:workers]) as pool:
         res = pool.map(_pool_job, jobs, chunksize=1)
     wall = time.perf_counter() - t0
     px = sum(r[0] for r in res)
     return {"value": round(px / wall / 1e6, 3), "unit": "Mpixels/s", "cores": workers, "kind": "port",
             "sample": f"{len(jobs)} x {args.size}x{args.size} {args.kind} slices ({which} oracle) over a "
-                      f"{workers}-process pool (fork; {CPU_DISTINCT} distinct covers generated beforehand), wall clock",
-            "seconds": round(wall, 2), "cpu_model": _cpu_model()}
+                      f"{workers}-process pool, one core per worker (fork; {CPU_DISTINCT} distinct covers "
+                      f"generated beforehand), wall clock",
+            "seconds": round(wall, 2), "cpu_model": _cpu_model(), "cores_available": len(cores),
+            "pinned_cores": cores[:workers]}
 
 
 # ------------------------------------------------------------------ helpers
@@ -331,7 +375,7 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
         kernels()
         if xch is not None:
             xch.start(meta, lm)
-            xch.join()
+            xch.join_records()     # no host read in the timed step; overflows() checked after
 
     for _ in range(args.warmup):
         step()
@@ -371,21 +415,24 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
     if T == "auto":
         res["T_chosen"] = {str(t): int(sum(1 for r in recs if r.T == t)) for t in sorted({r.T for r in recs})}
     if xch is not None:
-        # every timed gather was wide enough (device-side count, read once now), and this
-        # rank's rows of the last one are its own meta + map prefix (zeroed past `end`)
+        # every timed gather was wide enough (device-side count, read once now), this rank's
+        # rows of the last one are its own records, and they decode to its own metas and maps
         narrow = xch.overflows()
-        om, ol = xch.own_rows(rank)
+        own = xch.own_rows(rank)
+        om, ol = D.unpack_pee_records(own, int(D.dense_words_needed(meta)))
         res["exchange_ok"] = narrow == 0 and \
-            bool(torch.equal(om.contiguous().view(torch.uint8)[:, : _lib.PEE_META_BYTES], meta)) and \
-            bool(torch.equal(ol, D.map_prefix(meta, lm, xch.lm_words)))
-        t_g = _timed(torch, dist, world, dev, lambda: (xch.start(meta, lm), xch.join()), steps) / steps
+            bool(torch.equal(own, D.pack_pee_records(meta, lm, xch.width))) and \
+            bool(torch.equal(om, meta)) and bool(torch.equal(ol, D.map_prefix(meta, lm, ol.shape[1])))
+        t_g = _timed(torch, dist, world, dev, lambda: (xch.start(meta, lm), xch.join_records()), steps) / steps
         t_k = _timed(torch, dist, world, dev, kernels, steps) / steps
         res["distributed"] = {
             "allgather_ms": round(t_g * 1e3, 4),
-            "allgather_bytes": int(xch._out.numel() * 8),
+            "allgather_bytes": xch.gathered_bytes,
+            "record_bytes_per_slice": xch.record_bytes,
+            "dense_prefix_bytes_per_slice": 64 + 8 * int(D.dense_words_needed(meta)),
             "collectives_per_step": 1,
             "narrow_gathers": narrow,
-            "lm_words_gathered": xch.lm_words,
+            "record_map_words": xch.width,
             "kernels_only_ms_per_step": round(t_k * 1e3, 4),
             "kernels_only_value": round(B * H * W * world / t_k / 1e6, 1)}
     kern = _profile(_lib.load(), _lib, kernels, steps) if not args.no_profile else {}
@@ -751,11 +798,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     pools = {}
-    if args.cpu_seconds > 0 and world == 1 and args.cpu_pool > 0:
-        # before anything touches the GPU: the pools fork this process
-        pools["pee"] = cpu_baseline_pool(args, "pee")
-        if args.cpu_ref_seconds > 0:
-            pools["lsb"] = cpu_baseline_pool(args, "lsb")
+    cpu_base = None
+    if args.cpu_seconds > 0 and world == 1:
+        # before anything touches the GPU: the baselines run in forked, core-pinned children
+        cpu_base = cpu_baseline(args)
+        if args.cpu_pool > 0:
+            pools["pee"] = cpu_baseline_pool(args, "pee")
+            if args.cpu_ref_seconds > 0:
+                pools["lsb"] = cpu_baseline_pool(args, "lsb")
     ndev = torch.cuda.device_count()   # counting devices does not initialise the GPU
     if world > 1 and args.backend == "nccl" and ndev < world:
         sys.exit(f"bench.py: {world} ranks over RCCL need {world} GPUs, {ndev} visible "
@@ -826,8 +876,8 @@ def main():
             out["c4"] = c4
         if c2 is not None:
             out["c2"] = c2
-        if args.cpu_seconds > 0 and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args)
+        if cpu_base is not None:
+            out["cpu_baseline"] = cpu_base
             if "pee" in pools:
                 out["cpu_baseline"]["pool"] = pools["pee"]
             if "lsb" in pools and "reference_path" in out["cpu_baseline"]:

@@ -64,6 +64,7 @@ class PeeMeta(C.Structure):
 
 
 PEE_PARTIAL = 1
+PEE_RECORD_HDR_WORDS = 8   # CODEC_PEE_RECORD_HDR_WORDS: codec_pee_meta in uint64 words
 META_BYTES = C.sizeof(SliceMeta)
 PEE_META_BYTES = C.sizeof(PeeMeta)
 CODEC_PEE_ELOOKBACK = 2  # meta.status: look-back gave up (include/codec_tcc.h)
@@ -97,6 +98,8 @@ _SIGS = {
     "codec_pee_capacity": (C.c_int, [C.POINTER(PeeParams), _VP, C.c_int32, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),
     "codec_pee_embed_auto": (C.c_int, [C.POINTER(PeeParams), _VP, _VP, _VP, _VP, C.c_int32, _VP, _VP, _VP, _VP,
                                        C.c_size_t, _VP]),
+    "codec_pee_pack_records": (C.c_int, [C.c_int32, C.c_int32, _VP, _VP, C.c_int32, _VP, _VP]),
+    "codec_pee_unpack_records": (C.c_int, [C.c_int32, C.c_int32, _VP, C.c_int32, _VP, _VP, _VP]),
     "codec_quality_moments": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP, _VP, _VP, _VP]),
     "codec_block_variance": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP, _VP, _VP]),
     "codec_lsb_runs": (C.c_int, [C.c_int32, C.c_int64, C.c_int32, _VP, _VP, _VP, C.c_int64, _VP, C.c_int32, _VP]),

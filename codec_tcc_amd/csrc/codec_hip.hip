@@ -2842,10 +2842,18 @@ int codec_abi_version(void) { return CODEC_ABI_VERSION; }
 
 int codec_profile_begin(int32_t capacity) {
     if (g_prof.ev) return set_err(CODEC_EINVAL, "profile window already open");
-    if (capacity < 1) return set_err(CODEC_EINVAL, "capacity must be >= 1");
-    g_prof.ev = new hipEvent_t[2 * (size_t)capacity];
+    if (capacity < 1 || capacity > (1 << 20)) return set_err(CODEC_EINVAL, "capacity must be in 1..2^20");
+    hipEvent_t* ev = new hipEvent_t[2 * (size_t)capacity];
+    for (int i = 0; i < 2 * capacity; ++i) {
+        const hipError_t e = hipEventCreate(&ev[i]);
+        if (e != hipSuccess) {   // leave no half-open window behind (the next begin must work)
+            for (int j = 0; j < i; ++j) (void)hipEventDestroy(ev[j]);
+            delete[] ev;
+            return set_err(-(int)e, "hipEventCreate: %s", hipGetErrorString(e));
+        }
+    }
+    g_prof.ev = ev;
     g_prof.tag = new int32_t[capacity];
-    for (int i = 0; i < 2 * capacity; ++i) HIP_TRY(hipEventCreate(&g_prof.ev[i]));
     g_prof.cap = capacity;
     g_prof.n = 0;
     return 0;
@@ -2853,7 +2861,7 @@ int codec_profile_begin(int32_t capacity) {
 
 int codec_profile_end(float* ms, int32_t* tag, int32_t capacity) {
     if (!g_prof.ev) return set_err(CODEC_EINVAL, "no profile window open");
-    const int n = g_prof.n < capacity ? g_prof.n : capacity;
+    const int n = g_prof.n < capacity ? g_prof.n : (capacity > 0 ? capacity : 0);
     int rc = 0;
     for (int i = 0; i < n; ++i) {
         float t = 0.f;
@@ -2862,7 +2870,7 @@ int codec_profile_end(float* ms, int32_t* tag, int32_t capacity) {
         if (ms) ms[i] = t;
         if (tag) tag[i] = g_prof.tag[i];
     }
-    for (int i = 0; i < 2 * g_prof.cap; ++i) hipEventDestroy(g_prof.ev[i]);
+    for (int i = 0; i < 2 * g_prof.cap; ++i) (void)hipEventDestroy(g_prof.ev[i]);
     delete[] g_prof.ev;
     delete[] g_prof.tag;
     g_prof = ProfWin();

@@ -2887,6 +2887,7 @@ int codec_debug_lb_trace(unsigned long long* out, int n) {   // diagnostic build
 }
 #endif
 int codec_debug_res_trace(unsigned long long* out, int n) {   // CODEC_PEE_RES_TRACE=1 runs only
+    if (!out || n < 0) return set_err(CODEC_EINVAL, "codec_debug_res_trace: bad arguments");
     if (n > RES_TRACE_WG * 5) n = RES_TRACE_WG * 5;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_res_trace), (size_t)n * 8) == hipSuccess ? n : -1;
 }

@@ -9,8 +9,9 @@ slice's location map -- is an `all_gather_into_tensor` of fixed-size records:
 * LSB path (`RecordExchange`): codec_slice_meta + packed maps, ~1.6 KB per slice, one
   collective; never the dense s*H*W bitmaps (335 MB for 2048 x 512^2).
 * MED-PEE path (`PeeRecordExchange`): one collective of records = the 64-byte
-  codec_pee_meta of every slice + its location-map prefix [0, end], padded to a job-wide
-  width that is agreed once and then carried from step to step without a host sync (the
+  codec_pee_meta of every slice + its location map, sparse (candidate indices of the set
+  bits) or dense up to `end`, whichever the job-wide width holds (codec_pee_pack_records);
+  the width is agreed once and then carried from step to step without a host sync (the
   device checks every gather against the width its metas needed; see the class).
 
 Uneven shards (e.g. 2049 slices over 8 ranks) are padded to ceil(N / world) rows per
@@ -218,55 +219,140 @@ class RecordExchange:
 
 PEE_META_WORDS = (_lib.PEE_META_BYTES + 7) // 8
 PEE_END_FIELD = 3          # int32 index of codec_pee_meta.end
+PEE_LMCOUNT_FIELD = 9      # int32 index of codec_pee_meta.lm_count
+assert PEE_META_WORDS == _lib.PEE_RECORD_HDR_WORDS
 
 
 def map_prefix(meta, lm, lmw: int, out=None):
-    """The first `lmw` location-map words of every slice with the words past its own
-    ceil((end + 1) / 64) zeroed (the embed leaves them unwritten) -- what a gathered row holds."""
+    """The first `lmw` location-map words of every slice with every bit past its own `end`
+    cleared (the embed leaves the words past ceil((end + 1) / 64) unwritten) -- the map as a
+    gathered record carries it."""
     import torch
     ends = meta.contiguous().view(torch.int32)[:, PEE_END_FIELD].to(torch.int64)
-    words = torch.div(ends + 64, 64, rounding_mode="floor")           # ceil((end + 1) / 64)
-    cols = torch.arange(lmw, device=lm.device, dtype=torch.int64)
+    nbits = torch.clamp(ends[:, None] + 1 - 64 * torch.arange(lmw, device=lm.device, dtype=torch.int64)[None, :], 0, 64)
+    keep = torch.where(nbits >= 64, torch.full_like(nbits, -1),
+                       (torch.ones_like(nbits) << nbits) - 1)            # low nbits of each word
     if out is None:
         out = torch.empty((lm.shape[0], lmw), dtype=torch.int64, device=lm.device)
-    return out.copy_(lm[:, :lmw]).masked_fill_(cols[None, :] >= words[:, None], 0)
+    return torch.bitwise_and(lm[:, :lmw], keep, out=out)
 
 
-def _map_words_needed(ends, cap: int):
-    """Device int64 scalar: map words the slices with these `end` fields need,
-    ceil((max end + 1) / 64) clamped to [1, cap] (no host read)."""
+def record_width_needed(meta, cap: Optional[int] = None):
+    """Device int64 scalar: the record width (map words) that carries every one of these
+    slices' maps exactly -- max over slices of min(ceil(lm_count / 2), ceil((end + 1) / 64)),
+    at least 1, at most `cap` (codec_pee_pack_records' rule; no host read)."""
     import torch
-    e = ends.max().to(torch.int64)
-    return torch.clamp(torch.div(e + 64, 64, rounding_mode="floor"), 1, int(cap))
+    m = meta.contiguous().view(torch.int32)
+    end = m[:, PEE_END_FIELD].to(torch.int64)
+    cnt = m[:, PEE_LMCOUNT_FIELD].to(torch.int64)
+    need = torch.minimum(torch.div(cnt + 1, 2, rounding_mode="floor"),
+                         torch.div(end + 64, 64, rounding_mode="floor"))
+    w = need.max() if need.numel() else torch.zeros((), dtype=torch.int64, device=meta.device)
+    w = torch.clamp(w, min=1)
+    return torch.clamp(w, max=int(cap)) if cap is not None else w
+
+
+def dense_words_needed(meta):
+    """Device int64 scalar: ceil((max end + 1) / 64), the dense prefix every map fits in."""
+    import torch
+    e = meta.contiguous().view(torch.int32)[:, PEE_END_FIELD].to(torch.int64)
+    return torch.clamp(torch.div(e.max() + 64, 64, rounding_mode="floor"), min=1) if e.numel() else \
+        torch.ones((), dtype=torch.int64, device=meta.device)
+
+
+def pack_pee_records(meta, lm, width: int, out=None):
+    """[B, 64] uint8 metas + [B, lm_words] int64 maps -> [B, 8 + width] int64 records
+    (codec_pee_pack_records: the meta, then the map sparse -- ascending candidate indices of
+    its set bits -- when lm_count <= 2 * width, else dense, bits past `end` cleared).  CUDA
+    tensors run the HIP kernel; CPU tensors (the gloo tests' synthetic records) a row loop
+    of the same rule."""
+    import torch
+    B, lmw = int(meta.shape[0]), int(lm.shape[1])
+    if out is None:
+        out = torch.empty((B, PEE_META_WORDS + int(width)), dtype=torch.int64, device=meta.device)
+    if meta.is_cuda:
+        from .codec import _stream
+        _lib.check(_lib.load().codec_pee_pack_records(B, lmw, meta.data_ptr(), lm.data_ptr(), int(width),
+                                                      out.data_ptr(), _stream()), "codec_pee_pack_records")
+        return out
+    import numpy as np
+    out.zero_()
+    out[:, :PEE_META_WORDS].view(torch.uint8)[:, : _lib.PEE_META_BYTES].copy_(meta)
+    m = meta.contiguous().view(torch.int32)
+    pref = map_prefix(meta, lm, lmw).numpy().view(np.uint64)
+    for b in range(B):
+        cnt = int(m[b, PEE_LMCOUNT_FIELD])
+        if 0 <= cnt <= 2 * width:
+            bits = np.unpackbits(pref[b].view(np.uint8), bitorder="little")
+            idx = np.flatnonzero(bits)[:cnt].astype(np.uint32)
+            slots = np.zeros(2 * width, dtype=np.uint32)
+            slots[: idx.size] = idx
+            out[b, PEE_META_WORDS:] = torch.from_numpy(slots.view(np.int64))
+        else:
+            n = min(width, lmw)
+            out[b, PEE_META_WORDS: PEE_META_WORDS + n] = torch.from_numpy(pref[b, :n].view(np.int64))
+    return out
+
+
+def unpack_pee_records(records, lm_cols: int, out=None):
+    """[n, 8 + width] records -> (meta uint8 [n, 64], lm int64 [n, lm_cols]): every slice's
+    map dense, zero past its `end` (codec_pee_unpack_records on CUDA tensors)."""
+    import torch
+    n, width = int(records.shape[0]), int(records.shape[1]) - PEE_META_WORDS
+    meta = records[:, :PEE_META_WORDS].contiguous().view(torch.uint8)[:, : _lib.PEE_META_BYTES]
+    if out is None:
+        out = torch.empty((n, int(lm_cols)), dtype=torch.int64, device=records.device)
+    if records.is_cuda:
+        from .codec import _stream
+        rec = records.contiguous()
+        _lib.check(_lib.load().codec_pee_unpack_records(n, width, rec.data_ptr(), int(lm_cols), None,
+                                                        out.data_ptr(), _stream()), "codec_pee_unpack_records")
+        return meta, out
+    import numpy as np
+    out.zero_()
+    m = meta.contiguous().view(torch.int32)
+    for b in range(n):
+        cnt = int(m[b, PEE_LMCOUNT_FIELD])
+        pay = records[b, PEE_META_WORDS:].numpy()
+        if 0 <= cnt <= 2 * width:
+            idx = pay.view(np.uint32)[:cnt].astype(np.int64)
+            idx = idx[idx < 64 * lm_cols]
+            bits = np.zeros(64 * lm_cols, dtype=np.uint8)
+            bits[idx] = 1
+            out[b] = torch.from_numpy(np.packbits(bits, bitorder="little").view(np.int64))
+        else:
+            dw = min(width, lm_cols, max(0, (int(m[b, PEE_END_FIELD]) + 64) // 64))
+            out[b, :dw] = records[b, PEE_META_WORDS: PEE_META_WORDS + dw]
+    return meta, out
 
 
 class PeeRecordExchange:
     """The MED-PEE side information of every slice to every rank (north star: "an RCCL
     all-gather of per-slice location maps").
 
-    One collective per step: every slice's record is its fixed 64-byte codec_pee_meta (T, L,
-    end, maxval, status, capacity ...) followed by the first `lm_words` words of its location
-    map.  A map only means something up to candidate `end`, so `lm_words` only has to cover
-    ceil((end_max + 1) / 64), end_max over the whole job -- but that number is on the device.
-    Reading it every step would block the host on the side stream, so the width is carried
-    over instead (no host sync in ``start``):
+    One collective per step of fixed-width records (codec_pee_pack_records): every slice's
+    64-byte codec_pee_meta (T, L, end, maxval, status, capacity, lm_count ...) followed by
+    `width` words of its location map -- sparse (the candidate indices of its set bits) when
+    lm_count <= 2 * width, else the dense prefix up to `end`.  Real maps are nearly empty
+    (only overflow-prone candidates are set), so a 2048^2 ct12 slice's record is 72 bytes
+    where the dense prefix was ~15.8 KB.
 
-    * the first gather agrees it exactly: metas first, one host read of end_max (a sync of
-      the side stream only), then the maps;
+    The width that carries every map exactly is the job-wide max of
+    min(ceil(lm_count / 2), ceil((end + 1) / 64)) -- a device value.  Reading it every step
+    would block the host on the side stream, so it is carried over (no host sync in start()):
+    * the first gather agrees it exactly: metas first, one host read, then the records;
     * every gather computes, on the device, the width its own metas needed, bumps a sticky
-      device counter (``overflows()``) when it exceeded the width used, and copies the
-      figure into pinned host memory behind an event; a later ``start`` adopts a larger
-      width as soon as that event has completed (``Event.query``, never a wait);
-    * ``join(verify=True)`` (or ``verify()`` before the next embed overwrites meta/lm) makes
-      one host read of the figure and re-gathers at the wider width if the gather was too
-      narrow, so a caller that needs the maps immediately still gets exact rows.
-
-    Words past a slice's own end are zeroed before the gather (the embed leaves them
-    unwritten), so every gathered row is exactly its map zero-extended.  Uneven shards are
-    padded as in RecordExchange."""
+      device counter (``overflows()``) when it exceeded the width used, and copies the figure
+      into pinned host memory behind an event; a later ``start`` adopts a larger width as
+      soon as that event has completed (``Event.query``, never a wait);
+    * ``join()`` is exact: one host read, a re-gather at the wider width if this step's
+      maps did not fit (ADVICE r3: never cut-short rows by default), then the dense maps;
+    * ``join_records()`` is the benchmark's opt-in: no host read, the raw gathered records,
+      exact only if ``overflows()`` reads 0 afterwards.
+    Uneven shards are padded as in RecordExchange."""
 
     def __init__(self, batch: int, world: int, device, group=None, n_total: Optional[int] = None,
-                 lm_words: Optional[int] = None):
+                 width: Optional[int] = None):
         import torch
         self.group = group
         self.world = int(world)
@@ -278,38 +364,50 @@ class PeeRecordExchange:
         self.device = torch.device(device)
         self.even = self.rows * self.world == self.n_total
         self.index = None if self.even else torch.tensor(valid_rows(self.n_total, self.world), device=device)
-        self.lm_words = int(lm_words) if lm_words else 0
+        self.width = int(width) if width else 0
         self._rec_flat = None
         self._out_flat = None
         self._rec = self._out = None
+        self._dense = None
         self._cuda = self.device.type == "cuda"
-        self._need = torch.zeros((), dtype=torch.int64, device=device)
+        self._need = torch.zeros(2, dtype=torch.int64, device=device)       # [record width, dense words]
         self._overflow = torch.zeros((), dtype=torch.int64, device=device)
-        self._need_host = torch.zeros(1, dtype=torch.int64, pin_memory=self._cuda)
+        self._need_host = torch.zeros(2, dtype=torch.int64, pin_memory=self._cuda)
         self._need_ev = torch.cuda.Event() if self._cuda else None
         self._pending = False
         self._last = None
         self._side = _SideStream(device)
 
-    # -- buffers: [rows, META_WORDS + lmw] records, [world * rows, ...] gathered
-    def _buffers(self, lmw: int):
+    # -- buffers: [rows, META_WORDS + width] records, [world * rows, ...] gathered
+    def _buffers(self, width: int):
         import torch
-        width = PEE_META_WORDS + lmw
-        need = self.rows * width
+        w = PEE_META_WORDS + width
+        need = self.rows * w
         if self._rec_flat is None or self._rec_flat.numel() < need:
             self._rec_flat = torch.zeros(need, dtype=torch.int64, device=self.device)
             self._out_flat = torch.empty(self.world * need, dtype=torch.int64, device=self.device)
-        self._rec = self._rec_flat[:need].view(self.rows, width)
-        self._out = self._out_flat[: self.world * need].view(self.world * self.rows, width)
+        self._rec = self._rec_flat[:need].view(self.rows, w)
+        self._out = self._out_flat[: self.world * need].view(self.world * self.rows, w)
         return self._rec, self._out
+
+    @property
+    def lm_words(self) -> int:
+        """Map words per gathered record (the carried width)."""
+        return self.width
+
+    @property
+    def record_bytes(self) -> int:
+        """Bytes per slice record of the last gather (meta + map payload)."""
+        return (PEE_META_WORDS + self.width) * 8
+
+    @property
+    def gathered_bytes(self) -> int:
+        """Bytes every rank receives per gather."""
+        return 0 if self._out is None else int(self._out.numel()) * 8
 
     @property
     def meta_padded(self):
         return self._out[:, :PEE_META_WORDS]
-
-    @property
-    def _lm_padded(self):
-        return self._out[:, PEE_META_WORDS:]
 
     def mark(self):
         self._side.mark()
@@ -319,25 +417,26 @@ class PeeRecordExchange:
         if self._pending and (self._need_ev is None or self._need_ev.query()):
             need = int(self._need_host[0])
             self._pending = False
-            if need > self.lm_words:
-                self.lm_words = min(need, cap)
+            if need > self.width:
+                self.width = min(need, cap)
 
-    def _gather(self, meta, lm, lmw: int):
-        """Pack meta + the masked map prefix into the records and gather them (side stream)."""
+    def _gather(self, meta, lm, width: int):
+        """Pack the records (HIP kernel) and gather them (side stream)."""
         import torch
         B = meta.shape[0]
-        rec, out = self._buffers(lmw)
-        rec[:B, :PEE_META_WORDS].view(torch.uint8)[:, : _lib.PEE_META_BYTES].copy_(meta)
-        map_prefix(meta, lm, lmw, out=rec[:B, PEE_META_WORDS:])
+        rec, out = self._buffers(width)
+        pack_pee_records(meta, lm, width, out=rec[:B])
         if B < self.rows:
             rec[B:].zero_()
         gather_records(rec, self.group, out=out, rows=self.rows)
-        # the width this gather needed, over the whole job (every rank computes the same)
-        gends = out[:, :PEE_META_WORDS].contiguous().view(torch.int32)[:, PEE_END_FIELD]
-        need = _map_words_needed(gends, int(lm.shape[1]))
-        self._need.copy_(need)
-        self._overflow.add_((need > lmw).to(torch.int64))
-        self._need_host.copy_(need.view(1), non_blocking=self._cuda)
+        # the widths this gather needed, over the whole job (every rank computes the same)
+        gm = out[:, :PEE_META_WORDS].contiguous().view(torch.uint8)
+        if not self.even:
+            gm = gm.index_select(0, self.index)
+        self._need[0].copy_(record_width_needed(gm, int(lm.shape[1])))
+        self._need[1].copy_(dense_words_needed(gm))
+        self._overflow.add_((self._need[0] > width).to(torch.int64))
+        self._need_host.copy_(self._need, non_blocking=self._cuda)
         if self._need_ev is not None:
             self._need_ev.record()
         self._pending = True
@@ -351,55 +450,62 @@ class PeeRecordExchange:
         self._adopt_width(cap)
         self._last = (meta, lm)
         with self._side.enter():
-            if self.lm_words <= 0:
+            if self.width <= 0:
                 # first call: agree the width exactly (metas first, one host read)
-                self._buffers(1)
-                self._rec[: meta.shape[0], :PEE_META_WORDS].view(torch.uint8)[:, : _lib.PEE_META_BYTES].copy_(meta)
+                rec, _ = self._buffers(1)
+                rec[: meta.shape[0], :PEE_META_WORDS].view(torch.uint8)[:, : _lib.PEE_META_BYTES].copy_(meta)
                 if meta.shape[0] < self.rows:
-                    self._rec[meta.shape[0]:].zero_()
-                mrec = self._rec[:, :PEE_META_WORDS].contiguous()
-                mout = gather_records(mrec, self.group, rows=self.rows)
-                self.lm_words = int(_map_words_needed(mout.view(torch.int32)[:, PEE_END_FIELD], cap).item())
-            self.lm_words = min(self.lm_words, cap)
-            self._gather(meta, lm, self.lm_words)
+                    rec[meta.shape[0]:].zero_()
+                mout = gather_records(rec[:, :PEE_META_WORDS].contiguous(), self.group, rows=self.rows)
+                self.width = int(record_width_needed(mout.view(torch.uint8), cap).item())
+            self.width = min(self.width, cap)
+            self._gather(meta, lm, self.width)
 
     def verify(self) -> bool:
-        """One host read: was the last gather wide enough?  If not, re-gather it at the
+        """One host read: did the last gather carry every map?  If not, re-gather it at the
         needed width (meta/lm of that step must still be intact) and keep that width.
         Returns True when the last gather had to be repeated."""
         if self._last is None:
             return False
         self._side.join()
-        need = int(self._need.item())
-        if need <= self.lm_words:
+        need = int(self._need[0].item())
+        if need <= self.width:
             return False
         meta, lm = self._last
-        self.lm_words = min(need, int(lm.shape[1]))
+        self.width = min(need, int(lm.shape[1]))
         with self._side.enter():
-            self._gather(meta, lm, self.lm_words)
-            self._overflow.sub_(1)   # repaired: this step's rows are now complete
+            self._gather(meta, lm, self.width)
+            self._overflow.sub_(1)   # repaired: this step's records are now complete
         return True
 
     def overflows(self) -> int:
         """Gathers (since construction) whose width was too narrow and not repaired by
-        verify(): their map rows were cut short (one host read)."""
+        verify(): some of their maps were cut short (one host read)."""
         self._side.join()
         return int(self._overflow.item())
 
     def own_rows(self, rank: int):
-        """(meta, lm) rows of this rank in the gathered (padded) buffers."""
+        """This rank's rows of the gathered (padded) records."""
         a = rank * self.rows
-        return self.meta_padded[a: a + self.batch], self._lm_padded[a: a + self.batch]
+        return self._out[a: a + self.batch]
 
-    def join(self, verify: bool = False):
-        """(meta uint8 [n_total, PEE_META_BYTES], lm int64 [n_total, lm_words]) in global
-        slice order; a slice's full map is its row zero-extended to the codec's lm_words.
-        verify=True: exact rows guaranteed now (one host read, see verify())."""
-        import torch
-        if verify:
-            self.verify()
+    def join_records(self):
+        """The gathered records [n_total, 8 + width] in global slice order, without any host
+        read (benchmarks; check overflows() == 0 afterwards).  Decode a row with
+        unpack_pee_records."""
         self._side.join()
-        meta, lm = self.meta_padded, self._lm_padded
-        if not self.even:
-            meta, lm = meta.index_select(0, self.index), lm.index_select(0, self.index)
-        return meta.contiguous().view(torch.uint8)[:, : _lib.PEE_META_BYTES], lm
+        return self._out if self.even else self._out.index_select(0, self.index)
+
+    def join(self):
+        """(meta uint8 [n_total, PEE_META_BYTES], lm int64 [n_total, words]) in global slice
+        order, exact: every slice's location map dense up to the job's largest `end` (words =
+        ceil((max end + 1) / 64)), zero past its own end.  One host read (verify())."""
+        import torch
+        self.verify()
+        self._side.join()
+        cols = int(self._need[1].item())
+        rec = self._out if self.even else self._out.index_select(0, self.index)
+        if self._dense is None or self._dense.numel() < rec.shape[0] * cols:
+            self._dense = torch.empty(rec.shape[0] * cols, dtype=torch.int64, device=self.device)
+        meta, lm = unpack_pee_records(rec, cols, out=self._dense[: rec.shape[0] * cols].view(rec.shape[0], cols))
+        return meta.contiguous(), lm

@@ -9,6 +9,7 @@ oracle/pee_cpu.py (parity unpinned) and summarised in include/codec_tcc.h.
 from __future__ import annotations
 
 import ctypes as C
+from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -157,10 +158,7 @@ class PeeCodec:
         """(list of 0/1 bit vectors, restored cover tensor); raises if a slice overflowed."""
         recs = enc.records()
         _raise_lookback(recs)
-        bad = [i for i, r in enumerate(recs) if r.status != 0]
-        if bad:
-            raise ValueError(f"payload exceeds PEE capacity in slices {bad} "
-                             f"(T={'auto, tmax=%d' % self.tmax if self.auto else self.T})")
+        _raise_status(recs, f"T={'auto, tmax=%d' % self.tmax if self.auto else self.T}")
         words, cover = self.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words)
         host = words.cpu().numpy()
         if self.lookback_failed(enc.payload_words):
@@ -169,7 +167,16 @@ class PeeCodec:
         return [framing.unpack_bits(host[i], enc.lengths[i]) for i in range(self.B)], cover
 
 
-_CODECS = {}
+# one PeeCodec (and its zeroed workspace) per (shape, dtype, T, tmax, maxval, device); the
+# least recently used one is dropped past _CODECS_MAX entries, so varied shapes do not keep
+# GPU memory alive indefinitely (clear_codec_cache() drops them all)
+_CODECS: "OrderedDict" = OrderedDict()
+_CODECS_MAX = 8
+
+
+def clear_codec_cache():
+    """Drop every cached PeeCodec of encode()/decode() (frees their workspaces)."""
+    _CODECS.clear()
 
 
 def _codec_for(shape, dtype: str, *, T, tmax: int, maxval: Optional[int]) -> PeeCodec:
@@ -181,7 +188,44 @@ def _codec_for(shape, dtype: str, *, T, tmax: int, maxval: Optional[int]) -> Pee
     if c is None:
         c = PeeCodec(*shape, dtype=dtype, T=T, tmax=tmax, maxval=maxval)
         _CODECS[key] = c
+        while len(_CODECS) > _CODECS_MAX:
+            _CODECS.popitem(last=False)
+    else:
+        _CODECS.move_to_end(key)
     return c
+
+
+_STATUS_TEXT = {1: "payload exceeds PEE capacity", _lib.CODEC_PEE_ELOOKBACK: "in-place cursor look-back timed out"}
+
+
+def _raise_status(recs, what: str):
+    """ValueError for capacity overflows (status 1), RuntimeError naming any other code."""
+    bad = {}
+    for i, r in enumerate(recs):
+        if r.status != 0:
+            bad.setdefault(int(r.status), []).append(i)
+    if not bad:
+        return
+    if set(bad) == {1}:
+        raise ValueError(f"payload exceeds PEE capacity in slices {bad[1]} ({what})")
+    text = "; ".join(f"status {c} ({_STATUS_TEXT.get(c, 'unknown status')}) in slices {v}" for c, v in sorted(bad.items()))
+    raise RuntimeError(f"codec_pee: {text} ({what})")
+
+
+def _config_from_records(enc: "PeeEncoded") -> dict:
+    """The codec configuration of a PeeEncoded built without one (e.g. by hand): dtype from
+    the stego tensor, maxval and T from the per-slice meta records."""
+    recs = enc.records()
+    if not recs:
+        raise ValueError("PeeEncoded holds no slice records")
+    dt = "uint16" if _elem_bytes(enc.stego) == 2 else "uint8"
+    maxvals = {int(r.maxval) for r in recs}
+    if len(maxvals) != 1:
+        raise ValueError(f"slices were embedded with different maxval {sorted(maxvals)}; pass a config")
+    ts = {int(r.T) for r in recs}
+    T = ts.pop() if len(ts) == 1 else "auto"
+    tmax = max(16, max(int(r.T) for r in recs))
+    return dict(method="pee", T=T, tmax=min(tmax, 64), maxval=maxvals.pop(), dtype=dt)
 
 
 def encode(covers, payloads: Sequence, *, T=2, tmax: int = 16, maxval: Optional[int] = None) -> PeeEncoded:
@@ -198,9 +242,7 @@ def encode(covers, payloads: Sequence, *, T=2, tmax: int = 16, maxval: Optional[
     dt = "uint16" if _elem_bytes(covers) == 2 else "uint8"
     codec = _codec_for(tuple(covers.shape), dt, T=T, tmax=tmax, maxval=maxval)
     enc = codec.embed(covers, payloads)
-    bad = [i for i, r in enumerate(enc.records()) if r.status != 0]
-    if bad:
-        raise ValueError(f"payload exceeds PEE capacity in slices {bad} (T={T}, tmax={tmax})")
+    _raise_status(enc.records(), f"T={T}, tmax={tmax}")
     return enc
 
 
@@ -209,7 +251,7 @@ def decode(enc: PeeEncoded, *, restore: bool = True):
     is a numpy 0/1 vector of slice b's embedded bits, cover the restored [B,H,W] tensor
     (None with restore=False)."""
     _require_gpu()
-    cfg = enc.config
+    cfg = enc.config or _config_from_records(enc)
     codec = _codec_for(tuple(enc.stego.shape), cfg.get("dtype", "uint16"), T=cfg.get("T", 2),
                        tmax=cfg.get("tmax", 16), maxval=cfg.get("maxval"))
     bits, cover = codec.decode(enc)

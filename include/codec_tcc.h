@@ -287,6 +287,23 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
                       const uint64_t* lm, void* cover_out, uint64_t* payload_out, void* workspace,
                       size_t workspace_bytes, void* stream);
 
+/* ---- exchange records of the MED-PEE side information (north star: "an RCCL all-gather of
+ * per-slice location maps"; no reference counterpart -- the reference is
+ * single-process).  Record b = CODEC_PEE_RECORD_HDR_WORDS uint64 words holding slice b's
+ * codec_pee_meta, then `width` words of location map:
+ *   sparse (meta.lm_count <= 2 * width): the candidate indices of the map's set bits,
+ *          ascending, as uint32 (two per word), unused slots zero;
+ *   dense  (otherwise): map words 0 .. width-1 with every bit past `end` zero.
+ * Slice b's map travels exactly when width >= min(ceil(lm_count / 2), ceil((end + 1) / 64)).
+ * meta/lm: codec_pee_embed outputs ([B], [B][lm_words]); records: [B][HDR + width]. */
+#define CODEC_PEE_RECORD_HDR_WORDS 8
+int codec_pee_pack_records(int32_t B, int32_t lm_words, const codec_pee_meta* meta, const uint64_t* lm,
+                           int32_t width, uint64_t* records, void* stream);
+/* Inverse for n gathered records: meta_out[n] (may be NULL) and lm_out[n][lm_cols] (may be
+ * NULL) = each slice's location map, dense, zero past `end` and truncated to lm_cols words. */
+int codec_pee_unpack_records(int32_t n, int32_t width, const uint64_t* records, int32_t lm_cols,
+                             codec_pee_meta* meta_out, uint64_t* lm_out, void* stream);
+
 /* ---- stego quality (replaces the metric arithmetic of src/mse.py: AnalisadorMSE.
  * calcular_mse :74-117, calcular_psnr :119-133, calcular_ssim_simples :135-177 and the
  * difference statistics of analisar_par_imagens :201-207).  One read-only pass over two

@@ -20,6 +20,7 @@ def _args(**kw):
 def test_cpu_baseline_small():
     r = bench.cpu_baseline(_args())
     assert r["kind"] == "port" and r["cores"] == 1 and r["value"] > 0 and r["unit"] == "Mpixels/s"
+    assert r["pinned_core"] == min(os.sched_getaffinity(0)) and r["cores_available"] == len(os.sched_getaffinity(0))
     assert "pee_cpu" in r["sample"] and r["reference_path"]["value"] > 0
     assert "reference_path" not in bench.cpu_baseline(_args(cpu_ref_seconds=0))
 
@@ -28,6 +29,23 @@ def test_cpu_baseline_pool_small():
     for which in ("pee", "lsb"):
         r = bench.cpu_baseline_pool(_args(), which, per_worker=1)
         assert r["cores"] == 2 and r["value"] > 0 and "pool" in r["sample"] and which in r["sample"]
+        assert r["pinned_cores"] == sorted(os.sched_getaffinity(0))[:2]
+    # the pool never exceeds the cores this process may use
+    big = bench.cpu_baseline_pool(_args(cpu_pool=10_000), "pee", per_worker=1)
+    assert big["cores"] == len(os.sched_getaffinity(0)) == big["cores_available"]
+
+
+def test_pinned_workers_run_on_their_core():
+    cores = sorted(os.sched_getaffinity(0))[:2]
+    with bench._pinned_pool(2, cores) as pool:
+        got = sorted(pool.map(_affinity_of_worker, range(8), chunksize=1))
+    assert set(got) <= {frozenset([c]) for c in cores}
+
+
+def _affinity_of_worker(_i):
+    import time
+    time.sleep(0.05)
+    return frozenset(os.sched_getaffinity(0))
 
 
 def test_payload_equal_masks_lengths():

@@ -63,19 +63,78 @@ def _lsb_records(lo, hi, mw):
     return meta, maps
 
 
-def _pee_records(lo, hi, lm_words):
-    """codec_pee_meta rows with end = 37 * g + 5 (g = global slice id) and location maps
-    whose words before the end carry g; words past `end` are garbage the exchange must drop."""
+def _pee_records(lo, hi, lm_words, heavy=()):
+    """codec_pee_meta rows with end = 37 * g + 5 (g = global slice id); the location map of
+    slice g has bits 3g+1 and 5g+2 set (a few overflow candidates, sparse records) -- or, for
+    g in `heavy`, every third candidate up to `end` (an overflow-heavy slice, e.g. uniform
+    u16 data, whose record goes dense) -- and garbage (-7) past `end`, which the exchange
+    must drop.  lm_count = the map's popcount, as the embed writes it."""
+    import numpy as np
     B = hi - lo
     meta = torch.zeros((B, _lib.PEE_META_BYTES), dtype=torch.uint8)
     lm = torch.full((B, lm_words), -7, dtype=torch.int64)
     for i in range(B):
         g = lo + i
+        end = 37 * g + 5
+        bits = np.zeros(64 * lm_words, dtype=np.uint8)
+        if g in heavy:
+            bits[0: end + 1: 3] = 1
+        else:
+            bits[[3 * g + 1, 5 * g + 2]] = 1
+        bits[end + 1:] = 0
+        nw = (end + 1 + 63) // 64
+        words = np.packbits(bits, bitorder="little").view(np.int64)
+        lm[i, :nw] = torch.from_numpy(words[:nw].copy())
+        if (end + 1) % 64:                       # garbage past `end` inside its last word too
+            lm[i, nw - 1] |= torch.tensor(-1 << ((end + 1) % 64), dtype=torch.int64)
         m = meta[i].view(torch.int32)
-        m[0], m[2], m[3], m[4] = 2, 1000 + g, 37 * g + 5, 64 * lm_words
-        nw = (37 * g + 5 + 1 + 63) // 64
-        lm[i, :nw] = torch.arange(nw, dtype=torch.int64) * 1000 + g
+        m[0], m[2], m[3], m[4], m[9] = 2, 1000 + g, end, 64 * lm_words, int(bits.sum())
     return meta, lm
+
+
+def _want_map(g, lm_words, heavy=()):
+    """Slice g's map as _pee_records defines it, dense, zero past `end`."""
+    import numpy as np
+    end = 37 * g + 5
+    bits = np.zeros(64 * lm_words, dtype=np.uint8)
+    if g in heavy:
+        bits[0: end + 1: 3] = 1
+    else:
+        bits[[3 * g + 1, 5 * g + 2]] = 1
+    bits[end + 1:] = 0
+    return torch.from_numpy(np.packbits(bits, bitorder="little").view(np.int64).copy())
+
+
+def _want_width(gs, lm_words, heavy=()):
+    """max over slices of min(ceil(popcount / 2), ceil((end + 1) / 64)), at least 1."""
+    w = 1
+    for g in gs:
+        cnt = int(sum(bin(int(x) & (2**64 - 1)).count("1") for x in _want_map(g, lm_words, heavy)))
+        w = max(w, min((cnt + 1) // 2, (37 * g + 5 + 64) // 64))
+    return w
+
+
+def test_pee_records_pack_unpack_cpu():
+    """Sparse and dense records (codec_pee_pack_records' rule) round-trip every map exactly,
+    and the width rule picks the shorter form per slice."""
+    lm_words = 16
+    heavy = (5,)
+    meta, lm = _pee_records(0, 8, lm_words, heavy)
+    need = int(D.record_width_needed(meta, lm_words))
+    # sparse slices need ceil(2 / 2) = 1 word; slice 5 (end 190, 64 set bits) needs min(32, 3) = 3
+    assert need == 3
+    for width in (need, need + 4):
+        rec = D.pack_pee_records(meta, lm, width)
+        assert tuple(rec.shape) == (8, D.PEE_META_WORDS + width)
+        m2, l2 = D.unpack_pee_records(rec, lm_words)
+        assert torch.equal(m2, meta)
+        for g in range(8):
+            assert torch.equal(l2[g], _want_map(g, lm_words, heavy)), (width, g)
+        assert torch.equal(l2, D.map_prefix(meta, lm, lm_words))
+    # too narrow a width cuts the heavy slice's map (what overflows() counts)
+    rec = D.pack_pee_records(meta, lm, 1)
+    _m, l1 = D.unpack_pee_records(rec, lm_words)
+    assert not torch.equal(l1[5], _want_map(5, lm_words, heavy))
 
 
 def _worker(rank, world, port, n_slices, q):
@@ -101,44 +160,42 @@ def _worker(rank, world, port, n_slices, q):
         ok &= not gp[g, w:].any()
     ok &= torch.equal(D.pack_records(meta, maps, out=torch.zeros((B, D.record_words(5)), dtype=torch.int64)),
                       xch.own_rows(rank))
-    # ---- MED-PEE records: metas, then location-map prefixes up to the job's largest end
+    # ---- MED-PEE records: meta + the map, sparse or dense (slice 2 is overflow-heavy)
     lm_words = 16
-    pmeta, lm = _pee_records(lo, hi, lm_words)
+    heavy = (2,)
+    pmeta, lm = _pee_records(lo, hi, lm_words, heavy)
     px = D.PeeRecordExchange(B, world, "cpu", n_total=n_slices)
     px.mark()
     px.start(pmeta, lm)
     gmeta, glm = px.join()
     end_max = 37 * (n_slices - 1) + 5
-    ok &= px.lm_words == (end_max + 1 + 63) // 64
-    ok &= tuple(gmeta.shape) == (n_slices, _lib.PEE_META_BYTES) and tuple(glm.shape) == (n_slices, px.lm_words)
+    ok &= px.width == _want_width(range(n_slices), lm_words, heavy)
+    ok &= tuple(gmeta.shape) == (n_slices, _lib.PEE_META_BYTES)
+    ok &= tuple(glm.shape) == (n_slices, (end_max + 1 + 63) // 64)
     for g in range(n_slices):
         m = gmeta[g].contiguous().view(torch.int32)
         ok &= int(m[2]) == 1000 + g and int(m[3]) == 37 * g + 5
-        nw = (37 * g + 5 + 1 + 63) // 64
-        ok &= torch.equal(glm[g, :nw], torch.arange(nw, dtype=torch.int64) * 1000 + g)
-    om, ol = px.own_rows(rank)
-    ok &= torch.equal(om.contiguous().view(torch.uint8)[:, : _lib.PEE_META_BYTES], pmeta)
-    # words past each slice's own end were garbage (-7): the gathered rows carry zeros there
-    for i in range(B):
-        nw = (37 * (lo + i) + 5 + 1 + 63) // 64
-        ok &= torch.equal(ol[i, :nw], lm[i, :nw]) and not ol[i, nw:].any()
+        ok &= torch.equal(glm[g], _want_map(g, lm_words, heavy)[: glm.shape[1]])
+    own = px.own_rows(rank)
+    ok &= torch.equal(own, D.pack_pee_records(pmeta, lm, px.width))
     ok &= px.overflows() == 0
-    # ---- a later step whose maps are longer: the carried width is too narrow for that
-    # gather (the device counts it), verify() re-gathers it at the needed width, and the
-    # following step adopts that width without any host read
-    w0 = px.lm_words
-    pmeta2, lm2 = _pee_records(lo, hi, lm_words)
-    for i in range(B):
-        pmeta2[i].view(torch.int32)[3] = 64 * (w0 + 1) + i          # end -> w0 + 2 words
-        lm2[i, : w0 + 2] = torch.arange(w0 + 2, dtype=torch.int64) + 100 * (lo + i)
+    # ---- a later step whose maps need more: the carried width is too narrow for that
+    # gather (the device counts it); join() is exact anyway (it re-gathers at the needed
+    # width), and the following step adopts that width without any host read
+    w0 = px.width
+    heavy2 = tuple(range(n_slices))                                  # every slice overflow-heavy
+    pmeta2, lm2 = _pee_records(lo, hi, lm_words, heavy2)
+    w1 = _want_width(range(n_slices), lm_words, heavy2)
     px.start(pmeta2, lm2)
-    ok &= px.overflows() == 1 and px.lm_words == w0
-    ok &= px.verify() is True and px.overflows() == 0 and px.lm_words == w0 + 2
-    gmeta2, glm2 = px.join()
+    ok &= px.overflows() == int(w1 > w0) and px.width == w0
+    rec_cut = px.join_records()                                      # the benchmark's unverified view
+    ok &= rec_cut.shape[1] == D.PEE_META_WORDS + w0
+    gmeta2, glm2 = px.join()                                         # exact by default
+    ok &= px.overflows() == 0 and px.width == w1
     for g in range(n_slices):
-        ok &= torch.equal(glm2[g, : w0 + 2], torch.arange(w0 + 2, dtype=torch.int64) + 100 * g)
+        ok &= torch.equal(glm2[g], _want_map(g, lm_words, heavy2)[: glm2.shape[1]])
     px.start(pmeta2, lm2)
-    ok &= px.lm_words == w0 + 2 and px.overflows() == 0 and px.verify() is False
+    ok &= px.width == w1 and px.overflows() == 0 and px.verify() is False
     # ---- the plain gather helper with equal shards
     rec = D.pack_records(*_lsb_records(lo, hi, 4))
     ok &= D.gather_records(rec, rows=D.shard_rows(n_slices, world)).shape[0] == world * D.shard_rows(n_slices, world)

@@ -22,9 +22,18 @@ def _free_port():
     return p
 
 
-def _covers(n, h, w, dev):
+def _covers(n, h, w, dev, heavy=()):
+    """ct12 slices; the slices in `heavy` hold only the values {0, 1, 65534, 65535}, so about
+    half their candidates are overflow-prone at any T (their location maps are dense)."""
     from codec_tcc_amd import synth
-    return torch.from_numpy(np.stack([synth.GENERATORS["ct12"](h, w, 60 + i) for i in range(n)])).to(dev)
+    out = []
+    for i in range(n):
+        if i in heavy:
+            v = np.random.default_rng(900 + i).integers(0, 4, (h, w))
+            out.append(np.where(v < 2, v, 65532 + v).astype(np.uint16))
+        else:
+            out.append(synth.GENERATORS["ct12"](h, w, 60 + i))
+    return torch.from_numpy(np.stack(out)).to(dev)
 
 
 def _worker(rank, world, port, n, q):
@@ -41,13 +50,13 @@ def _worker(rank, world, port, n, q):
         from codec_tcc_amd import distributed as D
         from codec_tcc_amd.pee import PeeCodec
         H = W = 256
-        allc = _covers(n, H, W, dev)
+        allc = _covers(n, H, W, dev, heavy=(1,))      # slice 1 overflow-heavy: a dense record
         pays = [framing.to_bits(synth.payload(96, 500 + g)) for g in range(n)]
         lo, hi = D.shard_range(n, world, rank)
         B = hi - lo
         # ---- MED-PEE: the whole batch locally (reference rows), then this rank's shard
         full = PeeCodec(n, H, W, dtype="uint16", T=2, device=dev)
-        ref = full.embed(allc, pays)
+        ref = full.embed(allc, pays, check=False)
         codec = PeeCodec(B, H, W, dtype="uint16", T=2, device=dev)
         enc = codec.embed(allc[lo:hi].contiguous(), pays[lo:hi], check=False)
         xch = D.PeeRecordExchange(B, world, dev, n_total=n)
@@ -60,9 +69,10 @@ def _worker(rank, world, port, n, q):
         ok &= tuple(gmeta.shape) == (n, _lib.PEE_META_BYTES)
         ok &= bool(torch.equal(gmeta, ref.meta))
         recs = ref.records()
-        for g in range(n):
-            nw = (recs[g].end + 1 + 63) // 64
-            ok &= nw <= glm.shape[1] and bool(torch.equal(glm[g, :nw], ref.lm[g, :nw]))
+        ok &= recs[1].lm_count > 2 * xch.width and recs[0].lm_count <= 2 * xch.width   # dense and sparse rows
+        ok &= glm.shape[1] == max((r.end + 64) // 64 for r in recs)
+        ok &= bool(torch.equal(glm, D.map_prefix(ref.meta, ref.lm, glm.shape[1])))
+        ok &= xch.overflows() == 0
         # ---- LSB records: own rows of the gathered records equal the local packing
         lcodec = ct.Codec(B, H, W, dtype="uint16", beta=0.4, block=16, device=dev)
         pl = ct.make_payloads([synth.payload(96, 700 + g) for g in range(lo, hi)], dev)
@@ -172,8 +182,20 @@ def _rccl_worker(port, q):
             gmeta, glm = xch.join()
             torch.cuda.synchronize()
             ok &= bool(torch.equal(gmeta, enc.meta))
-            ok &= bool(torch.equal(glm, D.map_prefix(enc.meta, enc.lm, xch.lm_words)))
+            ok &= bool(torch.equal(glm, D.map_prefix(enc.meta, enc.lm, glm.shape[1])))
         ok &= xch.overflows() == 0 and D.agree_max(7, device=dev) == 7
+        # a later step whose maps need a wider record (an overflow-heavy slice
+        # appears): join() -- no explicit verify() -- still returns every map exactly
+        w0 = xch.width
+        hc = _covers(n, H, W, dev, heavy=(2,))
+        enc2 = codec.embed(hc, [framing.to_bits(synth.payload(96, 40 + g)) for g in range(n)], check=False)
+        xch.mark()
+        xch.start(enc2.meta, enc2.lm)
+        gmeta, glm = xch.join()
+        torch.cuda.synchronize()
+        ok &= xch.width > w0 and xch.overflows() == 0
+        ok &= bool(torch.equal(gmeta, enc2.meta))
+        ok &= bool(torch.equal(glm, D.map_prefix(enc2.meta, enc2.lm, glm.shape[1])))
         lcodec = ct.Codec(n, H, W, dtype="uint16", beta=0.4, block=16, device=dev)
         pl = ct.make_payloads([synth.payload(96, 70 + g) for g in range(n)], dev)
         lenc = lcodec.encode(allc, pl)
@@ -207,3 +229,35 @@ def test_exchanges_over_rccl_world1():
             p.kill()
             p.join(timeout=10)
     assert ok, err
+
+
+def test_pee_record_kernels_match_host_rule():
+    """codec_pee_pack_records / codec_pee_unpack_records on real embed outputs (ct12 slices
+    with near-empty maps, one overflow-heavy slice) equal the host restatement of the record
+    rule (distributed.pack_pee_records on CPU tensors) word for word, and unpacking returns
+    every map exactly whenever the width is the needed one or wider."""
+    from codec_tcc_amd import distributed as D
+    from codec_tcc_amd import framing, synth
+    from codec_tcc_amd.pee import PeeCodec
+    dev = torch.device("cuda", 0)
+    n, H, W = 5, 256, 256
+    covers = _covers(n, H, W, dev, heavy=(3,))
+    codec = PeeCodec(n, H, W, dtype="uint16", T=2, device=dev)
+    enc = codec.embed(covers, [framing.to_bits(synth.payload(64 + 40 * g, 10 + g)) for g in range(n)], check=False)
+    lm_cpu, meta_cpu = enc.lm.cpu(), enc.meta.cpu()
+    need = int(D.record_width_needed(enc.meta, codec.lm_words))
+    assert need == int(D.record_width_needed(meta_cpu, codec.lm_words)) > 1
+    cols = int(D.dense_words_needed(enc.meta))
+    want = D.map_prefix(meta_cpu, lm_cpu, cols)
+    for width in (1, need, need + 3):
+        rec = D.pack_pee_records(enc.meta, enc.lm, width)
+        torch.cuda.synchronize()
+        assert torch.equal(rec.cpu(), D.pack_pee_records(meta_cpu, lm_cpu, width)), width
+        meta2, lm2 = D.unpack_pee_records(rec, cols)
+        assert torch.equal(meta2.cpu(), meta_cpu)
+        _m, lm2_cpu = D.unpack_pee_records(rec.cpu(), cols)
+        assert torch.equal(lm2.cpu(), lm2_cpu), width
+        if width >= need:
+            assert torch.equal(lm2.cpu(), want), width
+        else:
+            assert not torch.equal(lm2.cpu(), want)      # the heavy slice is cut: what overflows() flags

@@ -660,6 +660,42 @@ def test_package_encode_decode_pee(T):
         ct.encode(covers[0], msgs[0], method="jxl")
 
 
+def test_status_codes_are_named():
+    """only status 1 is reported as a capacity overflow; any other code raises a
+    RuntimeError that names it."""
+    from types import SimpleNamespace as NS
+
+    from codec_tcc_amd import pee
+    pee._raise_status([NS(status=0), NS(status=0)], "x")
+    with pytest.raises(ValueError, match=r"exceeds PEE capacity in slices \[1\]"):
+        pee._raise_status([NS(status=0), NS(status=1)], "x")
+    with pytest.raises(RuntimeError, match=r"status 2 \(in-place cursor look-back timed out\) in slices \[0\]"):
+        pee._raise_status([NS(status=2), NS(status=1)], "x")
+    with pytest.raises(RuntimeError, match=r"status 7 \(unknown status\)"):
+        pee._raise_status([NS(status=7)], "x")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,maxval", [("u8", None), ("ct12", 4095)])
+def test_package_decode_without_config(kind, maxval):
+    """a PeeEncoded built by hand (config {}) decodes with the dtype of its stego
+    tensor and the maxval / T of its meta records, not a uint16 / 65535 default."""
+    torch = pytest.importorskip("torch")
+    import codec_tcc_amd as ct
+    from codec_tcc_amd import framing
+    from codec_tcc_amd.pee import PeeEncoded
+    covers = np.stack([synth.GENERATORS[kind](128, 128, 40 + i) for i in range(2)])
+    msgs = ["abc", "hand-built record"]
+    enc = ct.encode(torch.from_numpy(covers).cuda(), msgs, method="pee", T="auto", maxval=maxval)
+    bare = PeeEncoded(enc.stego, enc.lm, enc.meta, enc.lengths, enc.payload_words)
+    assert bare.config == {}
+    got, cover = ct.decode(bare)
+    assert cover.dtype == enc.stego.dtype
+    np.testing.assert_array_equal(cover.cpu().numpy(), covers)
+    for i, m in enumerate(msgs):
+        np.testing.assert_array_equal(got[i], framing.to_bits(m))
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("per_wg,delay", [("4096", None), ("512", None), ("64", None), ("512", "1"), ("512", "4"),
                                           ("64", "8"), ("64", "15"), ("100000", "2")])
