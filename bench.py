@@ -88,7 +88,7 @@ def pmc_traffic(kernel: str, b: int, h: int, w: int, kind: str, targs=None):
     instantiations by template argument (e.g. {2: "true"} = the in-place PEE kernels);
     the lookup succeeds only when exactly one instantiation matches."""
     d = None
-    for name in ("pmc_traffic.json", "pmc_traffic_c3.json"):   # headline shape, C3 shape
+    for name in ("pmc_traffic.json", "pmc_traffic_c3.json", "pmc_traffic_c2.json"):   # headline, C3, C2 shapes
         path = os.path.join(REPO, "profiles", name)
         try:
             with open(path) as f:
