@@ -961,7 +961,7 @@ __device__ __forceinline__ uint32_t ld_agent(uint32_t* p) {
 #endif
 struct NoFallback {
     static constexpr bool can = false;
-    __device__ uint32_t operator()(int) const { return 0u; }
+    __device__ u64 operator()(int) const { return 0ull; }
 };
 
 // expandable, non-overflow candidates of chunk j (the embed's aggregate), counted by the
@@ -973,10 +973,10 @@ struct EmbedCount {
     int W, CR;
     uint32_t items;
     int Tthr, maxval;
-    __device__ uint32_t operator()(int j) const {
+    __device__ u64 operator()(int j) const {   // expandable | unsafe << 32 (a status word's value)
         typedef typename Vec8<T>::type V;
         const int lane = threadIdx.x & 63;
-        uint32_t n = 0;
+        uint32_t n = 0, un = 0;
         for (int u = 0; u < PEE_CHUNK / 64; ++u) {
             const uint32_t it = (uint32_t)j * PEE_CHUNK + (uint32_t)(u * 64 + lane);
             if (it >= items) break;
@@ -989,11 +989,15 @@ struct EmbedCount {
                 const PeeCand pc = pee_classify((int)get_px(v1, 2 * q + 1), (int)get_px(v1, 2 * q), (int)get_px(v0, 2 * q + 1),
                                                 (int)get_px(v0, 2 * q), Tthr, maxval);
                 n += (pc.expand && pc.safe) ? 1u : 0u;
+                un += pc.safe ? 0u : 1u;
             }
         }
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) n += __shfl_xor(n, o, 64);
-        return n;
+        for (int o = 32; o >= 1; o >>= 1) {
+            n += __shfl_xor(n, o, 64);
+            un += __shfl_xor(un, o, 64);
+        }
+        return (u64)n | ((u64)un << 32);
     }
 };
 
@@ -1007,7 +1011,7 @@ struct ExtractCount {
     int W, CR;
     uint32_t items;
     int end, Tthr;
-    __device__ uint32_t operator()(int j) const {
+    __device__ u64 operator()(int j) const {
         typedef typename Vec8<T>::type V;
         const int lane = threadIdx.x & 63;
         uint32_t n = 0;
@@ -1042,11 +1046,25 @@ struct ExtractCount {
 #ifndef PEE_LB_PARTIAL
 #define PEE_LB_PARTIAL 1   // embed: a partial sum of the published words may end the wait (past `end`)
 #endif
+// Status words carry two counts (round 4): bits 0-31 the chunk's (or prefix's) expandable /
+// inner count, bits 32-61 its unsafe-candidate count (the embed's location-map bits, so the
+// chunk holding `end` learns lm_count from the look-back itself: no meta atomics, no memset).
+// The two fields are summed separately (64-bit each), so a sum can never carry between them.
+#define LB_LO(w) ((w) & 0xFFFFFFFFull)
+#define LB_HI(w) (((w) >> 32) & 0x3FFFFFFFull)
+struct LbSum {
+    u64 e, u;   // summed low / high fields of the predecessors
+};
+__device__ __forceinline__ u64 wave_sum_u64(u64 v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
 template <typename F>
-__device__ uint32_t lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, uint32_t spin_max, const F& count,
-                                 uint32_t* done = nullptr, uint32_t sat = 0) {
+__device__ LbSum lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, uint32_t spin_max, const F& count,
+                              uint32_t* done = nullptr, uint32_t sat = 0) {
     const int lane = threadIdx.x & 63;
-    uint32_t excl = 0;
+    LbSum ex{0ull, 0ull};
     int p = c - 1;            // the highest predecessor not summed yet
     uint32_t spins = 0;
     for (;;) {
@@ -1068,15 +1086,13 @@ __device__ uint32_t lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, 
             const int first = inc ? (int)__builtin_ctzll(inc) : 64;        // nearest inclusive
             const u64 need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);  // lanes 0..first
             if (notready & need) {
-                if (done && ld_agent(done)) return sat;
+                if (done && ld_agent(done)) return LbSum{(u64)sat, 0ull};
                 if (done && (PEE_LB_PARTIAL)) {
                     // the published words already bound the prefix from below (aggregates of
                     // disjoint chunks, or an inclusive prefix): reaching `sat` (= L) places this
                     // chunk past `end` without waiting for the missing ones
-                    uint32_t lo = (lane <= first && fl != 0u) ? (uint32_t)w : 0u;
-#pragma unroll
-                    for (int o = 32; o >= 1; o >>= 1) lo += __shfl_xor(lo, o, 64);
-                    if (excl + lo >= sat) return excl + lo;
+                    const u64 lo = wave_sum_u64((lane <= first && fl != 0u) ? LB_LO(w) : 0ull);
+                    if (ex.e + lo >= sat) return LbSum{ex.e + lo, 0ull};
                 }
                 if (++spins <= spin_max) {
                     __builtin_amdgcn_s_sleep(PEE_LB_SLEEP);
@@ -1086,7 +1102,7 @@ __device__ uint32_t lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, 
                 }
                 if constexpr (!F::can) {
                     *timeout = true;
-                    return excl;
+                    return ex;
                 } else {
                     // the missing aggregates from the pixels, one chunk per round of the wave; a
                     // chunk that published meanwhile keeps its own word (CAS from what was read)
@@ -1094,9 +1110,9 @@ __device__ uint32_t lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, 
                     while (m) {
                         const int l = (int)__builtin_ctzll(m);
                         m &= m - 1ull;
-                        const uint32_t a = count(pr - l);
+                        const u64 a = count(pr - l);   // packed like a status word's value
                         if (lane == l) {
-                            const u64 mine = LB_AGG | (u64)a;
+                            const u64 mine = LB_AGG | a;
                             atomicCAS(reinterpret_cast<unsigned long long*>(st + idx), (unsigned long long)w,
                                       (unsigned long long)mine);
                             w = mine;
@@ -1107,15 +1123,13 @@ __device__ uint32_t lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, 
                     spins = 0;
                 }
             }
-            uint32_t v = lane <= first ? (uint32_t)w : 0u;
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-            excl += v;
-            if (first < 64) return excl;
+            ex.e += wave_sum_u64(lane <= first ? LB_LO(w) : 0ull);
+            ex.u += wave_sum_u64(lane <= first ? LB_HI(w) : 0ull);
+            if (first < 64) return ex;
             // embed (done != nullptr): a partial sum that already reaches `sat` (= L) places the
             // chunk past `end`; the caller only compares the prefix with L, and publishes it as a
             // saturated inclusive value, as the done-flag path does
-            if (done && excl >= sat) return excl;
+            if (done && ex.e >= sat) return ex;
         }
         if (!reload) p -= 64 * LB_WIN;
     }
@@ -1211,7 +1225,27 @@ __device__ unsigned long long g_lb_trace[LB_TRACE_SLOTS * 12];
 #endif
 #define PEE_MODE_CMAJOR 1
 #define PEE_MODE_NOTICKET 2
+// self-cleaning out-of-place look-back (round 4): no zeroing launch before the pass.  The
+// workspace holds TWO status-word buffers; a call uses buffer `par` and clears its own words
+// of the other one for the next call.  `par` is the parity of the call count, which every
+// workgroup learns from the returning atomic that counts its arrival: per slice 8 shard
+// counters (chunk c counts on shard c % 8, n_g arrivals per call), call index = old / n_g.
+// The finished flag is doubled the same way; meta is written without atomics (status by the
+// chunk holding `end`, lm_count from the look-back's second field).  Calls that still zero
+// (in place, ticket modes) use buffer 1 and finished flag 1 and reset the counters, so the
+// next self-cleaning call (index 0: buffer 0) starts clean.
+#define PEE_MODE_SC 8
 #define PEE_CTL_WORDS(B) (32 + 32 * (size_t)(B))
+#define PEE_LINE_TICKET 0
+#define PEE_LINE_FIN0 1
+#define PEE_LINE_FIN1 4
+#define PEE_LINE_ARR 8    // 8 x u64 shard counters (words 8..23 of the slice's 32-word line)
+__device__ __forceinline__ int pee_call_parity(uint32_t* line, int c, int nchunks) {
+    const int g = c & 7;
+    const u64 old = atomicAdd(reinterpret_cast<unsigned long long*>(line + PEE_LINE_ARR + 2 * g), 1ull);
+    const uint32_t ng = (uint32_t)((nchunks - g + 7) >> 3);   // chunks of this slice on shard g
+    return (int)((old / ng) & 1ull);
+}
 #define PEE_SKIP 0xFFFFFFFFu
 #define PEE_STOP 0xFFFFFFFEu
 template <typename T, bool NT, bool INPLACE>
@@ -1224,7 +1258,9 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
     typedef typename Vec8<T>::type V;
     __shared__ u64 sh64[8];
     __shared__ uint32_t sh[8];
-    __shared__ uint32_t s_v, s_excl;
+    __shared__ uint32_t s_v, s_excl, s_uexcl, s_uns[4];
+    __shared__ int s_par;
+    const bool sc = !INPLACE && (mode & PEE_MODE_SC);
     __shared__ uint32_t lm32[4 * PEE_TILE / 32];
     __shared__ u64 s_pay[192];   // the slice's payload words when pw <= 192 (see below)
     const bool pay_st = pw <= 192;
@@ -1243,8 +1279,9 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
         int b, j;
         if (!pee_slot(v, B, nchunks, g8, &b, &j)) continue;   // uniform; no barrier passed
         LB_STAMP(0);
-        uint32_t* tick = ctl + 32 + 32 * (size_t)b;
-        u64* st = status_all + (size_t)b * nchunks;
+        uint32_t* line = ctl + 32 + 32 * (size_t)b;
+        uint32_t* tick = line + PEE_LINE_TICKET;
+        const size_t stride = (size_t)B * nchunks;   // one status-word buffer
         const uint32_t L = (uint32_t)max(0, lengths[b]);
         const int Tthr = tps ? tps[b] : T0;   // per-slice threshold (capacity control) or one for all
         codec_pee_meta* M = meta_all + b;
@@ -1252,47 +1289,62 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
         T* dst = stego + b * npx;
         V a0[4], a1[4];
         size_t o0[4];
-        // out of place the finished flag is read BEFORE the chunk's pixels are requested, so
-        // waiting for it does not wait for them too (vmcnt counts in issue order)
-        const uint32_t dn0 = !INPLACE ? ld_agent(tick + 1) : 0u;   // every lane (one request): no branch
+        // out of place the finished flags are read BEFORE the chunk's pixels are requested, so
+        // waiting for them does not wait for the pixels too (vmcnt counts in issue order)
+        const uint32_t dnA = !INPLACE ? ld_agent(line + (sc ? PEE_LINE_FIN0 : PEE_LINE_FIN1)) : 0u;   // every lane
+        const uint32_t dnB = (!INPLACE && sc) ? ld_agent(line + PEE_LINE_FIN1) : 0u;
         // out of place: the slot's own chunk j is loaded while the ticket is in flight (the
         // ticket equals j unless workgroups were dispatched out of order)
         if (!INPLACE) pee_load_chunk<T, NT>(src, W, CR, items, j, a0, a1, o0);
         if (tid == 0) {
             uint32_t cc = PEE_SKIP;
+            int par = 1;
             if (!INPLACE) {
                 // a flag seen set was set before this chunk started, so `end` lies in an
                 // earlier chunk; a flag set meanwhile but not seen only costs this chunk the
                 // full path
-                const uint32_t dn = dn0;
+                uint32_t dn = dnA;
+                if (sc) {
+                    par = pee_call_parity(line, j, nchunks);
+                    dn = par ? dnB : dnA;
+                }
                 cc = (mode & PEE_MODE_NOTICKET) ? (uint32_t)j : atomicAdd(tick, 1u);
                 if (dn) {   // `end` already placed: this chunk is a plain copy
-                    lb_store(st + cc, LB_INC | (u64)L);
+                    lb_store(status_all + par * stride + (size_t)b * nchunks + cc, LB_INC | (u64)L);
                     cc |= 0x80000000u;
                 }
             } else {
                 // the two flag loads and the ticket go out together (one round trip); a ticket
                 // taken for a finished slice is published as "prefix >= L" and skipped
                 const uint32_t nd = ld_agent(ctl);
-                const uint32_t dn = ld_agent(tick + 1);
+                const uint32_t dn = ld_agent(line + PEE_LINE_FIN1);
                 cc = atomicAdd(tick, 1u);
                 if (nd >= (uint32_t)B || dn) {
-                    if (cc < (uint32_t)nchunks) lb_store(st + cc, LB_INC | (u64)L);
+                    if (cc < (uint32_t)nchunks) lb_store(status_all + stride + (size_t)b * nchunks + cc, LB_INC | (u64)L);
                     cc = nd >= (uint32_t)B ? PEE_STOP : PEE_SKIP;
                 }
             }
             s_v = cc;
+            s_par = par;
         }
         if (tid < 4 * PEE_TILE / 32) lm32[tid] = 0;
         lds_barrier();
         LB_STAMP(1);
         const uint32_t cv = s_v;
+        const int par = s_par;
+        u64* st = status_all + par * stride + (size_t)b * nchunks;
+        uint32_t* fin_flag = line + (par ? PEE_LINE_FIN1 : PEE_LINE_FIN0);
         if (INPLACE) {
             if (cv == PEE_STOP) return;
             if (cv >= (uint32_t)nchunks) { lds_barrier(); continue; }
         }
         const bool copy_only = !INPLACE && (cv & 0x80000000u);
         const int c = (int)(cv & 0x7FFFFFFFu);
+        if (sc && tid == 0) {   // clear this chunk's word (and chunk 0: the flag) of the next call's buffer
+            lb_store(status_all + (1 - par) * stride + (size_t)b * nchunks + c, 0ull);
+            if (c == 0) __hip_atomic_store(line + (par ? PEE_LINE_FIN0 : PEE_LINE_FIN1), 0u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+        }
         if (INPLACE || c != j) pee_load_chunk<T, NT>(src, W, CR, items, c, a0, a1, o0);
         if (copy_only) {
 #pragma unroll
@@ -1317,6 +1369,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
         }
         uint32_t esm = 0, safem = 0, rightm = 0;   // bit 4u+q
         u64 packed = 0;
+        uint32_t uns = 0;   // unsafe candidates (location-map bits when the chunk lies before `end`)
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint32_t it = (uint32_t)c * PEE_CHUNK + u * 256u + tid;
@@ -1330,13 +1383,22 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                     if (pc.safe) safem |= bit;
                     if (pc.right) rightm |= bit;
                     if (pc.expand && pc.safe) { esm |= bit; ++n; }
+                    uns += pc.safe ? 0u : 1u;
                 }
                 packed |= (u64)n << (16 * u);
             }
         }
+        {   // the chunk's unsafe total: wave sums into LDS, read after the scan's barriers
+            uint32_t ws = uns;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) ws += __shfl_xor(ws, o, 64);
+            if ((tid & 63) == 0) s_uns[tid >> 6] = ws;
+        }
         u64 ptot;
         const u64 pex = block_excl_scan64_lds<256>(packed, sh64, &ptot);
         const uint32_t agg = (uint32_t)((ptot & 0xFFFFu) + ((ptot >> 16) & 0xFFFFu) + ((ptot >> 32) & 0xFFFFu) + (ptot >> 48));
+        const uint32_t agg_u = s_uns[0] + s_uns[1] + s_uns[2] + s_uns[3];
+        const u64 aggw = (u64)agg | ((u64)agg_u << 32);   // the chunk's status-word value
         const bool publish = !(b == 0 && c == dbg_skip);
         LB_STAMP(2);
         // waves 1-3 (idle during wave 0's look-back) fetch the payload words into LDS meanwhile:
@@ -1346,17 +1408,21 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
         u64 pwv = 0;
         if (pay_st && tid >= 64) pwv = payload_all[(size_t)b * pw + min(tid - 64, pw - 1)];
         if (c == 0) {
-            if (tid == 0) { if (publish) lb_store(st, LB_INC | (u64)agg); s_excl = 0; }
+            if (tid == 0) { if (publish) lb_store(st, LB_INC | aggw); s_excl = 0; s_uexcl = 0; }
         } else {
-            if (tid == 0 && publish) lb_store(st + c, LB_AGG | (u64)agg);
+            if (tid == 0 && publish) lb_store(st + c, LB_AGG | aggw);
             if (tid < 64) {
                 bool to = false, fb = false;
-                uint32_t ex;
-                if (INPLACE) ex = lb_exclusive(st, c, &to, &fb, spin_max, NoFallback(), tick + 1, L);
-                else ex = lb_exclusive(st, c, &to, &fb, spin_max, EmbedCount<T>{src, W, CR, items, Tthr, maxval}, tick + 1, L);
+                LbSum ex;
+                if (INPLACE) ex = lb_exclusive(st, c, &to, &fb, spin_max, NoFallback(), fin_flag, L);
+                else ex = lb_exclusive(st, c, &to, &fb, spin_max, EmbedCount<T>{src, W, CR, items, Tthr, maxval}, fin_flag, L);
                 if (tid == 0) {
-                    if (publish) lb_store(st + c, LB_INC | (u64)(ex + agg));
-                    s_excl = ex;
+                    // inclusive prefix; past `end` saturated to L (successors only compare it with L)
+                    const u64 ie = ex.e + agg;
+                    const u64 iu = (ex.u + agg_u) & 0x3FFFFFFFull;
+                    if (publish) lb_store(st + c, LB_INC | (ie >= L ? (u64)L : ie) | (iu << 32));
+                    s_excl = (uint32_t)min(ex.e, (u64)0xFFFFFFFFull);
+                    s_uexcl = (uint32_t)ex.u;
                     // sticky: the status words are only ever raised (atomicMax) after this
                     if (to) { atomicMax(&M->status, CODEC_PEE_ELOOKBACK); atomicAdd(diag + 2, 1u); }
                     if (fb) atomicAdd(diag, 1u);
@@ -1367,11 +1433,13 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
         lds_barrier();
         LB_STAMP(3);
         const uint32_t excl = s_excl;
+        const uint32_t uexcl = s_uexcl;
         const bool last = c == nchunks - 1;
         if (tid == 0) {
             if (c == 0) {
                 M->T = Tthr; M->maxval = maxval; M->L = (int)L; M->nc = nc; M->ntiles = ntiles; M->h = H; M->w = W;
-                if (L == 0) { M->end = -1; M->tile_end = -1; }   // status stays 0 (memset)
+                if (L == 0) { M->end = -1; M->tile_end = -1; }   // status: below (out of place) / memset (in place)
+                if (!INPLACE) M->reserved[0] = M->reserved[1] = M->reserved[2] = 0;
             }
             // the chunk holding `end` (or the last one on overflow) reports the capacity seen so
             // far: exact when it is the last chunk, else a lower bound (later chunks are not counted)
@@ -1380,10 +1448,15 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                 M->capacity = (int)(excl + agg);
                 M->flags = last ? 0 : CODEC_PEE_PARTIAL;
             }
-            if (last && excl + agg < L) { M->end = nc - 1; M->tile_end = ntiles - 1; atomicMax(&M->status, 1); }
+            if (last && excl + agg < L) {
+                M->end = nc - 1;
+                M->tile_end = ntiles - 1;
+                if (INPLACE) atomicMax(&M->status, 1);
+            }
         }
         lds_barrier();   // lm32 zeroing vs the ORs below
         LB_STAMP(6);
+        uint32_t nun = 0;
         if (excl < L) {   // some candidate of this chunk is active
             uint32_t base = excl;
             uint32_t unsafe_n = 0;
@@ -1452,16 +1525,21 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                 if (INPLACE && procm) stv<NT>(reinterpret_cast<V*>(dst + o0[u] + W), a1[u]);
             }
             LB_STAMP(7);
-            const uint32_t nun = block_sum_u32_lds<256>(unsafe_n, sh);   // also orders the lm32 ORs
+            nun = block_sum_u32_lds<256>(unsafe_n, sh);   // also orders the lm32 ORs
             LB_STAMP(8);
-            if (tid == 0 && nun) atomicAdd(&M->lm_count, (int)nun);
+            if (INPLACE && tid == 0 && nun) atomicAdd(&M->lm_count, (int)nun);
         }
         LB_STAMP(4);
         if (tid == 0) {   // `end` is in this chunk (or there is none): later chunks need no cursor
             const bool fin = (excl < L && excl + agg >= L) || (L == 0 && c == 0) || (last && excl + agg < L);
             if (fin) {
-                __hip_atomic_store(tick + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (INPLACE) atomicAdd(ctl, 1u);
+                __hip_atomic_store(fin_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (INPLACE) {
+                    atomicAdd(ctl, 1u);
+                } else {   // no meta atomics out of place: the chunk holding `end` writes them
+                    M->status = (last && excl + agg < L) ? 1 : 0;
+                    M->lm_count = (int)(uexcl + nun);
+                }
             }
         }
         if (!INPLACE) {
@@ -1490,6 +1568,55 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
     }
 }
 
+// The extract's read-ahead (self-cleaning payload writes): the bits of the first `need` (1..63)
+// inner candidates at or after item it0, in rank order, as the low bits of a u64 -- what
+// the following chunks will recover, computed from their (read-only) stego pixels and map
+// words.  One wave, 4 items per lane per round, rounds until `need` bits or `end`.
+template <typename T>
+__device__ u64 pee_read_ahead(const T* src, const u64* lm, int W, int CR, uint32_t items, int end, int Tthr, uint32_t it0,
+                              uint32_t need) {
+    typedef typename Vec8<T>::type V;
+    const int lane = threadIdx.x & 63;
+    u64 ra = 0ull;
+    uint32_t got = 0;
+    for (uint32_t itb = it0; got < need && itb < items && (int)(4 * itb) <= end; itb += 256u) {   // uniform
+        V v0[4], v1[4];
+        u64 lw[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {   // all loads of the round in flight together (clamped addresses)
+            const uint32_t it = min(itb + (uint32_t)(u * 64 + lane), items - 1u);
+            const uint32_t r = it / (uint32_t)CR, cc = it - r * (uint32_t)CR;
+            const size_t o = (size_t)(2 * r) * W + (size_t)cc * 8;
+            v0[u] = *reinterpret_cast<const V*>(src + o);
+            v1[u] = *reinterpret_cast<const V*>(src + o + W);
+            lw[u] = lm[(4 * it) >> 6];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t it = itb + (uint32_t)(u * 64 + lane);
+            const u64 mw = lw[u] >> ((4 * it) & 63);
+            uint32_t pk = 0, n = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int k = (int)(4 * it) + q;
+                const int x = (int)get_px(v1[u], 2 * q + 1);
+                const int e2 = x - med3((int)get_px(v1[u], 2 * q), (int)get_px(v0[u], 2 * q + 1), (int)get_px(v0[u], 2 * q));
+                const bool inner = it < items && k <= end && !((mw >> q) & 1ull) && e2 >= -2 * Tthr && e2 < 2 * Tthr;
+                pk |= (inner ? (uint32_t)(e2 & 1) : 0u) << n;
+                n += inner ? 1u : 0u;
+            }
+            const uint32_t incl = wave_incl_scan(n);
+            const uint32_t pos = got + incl - n;
+            u64 contrib = pos < 64u ? (u64)pk << pos : 0ull;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) contrib |= __shfl_xor(contrib, o, 64);
+            ra |= contrib;
+            got += (uint32_t)__shfl(incl, 63, 64);
+        }
+    }
+    return need >= 64u ? ra : (ra & ((1ull << need) - 1ull));
+}
+
 // extract: chunks up to the one holding `end` recover bits + pixels (look-back over the
 // inner-candidate counts); later chunks are a plain copy (out of place) or skipped.
 template <typename T, bool NT, bool INPLACE>
@@ -1502,6 +1629,12 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
     __shared__ u64 sh64[8];
     __shared__ uint32_t s_v, s_excl;
     __shared__ int s_cmax;
+    __shared__ u64 s_ra;
+    // self-cleaning (PEE_MODE_SC, small out-of-place batches): status words by call parity, and
+    // the payload written without atomics or a zeroed buffer -- every word by the chunk holding
+    // its first bit, which reads the word's later bits ahead from the following chunks' pixels
+    const bool sc = !INPLACE && (mode & PEE_MODE_SC);
+    const size_t stride = (size_t)B * nchunks;
     // the chunk's recovered bits: ranks [excl, excl + agg), agg <= 4096, from word excl / 64
     __shared__ u64 pbuf[PEE_CHUNK * 4 / 64 + 2];
     const int CR = W / 8;
@@ -1544,6 +1677,17 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
         // out of place chunk j is loaded while the ticket is in flight (a plain copy when past
         // `end`); in place only the ticketed chunk is read
         if (!INPLACE) pee_load_chunk<T, NT>(src, W, CR, items, j, a0, a1, o0);
+        int par = 1;   // status-word buffer (calls that zero first use buffer 1)
+        if (sc) {      // every slot arrives, copy chunks too; wave 0 (the look-back) learns the parity
+            if (tid == 0) {
+                par = pee_call_parity(ctl + 32 + 32 * (size_t)b, j, nchunks);
+                lb_store(status_all + (1 - par) * stride + (size_t)b * nchunks + j, 0ull);   // next call's word
+                // the in-place look-back flag (codec_pee_extract_flag_offset) reads clear after
+                // this call: an earlier in-place call may have set it, out of place nothing does
+                if (b == 0 && j == 0) __hip_atomic_store(ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            par = __shfl(par, 0, 64);
+        }
         const u64* lm = lm_all + (size_t)b * lmw;
         const bool noticket = !INPLACE && (mode & PEE_MODE_NOTICKET);
         u64 lwv[4] = {0, 0, 0, 0};   // location-map word of each item (4 bits of it used)
@@ -1592,7 +1736,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
             u64 ptot;
             const u64 pex = block_excl_scan64_lds<256>(packed, sh64, &ptot);
             const uint32_t agg = (uint32_t)((ptot & 0xFFFFu) + ((ptot >> 16) & 0xFFFFu) + ((ptot >> 32) & 0xFFFFu) + (ptot >> 48));
-            u64* st = status_all + (size_t)b * nchunks;
+            u64* st = status_all + par * stride + (size_t)b * nchunks;   // par: valid in wave 0
             const bool publish = c < cend && !(b == 0 && c == dbg_skip);
             if (c == 0) {
                 if (tid == 0) { if (publish) lb_store(st, LB_INC | (u64)agg); s_excl = 0; }
@@ -1600,12 +1744,12 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
                 if (tid == 0 && publish) lb_store(st + c, LB_AGG | (u64)agg);
                 if (tid < 64) {
                     bool to = false, fb = false;
-                    uint32_t ex;
+                    LbSum ex;
                     if (INPLACE) ex = lb_exclusive(st, c, &to, &fb, spin_max, NoFallback());
                     else ex = lb_exclusive(st, c, &to, &fb, spin_max, ExtractCount<T>{src, lm, W, CR, items, end, Tthr});
                     if (tid == 0) {
-                        if (publish) lb_store(st + c, LB_INC | (u64)(ex + agg));
-                        s_excl = ex;
+                        if (publish) lb_store(st + c, LB_INC | (ex.e + agg));
+                        s_excl = (uint32_t)ex.e;
                         if (to) { atomicOr(ctl + 1, 1u); atomicAdd(diag + 3, 1u); }   // codec_pee_extract_flag_offset
                         if (fb) atomicAdd(diag + 1, 1u);
                     }
@@ -1650,14 +1794,46 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
             // shared with the neighbouring chunks (OR-ed in); the host zeroed the payload
             lds_barrier();
             const int nw = (int)(((excl & 63u) + agg + 63u) >> 6);
-            if (tid < nw) {
-                const u64 wv = pbuf[tid];
-                if (wv) {
-                    const bool shared = (tid == 0 && (excl & 63u)) || (tid == nw - 1 && ((excl + agg) & 63u));
-                    if (shared) atomicOr(&payload[w0 + tid], wv);
-                    else payload[w0 + tid] = wv;
+            const uint32_t f = excl + agg;
+            if (!sc) {
+                if (tid < nw) {
+                    const u64 wv = pbuf[tid];
+                    if (wv) {
+                        const bool shared = (tid == 0 && (excl & 63u)) || (tid == nw - 1 && (f & 63u));
+                        if (shared) atomicOr(&payload[w0 + tid], wv);
+                        else payload[w0 + tid] = wv;
+                    }
                 }
+            } else {
+                // self-cleaning: this chunk writes the words that START in [excl, f) whole; the
+                // last one's bits past f come from the following chunks (read ahead from their
+                // pixels by wave 1, ranks f .. next word boundary); the word holding excl, when
+                // excl is not word-aligned, is the previous owner's.  The chunk holding `end`
+                // zeroes the words after its last one.
+                const bool ahead = c < cend && (f & 63u) != 0u;   // uniform
+                if (ahead) {
+                    if (tid >= 64 && tid < 128) {
+                        const u64 ra = pee_read_ahead<T>(src, lm, W, CR, items, end, Tthr, (uint32_t)(c + 1) * PEE_CHUNK,
+                                                         64u - (f & 63u));
+                        if (tid == 64) s_ra = ra;
+                    }
+                    lds_barrier();
+                }
+                if (tid < nw) {
+                    const int w = w0 + tid;
+                    const bool owned = tid > 0 || (excl & 63u) == 0u;
+                    if (owned && w < pw) {
+                        u64 wv = pbuf[tid];
+                        if (ahead && tid == nw - 1) wv |= s_ra << (f & 63u);
+                        payload[w] = wv;
+                    }
+                }
+                if (c == cend)
+                    for (int w = (int)((f + 63u) >> 6) + tid; w < pw; w += 256) payload[w] = 0ull;
             }
+        } else if (sc && c == 0 && cend < 0) {   // no embedded bit at all: the payload is zero
+            u64* payload = payload_all + (size_t)b * pw;
+            for (int w = tid; w < pw; w += 256) payload[w] = 0ull;
         }
         if (!INPLACE) {
 #pragma unroll
@@ -2794,7 +2970,8 @@ static PeeWs pee_ws(const codec_pee_params* P) {
     L.cnt = 0;
     L.off = align_up((size_t)P->B * L.ntiles_max * 4, 256);
     L.st = align_up(L.off + (size_t)P->B * L.ntiles_max * 4, 256);
-    L.ctl = L.st + (size_t)P->B * L.nchunks * 8;   // status words and ctl are cleared together
+    // two status-word buffers (PEE_MODE_SC), then ctl; zeroing calls clear them all together
+    L.ctl = L.st + 2 * (size_t)P->B * L.nchunks * 8;
     // diag: 4 cumulative uint32 counters (codec_pee_diag_offset), outside the per-call memset
     L.diag = align_up(L.ctl + PEE_CTL_WORDS(P->B) * 4, 16);
     // capacity-control error histogram (codec_pee_capacity; cleared by that call)
@@ -3024,13 +3201,19 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
     if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && onepass != 0) {
         u64* stw = reinterpret_cast<u64*>(static_cast<char*>(workspace) + L.st);
         uint32_t* ctl = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.ctl);
-        HIP_TRY(pee_zero(st, stw, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4, meta, (size_t)P->B * sizeof(codec_pee_meta),
-                         inplace ? lm : nullptr, inplace ? (size_t)P->B * P->lm_words * 8 : 0));
+        int mode = flat ? PEE_MODE_FLAT | (knob("CODEC_PEE_FLAT_TICKET", 0) ? 0 : PEE_MODE_NOTICKET)
+                        : (knob("CODEC_PEE_1P_CHUNK_MAJOR", 1) ? PEE_MODE_CMAJOR : 0) |
+                              (knob("CODEC_PEE_1P_NOTICKET", 1) ? PEE_MODE_NOTICKET : 0) |
+                              ((int)(knob("CODEC_PEE_1P_GROUP", 32) / 8) << 8);
+        // small out-of-place batches (flat slots, no ticket) clean up after themselves: no
+        // zeroing launch (C2: one launch of ~2 us fewer per call); meta is written without
+        // atomics out of place, so only in place (and the ticket modes) zero it
+        if (flat && (mode & PEE_MODE_NOTICKET) && knob("CODEC_PEE_SELFCLEAN", 1)) mode |= PEE_MODE_SC;
+        if (!(mode & PEE_MODE_SC))
+            HIP_TRY(pee_zero(st, stw, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4, inplace ? meta : nullptr,
+                             inplace ? (size_t)P->B * sizeof(codec_pee_meta) : 0, inplace ? lm : nullptr,
+                             inplace ? (size_t)P->B * P->lm_words * 8 : 0));
         ProfScope prof(st, CODEC_K_PEE_EMBED1);
-        const int mode = flat ? PEE_MODE_FLAT | (knob("CODEC_PEE_FLAT_TICKET", 0) ? 0 : PEE_MODE_NOTICKET)
-                              : (knob("CODEC_PEE_1P_CHUNK_MAJOR", 1) ? PEE_MODE_CMAJOR : 0) |
-                                    (knob("CODEC_PEE_1P_NOTICKET", 1) ? PEE_MODE_NOTICKET : 0) |
-                                    ((int)(knob("CODEC_PEE_1P_GROUP", 32) / 8) << 8);
         const long long total = pee_total_slots(P->B, L.nchunks, pee_group8(P->B, mode, inplace));
         long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));
         if (g > total) g = total;
@@ -3257,12 +3440,14 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
     if (vec && items > 0 && (long long)L.nchunks * P->B < 0x7FFFFFFFLL && onepass != 0) {
         u64* stw = reinterpret_cast<u64*>(static_cast<char*>(workspace) + L.st);
         uint32_t* ctl = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.ctl);
-        HIP_TRY(pee_zero(st, payload_out, (size_t)P->B * P->payload_words * 8, stw, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4));
+        int mode = flat ? PEE_MODE_FLAT | (knob("CODEC_PEE_FLAT_TICKET", 0) ? 0 : PEE_MODE_NOTICKET)
+                        : (knob("CODEC_PEE_X_CHUNK_MAJOR", knob("CODEC_PEE_1P_CHUNK_MAJOR", 1)) ? PEE_MODE_CMAJOR : 0) |
+                              (knob("CODEC_PEE_X_NOTICKET", 1) ? PEE_MODE_NOTICKET : 0) |
+                              ((int)(knob("CODEC_PEE_X_GROUP", 32) / 8) << 8);
+        if (flat && (mode & PEE_MODE_NOTICKET) && knob("CODEC_PEE_SELFCLEAN", 1)) mode |= PEE_MODE_SC;
+        if (!(mode & PEE_MODE_SC))
+            HIP_TRY(pee_zero(st, payload_out, (size_t)P->B * P->payload_words * 8, stw, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4));
         ProfScope prof(st, CODEC_K_PEE_EXTRACT1);
-        const int mode = flat ? PEE_MODE_FLAT | (knob("CODEC_PEE_FLAT_TICKET", 0) ? 0 : PEE_MODE_NOTICKET)
-                              : (knob("CODEC_PEE_X_CHUNK_MAJOR", knob("CODEC_PEE_1P_CHUNK_MAJOR", 1)) ? PEE_MODE_CMAJOR : 0) |
-                                    (knob("CODEC_PEE_X_NOTICKET", 1) ? PEE_MODE_NOTICKET : 0) |
-                                    ((int)(knob("CODEC_PEE_X_GROUP", 32) / 8) << 8);
         const long long total = pee_total_slots(P->B, L.nchunks, pee_group8(P->B, mode, inplace));
         long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));
         if (g > total) g = total;

@@ -67,6 +67,9 @@ def test_oracle_truncates_on_overflow():
 PATHS = {"auto": {}, "onepass": {"CODEC_PEE_ONEPASS": "1"}, "twopass": {"CODEC_PEE_ONEPASS": "0"},
          "onepass_lanes": {"CODEC_PEE_ONEPASS": "1", "CODEC_PEE_FLAT_MAXB": "0"},
          "onepass_flat_ticket": {"CODEC_PEE_ONEPASS": "1", "CODEC_PEE_FLAT_TICKET": "1", "CODEC_PEE_1P_WGS": "5"},
+         # small batches clean up after themselves (round 4: no zeroing launch); "0" restores
+         # the zeroing launch on the same flat slots
+         "onepass_zeroing": {"CODEC_PEE_ONEPASS": "1", "CODEC_PEE_SELFCLEAN": "0"},
          "onepass_small_grid": {"CODEC_PEE_ONEPASS": "1", "CODEC_PEE_1P_WGS": "7", "CODEC_PEE_IP_WGS": "3"},
          # decode-side tile counts: workgroup-per-tile (block sums) instead of wave-per-tile,
          # and wave-per-tile with one workgroup per slice (every wave strides over tiles)
@@ -325,6 +328,59 @@ def test_gpu_lookback_fallback_out_of_place(slots, monkeypatch):
     np.testing.assert_array_equal(cover.cpu().numpy(), covers)
     d = codec.diagnostics()
     assert d["extract_fallback_chunks"] >= 1 and d["embed_unrecovered_chunks"] == 0 == d["extract_unrecovered_chunks"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("h,w,bsz", [(256, 256, 3), (2048, 2048, 1), (130, 2048, 5)])
+def test_gpu_selfclean_across_calls(h, w, bsz, monkeypatch):
+    """Round 4: small out-of-place batches run the look-back with no zeroing launch -- two
+    status-word buffers picked by the parity of a per-slice call counter, each call clearing
+    the other buffer's words; meta without atomics; payload words written whole (no zeroed
+    output: each word by the chunk holding its first bit, reading the rest ahead).  A sequence
+    of out-of-place and in-place calls on ONE workspace (different covers, empty, short, long
+    and overflowing payloads) must each equal the oracle, with every payload word exact (zero
+    past the recovered bits) and the in-place look-back flag clear."""
+    torch = pytest.importorskip("torch")
+    from codec_tcc_amd import framing
+    from codec_tcc_amd.pee import PeeCodec, lm_bits
+    monkeypatch.setenv("CODEC_PEE_ONEPASS", "1")
+    T = 2
+    codec = PeeCodec(bsz, h, w, T=T)
+    pw = None
+    for k, mode in enumerate(["oop", "oop", "inplace", "oop", "inplace", "oop", "oop", "oop"]):
+        covers = np.stack([synth.ct12(h, w, 300 + 10 * k + i) for i in range(bsz)])
+        caps = [P.capacity(cv, T) for cv in covers]
+        if k % 3 == 0:
+            lens = [max(0, cp - 5 * i) for i, cp in enumerate(caps)]
+        elif k % 3 == 1:
+            lens = [37 * i + 3 for i in range(bsz)]
+        else:
+            lens = [0] + [min(cp, 4000 + i) for i, cp in enumerate(caps[1:])]
+        if k == 5:
+            lens[0] = caps[0] + 50                       # overflows: truncated, status 1
+        payloads = [_bits(n, 500 + 10 * k + i) for i, n in enumerate(lens)]
+        inplace = mode == "inplace"
+        dev = torch.from_numpy(covers).cuda()
+        enc = codec.embed(dev, payloads, stego=dev if inplace else None)
+        recs = enc.records()
+        stego = enc.stego.cpu().numpy()
+        got_bits = []
+        for i in range(bsz):
+            st, side = P.pee_embed(covers[i], payloads[i], T, truncate=True)
+            assert recs[i].end == side["end"] and recs[i].status == side["status"], (k, i)
+            assert recs[i].lm_count == int(side["lm"].sum()), (k, i)
+            assert tuple(recs[i].reserved) == (0, 0, 0)
+            np.testing.assert_array_equal(stego[i], st)
+            np.testing.assert_array_equal(lm_bits(enc, i), side["lm"])
+            got_bits.append(payloads[i][: side["L"]])
+        words, cover = codec.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words,
+                                     cover=enc.stego if inplace else None)
+        want, _ = framing.pack_bits(got_bits, words=enc.payload_words)
+        np.testing.assert_array_equal(words.cpu().numpy().view(np.uint64), want.view(np.uint64))
+        np.testing.assert_array_equal(cover.cpu().numpy(), covers)
+        assert not codec.lookback_failed(enc.payload_words)
+        pw = enc.payload_words
+    assert pw is not None and codec.diagnostics()["embed_unrecovered_chunks"] == 0
 
 
 @pytest.mark.gpu
