@@ -1240,11 +1240,15 @@ __device__ unsigned long long g_lb_trace[LB_TRACE_SLOTS * 12];
 #define PEE_LINE_FIN0 1
 #define PEE_LINE_FIN1 4
 #define PEE_LINE_ARR 8    // 8 x u64 shard counters (words 8..23 of the slice's 32-word line)
-__device__ __forceinline__ int pee_call_parity(uint32_t* line, int c, int nchunks) {
-    const int g = c & 7;
-    const u64 old = atomicAdd(reinterpret_cast<unsigned long long*>(line + PEE_LINE_ARR + 2 * g), 1ull);
-    const uint32_t ng = (uint32_t)((nchunks - g + 7) >> 3);   // chunks of this slice on shard g
+__device__ __forceinline__ u64 pee_arrive(uint32_t* line, int c) {   // returns the shard's old count
+    return atomicAdd(reinterpret_cast<unsigned long long*>(line + PEE_LINE_ARR + 2 * (c & 7)), 1ull);
+}
+__device__ __forceinline__ int pee_parity_of(u64 old, int c, int nchunks) {
+    const uint32_t ng = (uint32_t)((nchunks - (c & 7) + 7) >> 3);   // chunks of this slice on shard c % 8
     return (int)((old / ng) & 1ull);
+}
+__device__ __forceinline__ int pee_call_parity(uint32_t* line, int c, int nchunks) {
+    return pee_parity_of(pee_arrive(line, c), c, nchunks);
 }
 #define PEE_SKIP 0xFFFFFFFFu
 #define PEE_STOP 0xFFFFFFFEu
@@ -1677,17 +1681,10 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
         // out of place chunk j is loaded while the ticket is in flight (a plain copy when past
         // `end`); in place only the ticketed chunk is read
         if (!INPLACE) pee_load_chunk<T, NT>(src, W, CR, items, j, a0, a1, o0);
-        int par = 1;   // status-word buffer (calls that zero first use buffer 1)
-        if (sc) {      // every slot arrives, copy chunks too; wave 0 (the look-back) learns the parity
-            if (tid == 0) {
-                par = pee_call_parity(ctl + 32 + 32 * (size_t)b, j, nchunks);
-                lb_store(status_all + (1 - par) * stride + (size_t)b * nchunks + j, 0ull);   // next call's word
-                // the in-place look-back flag (codec_pee_extract_flag_offset) reads clear after
-                // this call: an earlier in-place call may have set it, out of place nothing does
-                if (b == 0 && j == 0) __hip_atomic_store(ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            par = __shfl(par, 0, 64);
-        }
+        // every slot arrives (copy chunks too); the returned count is used only later, so the
+        // map-word loads below are not held back behind the atomic's round trip
+        u64 arr_old = 0ull;
+        if (sc && tid == 0) arr_old = pee_arrive(ctl + 32 + 32 * (size_t)b, j);
         const u64* lm = lm_all + (size_t)b * lmw;
         const bool noticket = !INPLACE && (mode & PEE_MODE_NOTICKET);
         u64 lwv[4] = {0, 0, 0, 0};   // location-map word of each item (4 bits of it used)
@@ -1704,6 +1701,17 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
             lds_barrier();
             c = (int)s_v;
             if (INPLACE || c != j) pee_load_chunk<T, NT>(src, W, CR, items, c, a0, a1, o0);
+        }
+        int par = 1;   // status-word buffer (calls that zero first use buffer 1)
+        if (sc) {      // wave 0 (the look-back) learns the call parity
+            if (tid == 0) {
+                par = pee_parity_of(arr_old, j, nchunks);
+                lb_store(status_all + (1 - par) * stride + (size_t)b * nchunks + j, 0ull);   // next call's word
+                // the in-place look-back flag (codec_pee_extract_flag_offset) reads clear after
+                // this call: an earlier in-place call may have set it, out of place nothing does
+                if (b == 0 && j == 0) __hip_atomic_store(ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            par = __shfl(par, 0, 64);
         }
         if (c <= cend) {
             uint32_t actm = 0, innm = 0;
