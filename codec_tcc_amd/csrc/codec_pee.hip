@@ -1060,7 +1060,9 @@ __device__ __forceinline__ u64 wave_sum_u64(u64 v) {
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
-template <typename F>
+// TWO: also sum the high field (the self-cleaning embed's unsafe counts); otherwise only the
+// low one, as the zeroing paths need (fewer registers in the headline kernels)
+template <bool TWO = false, typename F>
 __device__ LbSum lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, uint32_t spin_max, const F& count,
                               uint32_t* done = nullptr, uint32_t sat = 0) {
     const int lane = threadIdx.x & 63;
@@ -1123,8 +1125,15 @@ __device__ LbSum lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, uin
                     spins = 0;
                 }
             }
-            ex.e += wave_sum_u64(lane <= first ? LB_LO(w) : 0ull);
-            ex.u += wave_sum_u64(lane <= first ? LB_HI(w) : 0ull);
+            if constexpr (TWO) {
+                ex.e += wave_sum_u64(lane <= first ? LB_LO(w) : 0ull);
+                ex.u += wave_sum_u64(lane <= first ? LB_HI(w) : 0ull);
+            } else {   // 32-bit sums, as before the second field existed
+                uint32_t v = lane <= first ? (uint32_t)w : 0u;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+                ex.e += v;
+            }
             if (first < 64) return ex;
             // embed (done != nullptr): a partial sum that already reaches `sat` (= L) places the
             // chunk past `end`; the caller only compares the prefix with L, and publishes it as a
@@ -1252,7 +1261,7 @@ __device__ __forceinline__ int pee_call_parity(uint32_t* line, int c, int nchunk
 }
 #define PEE_SKIP 0xFFFFFFFFu
 #define PEE_STOP 0xFFFFFFFEu
-template <typename T, bool NT, bool INPLACE>
+template <typename T, bool NT, bool INPLACE, bool SC = false>
 __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover, T* stego, int H, int W, int T0,
                                                     int maxval, const int32_t* __restrict__ lengths,
                                                     const u64* __restrict__ payload_all, int pw, int nchunks, int B,
@@ -1264,7 +1273,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
     __shared__ uint32_t sh[8];
     __shared__ uint32_t s_v, s_excl, s_uexcl, s_uns[4];
     __shared__ int s_par;
-    const bool sc = !INPLACE && (mode & PEE_MODE_SC);
+    constexpr bool sc = !INPLACE && SC;   // self-cleaning: a separate instantiation (PEE_MODE_SC)
     __shared__ uint32_t lm32[4 * PEE_TILE / 32];
     __shared__ u64 s_pay[192];   // the slice's payload words when pw <= 192 (see below)
     const bool pay_st = pw <= 192;
@@ -1296,7 +1305,8 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
         // out of place the finished flags are read BEFORE the chunk's pixels are requested, so
         // waiting for them does not wait for the pixels too (vmcnt counts in issue order)
         const uint32_t dnA = !INPLACE ? ld_agent(line + (sc ? PEE_LINE_FIN0 : PEE_LINE_FIN1)) : 0u;   // every lane
-        const uint32_t dnB = (!INPLACE && sc) ? ld_agent(line + PEE_LINE_FIN1) : 0u;
+        uint32_t dnB = 0u;
+        if constexpr (sc) dnB = ld_agent(line + PEE_LINE_FIN1);
         // out of place: the slot's own chunk j is loaded while the ticket is in flight (the
         // ticket equals j unless workgroups were dispatched out of order)
         if (!INPLACE) pee_load_chunk<T, NT>(src, W, CR, items, j, a0, a1, o0);
@@ -1308,7 +1318,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                 // earlier chunk; a flag set meanwhile but not seen only costs this chunk the
                 // full path
                 uint32_t dn = dnA;
-                if (sc) {
+                if constexpr (sc) {
                     par = pee_call_parity(line, j, nchunks);
                     dn = par ? dnB : dnA;
                 }
@@ -1387,12 +1397,12 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                     if (pc.safe) safem |= bit;
                     if (pc.right) rightm |= bit;
                     if (pc.expand && pc.safe) { esm |= bit; ++n; }
-                    uns += pc.safe ? 0u : 1u;
+                    if constexpr (sc) uns += pc.safe ? 0u : 1u;
                 }
                 packed |= (u64)n << (16 * u);
             }
         }
-        {   // the chunk's unsafe total: wave sums into LDS, read after the scan's barriers
+        if constexpr (sc) {   // the chunk's unsafe total: wave sums into LDS, read after the scan's barriers
             uint32_t ws = uns;
 #pragma unroll
             for (int o = 32; o >= 1; o >>= 1) ws += __shfl_xor(ws, o, 64);
@@ -1401,7 +1411,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
         u64 ptot;
         const u64 pex = block_excl_scan64_lds<256>(packed, sh64, &ptot);
         const uint32_t agg = (uint32_t)((ptot & 0xFFFFu) + ((ptot >> 16) & 0xFFFFu) + ((ptot >> 32) & 0xFFFFu) + (ptot >> 48));
-        const uint32_t agg_u = s_uns[0] + s_uns[1] + s_uns[2] + s_uns[3];
+        const uint32_t agg_u = sc ? s_uns[0] + s_uns[1] + s_uns[2] + s_uns[3] : 0u;
         const u64 aggw = (u64)agg | ((u64)agg_u << 32);   // the chunk's status-word value
         const bool publish = !(b == 0 && c == dbg_skip);
         LB_STAMP(2);
@@ -1419,14 +1429,19 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                 bool to = false, fb = false;
                 LbSum ex;
                 if (INPLACE) ex = lb_exclusive(st, c, &to, &fb, spin_max, NoFallback(), fin_flag, L);
-                else ex = lb_exclusive(st, c, &to, &fb, spin_max, EmbedCount<T>{src, W, CR, items, Tthr, maxval}, fin_flag, L);
+                else ex = lb_exclusive<sc>(st, c, &to, &fb, spin_max, EmbedCount<T>{src, W, CR, items, Tthr, maxval}, fin_flag, L);
                 if (tid == 0) {
-                    // inclusive prefix; past `end` saturated to L (successors only compare it with L)
-                    const u64 ie = ex.e + agg;
-                    const u64 iu = (ex.u + agg_u) & 0x3FFFFFFFull;
-                    if (publish) lb_store(st + c, LB_INC | (ie >= L ? (u64)L : ie) | (iu << 32));
-                    s_excl = (uint32_t)min(ex.e, (u64)0xFFFFFFFFull);
-                    s_uexcl = (uint32_t)ex.u;
+                    if constexpr (sc) {
+                        // inclusive prefix; past `end` saturated to L (successors only compare it with L)
+                        const u64 ie = ex.e + agg;
+                        const u64 iu = (ex.u + agg_u) & 0x3FFFFFFFull;
+                        if (publish) lb_store(st + c, LB_INC | (ie >= L ? (u64)L : ie) | (iu << 32));
+                        s_excl = (uint32_t)min(ex.e, (u64)0xFFFFFFFFull);
+                        s_uexcl = (uint32_t)ex.u;
+                    } else {
+                        if (publish) lb_store(st + c, LB_INC | (u64)(uint32_t)(ex.e + agg));
+                        s_excl = (uint32_t)ex.e;
+                    }
                     // sticky: the status words are only ever raised (atomicMax) after this
                     if (to) { atomicMax(&M->status, CODEC_PEE_ELOOKBACK); atomicAdd(diag + 2, 1u); }
                     if (fb) atomicAdd(diag, 1u);
@@ -1443,7 +1458,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
             if (c == 0) {
                 M->T = Tthr; M->maxval = maxval; M->L = (int)L; M->nc = nc; M->ntiles = ntiles; M->h = H; M->w = W;
                 if (L == 0) { M->end = -1; M->tile_end = -1; }   // status: below (out of place) / memset (in place)
-                if (!INPLACE) M->reserved[0] = M->reserved[1] = M->reserved[2] = 0;
+                if (sc) M->reserved[0] = M->reserved[1] = M->reserved[2] = 0;
             }
             // the chunk holding `end` (or the last one on overflow) reports the capacity seen so
             // far: exact when it is the last chunk, else a lower bound (later chunks are not counted)
@@ -1455,7 +1470,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
             if (last && excl + agg < L) {
                 M->end = nc - 1;
                 M->tile_end = ntiles - 1;
-                if (INPLACE) atomicMax(&M->status, 1);
+                if (!sc) atomicMax(&M->status, 1);
             }
         }
         lds_barrier();   // lm32 zeroing vs the ORs below
@@ -1531,16 +1546,15 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
             LB_STAMP(7);
             nun = block_sum_u32_lds<256>(unsafe_n, sh);   // also orders the lm32 ORs
             LB_STAMP(8);
-            if (INPLACE && tid == 0 && nun) atomicAdd(&M->lm_count, (int)nun);
+            if (!sc && tid == 0 && nun) atomicAdd(&M->lm_count, (int)nun);
         }
         LB_STAMP(4);
         if (tid == 0) {   // `end` is in this chunk (or there is none): later chunks need no cursor
             const bool fin = (excl < L && excl + agg >= L) || (L == 0 && c == 0) || (last && excl + agg < L);
             if (fin) {
                 __hip_atomic_store(fin_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (INPLACE) {
-                    atomicAdd(ctl, 1u);
-                } else {   // no meta atomics out of place: the chunk holding `end` writes them
+                if (INPLACE) atomicAdd(ctl, 1u);
+                if (sc) {   // no meta atomics (nothing zeroed it): the chunk holding `end` writes them
                     M->status = (last && excl + agg < L) ? 1 : 0;
                     M->lm_count = (int)(uexcl + nun);
                 }
@@ -1575,19 +1589,18 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
 // The extract's read-ahead (self-cleaning payload writes): the bits of the first `need` (1..63)
 // inner candidates at or after item it0, in rank order, as the low bits of a u64 -- what
 // the following chunks will recover, computed from their (read-only) stego pixels and map
-// words.  One wave, 4 items per lane per round, rounds until `need` bits or `end`.
+// words.  One wave, 4 items per lane per round.  The first round's loads are issued early
+// (load(), at the chunk's start, so they land during the look-back); bits() consumes them
+// and runs further rounds only if those 256 items held fewer than `need` inner candidates.
 template <typename T>
-__device__ u64 pee_read_ahead(const T* src, const u64* lm, int W, int CR, uint32_t items, int end, int Tthr, uint32_t it0,
-                              uint32_t need) {
+struct PeeReadAhead {
     typedef typename Vec8<T>::type V;
-    const int lane = threadIdx.x & 63;
-    u64 ra = 0ull;
-    uint32_t got = 0;
-    for (uint32_t itb = it0; got < need && itb < items && (int)(4 * itb) <= end; itb += 256u) {   // uniform
-        V v0[4], v1[4];
-        u64 lw[4];
+    V v0[4], v1[4];
+    u64 lw[4];
+    __device__ __forceinline__ void load(const T* src, const u64* lm, int W, int CR, uint32_t items, uint32_t itb) {
+        const int lane = threadIdx.x & 63;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {   // all loads of the round in flight together (clamped addresses)
+        for (int u = 0; u < 4; ++u) {   // clamped addresses: every load is valid
             const uint32_t it = min(itb + (uint32_t)(u * 64 + lane), items - 1u);
             const uint32_t r = it / (uint32_t)CR, cc = it - r * (uint32_t)CR;
             const size_t o = (size_t)(2 * r) * W + (size_t)cc * 8;
@@ -1595,35 +1608,44 @@ __device__ u64 pee_read_ahead(const T* src, const u64* lm, int W, int CR, uint32
             v1[u] = *reinterpret_cast<const V*>(src + o + W);
             lw[u] = lm[(4 * it) >> 6];
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t it = itb + (uint32_t)(u * 64 + lane);
-            const u64 mw = lw[u] >> ((4 * it) & 63);
-            uint32_t pk = 0, n = 0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int k = (int)(4 * it) + q;
-                const int x = (int)get_px(v1[u], 2 * q + 1);
-                const int e2 = x - med3((int)get_px(v1[u], 2 * q), (int)get_px(v0[u], 2 * q + 1), (int)get_px(v0[u], 2 * q));
-                const bool inner = it < items && k <= end && !((mw >> q) & 1ull) && e2 >= -2 * Tthr && e2 < 2 * Tthr;
-                pk |= (inner ? (uint32_t)(e2 & 1) : 0u) << n;
-                n += inner ? 1u : 0u;
-            }
-            const uint32_t incl = wave_incl_scan(n);
-            const uint32_t pos = got + incl - n;
-            u64 contrib = pos < 64u ? (u64)pk << pos : 0ull;
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) contrib |= __shfl_xor(contrib, o, 64);
-            ra |= contrib;
-            got += (uint32_t)__shfl(incl, 63, 64);
-        }
     }
-    return need >= 64u ? ra : (ra & ((1ull << need) - 1ull));
-}
+    __device__ u64 bits(const T* src, const u64* lm, int W, int CR, uint32_t items, int end, int Tthr, uint32_t it0,
+                        uint32_t need) {
+        const int lane = threadIdx.x & 63;
+        u64 ra = 0ull;
+        uint32_t got = 0;
+        for (uint32_t itb = it0; got < need && itb < items && (int)(4 * itb) <= end; itb += 256u) {   // uniform
+            if (itb != it0) load(src, lm, W, CR, items, itb);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t it = itb + (uint32_t)(u * 64 + lane);
+                const u64 mw = lw[u] >> ((4 * it) & 63);
+                uint32_t pk = 0, n = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int k = (int)(4 * it) + q;
+                    const int x = (int)get_px(v1[u], 2 * q + 1);
+                    const int e2 = x - med3((int)get_px(v1[u], 2 * q), (int)get_px(v0[u], 2 * q + 1), (int)get_px(v0[u], 2 * q));
+                    const bool inner = it < items && k <= end && !((mw >> q) & 1ull) && e2 >= -2 * Tthr && e2 < 2 * Tthr;
+                    pk |= (inner ? (uint32_t)(e2 & 1) : 0u) << n;
+                    n += inner ? 1u : 0u;
+                }
+                const uint32_t incl = wave_incl_scan(n);
+                const uint32_t pos = got + incl - n;
+                u64 contrib = pos < 64u ? (u64)pk << pos : 0ull;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) contrib |= __shfl_xor(contrib, o, 64);
+                ra |= contrib;
+                got += (uint32_t)__shfl(incl, 63, 64);
+            }
+        }
+        return need >= 64u ? ra : (ra & ((1ull << need) - 1ull));
+    }
+};
 
 // extract: chunks up to the one holding `end` recover bits + pixels (look-back over the
 // inner-candidate counts); later chunks are a plain copy (out of place) or skipped.
-template <typename T, bool NT, bool INPLACE>
+template <typename T, bool NT, bool INPLACE, bool SC = false>
 __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, int H, int W,
                                                       const codec_pee_meta* __restrict__ meta_all,
                                                       const u64* __restrict__ lm_all, int lmw, int nchunks, int B,
@@ -1637,7 +1659,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
     // self-cleaning (PEE_MODE_SC, small out-of-place batches): status words by call parity, and
     // the payload written without atomics or a zeroed buffer -- every word by the chunk holding
     // its first bit, which reads the word's later bits ahead from the following chunks' pixels
-    const bool sc = !INPLACE && (mode & PEE_MODE_SC);
+    constexpr bool sc = !INPLACE && SC;   // a separate instantiation: the read-ahead's registers
     const size_t stride = (size_t)B * nchunks;
     // the chunk's recovered bits: ranks [excl, excl + agg), agg <= 4096, from word excl / 64
     __shared__ u64 pbuf[PEE_CHUNK * 4 / 64 + 2];
@@ -1695,6 +1717,11 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
                 if (it < items) lwv[u] = lm[(4 * it) >> 6];
             }
         }
+        // the read-ahead's first round (wave 1): the first 256 items after this chunk, issued
+        // behind the chunk's own loads so that they land while wave 0 looks back (used only if
+        // this chunk's last payload word is incomplete; c == j without tickets)
+        PeeReadAhead<T> rah;
+        if (sc && j < cend && tid >= 64 && tid < 128) rah.load(src, lm, W, CR, items, (uint32_t)(j + 1) * PEE_CHUNK);
         int c = j;
         if (j <= cend && !noticket) {   // exactly cend+1 slots take tickets 0..cend
             if (tid == 0) s_v = atomicAdd(ctl + 32 + 32 * (size_t)b, 1u);
@@ -1821,8 +1848,8 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
                 const bool ahead = c < cend && (f & 63u) != 0u;   // uniform
                 if (ahead) {
                     if (tid >= 64 && tid < 128) {
-                        const u64 ra = pee_read_ahead<T>(src, lm, W, CR, items, end, Tthr, (uint32_t)(c + 1) * PEE_CHUNK,
-                                                         64u - (f & 63u));
+                        const u64 ra = rah.bits(src, lm, W, CR, items, end, Tthr, (uint32_t)(c + 1) * PEE_CHUNK,
+                                                64u - (f & 63u));
                         if (tid == 64) s_ra = ra;
                     }
                     lds_barrier();
@@ -3218,9 +3245,8 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
         // atomics out of place, so only in place (and the ticket modes) zero it
         if (flat && (mode & PEE_MODE_NOTICKET) && knob("CODEC_PEE_SELFCLEAN", 1)) mode |= PEE_MODE_SC;
         if (!(mode & PEE_MODE_SC))
-            HIP_TRY(pee_zero(st, stw, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4, inplace ? meta : nullptr,
-                             inplace ? (size_t)P->B * sizeof(codec_pee_meta) : 0, inplace ? lm : nullptr,
-                             inplace ? (size_t)P->B * P->lm_words * 8 : 0));
+            HIP_TRY(pee_zero(st, stw, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4, meta, (size_t)P->B * sizeof(codec_pee_meta),
+                             inplace ? lm : nullptr, inplace ? (size_t)P->B * P->lm_words * 8 : 0));
         ProfScope prof(st, CODEC_K_PEE_EMBED1);
         const long long total = pee_total_slots(P->B, L.nchunks, pee_group8(P->B, mode, inplace));
         long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));
@@ -3229,10 +3255,11 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
         const uint32_t spin_max = (uint32_t)debug_knob("CODEC_PEE_LB_SPINS", inplace ? (1 << 22) : (1 << 14));
         const int dbg_skip = (int)debug_knob("CODEC_PEE_DEBUG_SKIP", 0) - 1;
         uint32_t* diag = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.diag);
-#define PE1(TT, NTV, IP) hipLaunchKernelGGL((k_pee_embed1<TT, NTV, IP>), dim3((unsigned)g), dim3(256), 0, st, \
+#define PE1S(TT, NTV, IP, SCV) hipLaunchKernelGGL((k_pee_embed1<TT, NTV, IP, SCV>), dim3((unsigned)g), dim3(256), 0, st, \
             static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, \
             reinterpret_cast<const u64*>(payload), P->payload_words, L.nchunks, P->B, stw, ctl, meta, \
             reinterpret_cast<u64*>(lm), P->lm_words, mode, spin_max, dbg_skip, diag, tps)
+#define PE1(TT, NTV, IP) do { if (!(IP) && (mode & PEE_MODE_SC)) PE1S(TT, NTV, false, true); else PE1S(TT, NTV, IP, false); } while (0)
         if (P->bytes == 2) {
             if (inplace) { if (nt) PE1(uint16_t, true, true); else PE1(uint16_t, false, true); }
             else { if (nt) PE1(uint16_t, true, false); else PE1(uint16_t, false, false); }
@@ -3241,6 +3268,7 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
             else { if (nt) PE1(uint8_t, true, false); else PE1(uint8_t, false, false); }
         }
 #undef PE1
+#undef PE1S
         LAUNCH_CHECK("k_pee_embed1");
         // odd H: the last row of each slice belongs to no row pair (no candidate, no MED
         // neighbour); out of place it is copied verbatim
@@ -3463,10 +3491,11 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
         const uint32_t spin_max = (uint32_t)debug_knob("CODEC_PEE_LB_SPINS", inplace ? (1 << 22) : (1 << 14));
         const int dbg_skip = (int)debug_knob("CODEC_PEE_DEBUG_SKIP", 0) - 1;
         uint32_t* diag = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.diag);
-#define PX1(TT, NTV, IP) hipLaunchKernelGGL((k_pee_extract1<TT, NTV, IP>), dim3((unsigned)g), dim3(256), 0, st, \
+#define PX1S(TT, NTV, IP, SCV) hipLaunchKernelGGL((k_pee_extract1<TT, NTV, IP, SCV>), dim3((unsigned)g), dim3(256), 0, st, \
             static_cast<const TT*>(stego), static_cast<TT*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm), \
             P->lm_words, L.nchunks, P->B, stw, ctl, reinterpret_cast<u64*>(payload_out), P->payload_words, mode, spin_max, \
             dbg_skip, diag)
+#define PX1(TT, NTV, IP) do { if (!(IP) && (mode & PEE_MODE_SC)) PX1S(TT, NTV, false, true); else PX1S(TT, NTV, IP, false); } while (0)
         if (P->bytes == 2) {
             if (inplace) { if (nt) PX1(uint16_t, true, true); else PX1(uint16_t, false, true); }
             else { if (nt) PX1(uint16_t, true, false); else PX1(uint16_t, false, false); }
@@ -3475,6 +3504,7 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
             else { if (nt) PX1(uint8_t, true, false); else PX1(uint8_t, false, false); }
         }
 #undef PX1
+#undef PX1S
         LAUNCH_CHECK("k_pee_extract1");
         if ((P->H & 1) && !inplace) HIP_TRY(pee_copy_last_rows(P, stego, cover_out, st));
         return 0;
