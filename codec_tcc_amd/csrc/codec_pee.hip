@@ -1737,6 +1737,11 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
                 // the in-place look-back flag (codec_pee_extract_flag_offset) reads clear after
                 // this call: an earlier in-place call may have set it, out of place nothing does
                 if (b == 0 && j == 0) __hip_atomic_store(ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // the next call's finished flag (an embed's) starts clear: every self-cleaning
+                // call clears the other parity's flag, whichever kernel it is
+                if (j == 0)
+                    __hip_atomic_store(ctl + 32 + 32 * (size_t)b + (par ? PEE_LINE_FIN0 : PEE_LINE_FIN1), 0u,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             par = __shfl(par, 0, 64);
         }

@@ -17,7 +17,7 @@ typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
 constexpr int H = 2048, W = 2048, CR = W / 8;
-constexpr int NCHUNK = 30;                    // ~ the chunks up to `end` (1 KB at T = 2)
+constexpr int NCHUNK = 24;   // ~ the chunks up to `end` (30 at 1 KB, T = 2); divisible by ring depths 1-4
 constexpr int NT = 1024;
 
 __device__ __forceinline__ void lds_barrier() {
@@ -26,7 +26,9 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("" ::: "memory");
 }
 
-template <int D, bool BAR, int VALU>
+// EARLY: the slot's refill is issued right after its data is taken (into temporaries), before
+// the barrier and the compute -- D loads stay in flight through the barrier
+template <int D, bool BAR, int VALU, bool EARLY = false>
 __global__ __launch_bounds__(NT) void inplace_stream(unsigned short* img, int nchunk, unsigned* sink) {
     __shared__ unsigned pad[21 * 1024];   // one workgroup per CU, as the embed's pad
     const size_t npx = (size_t)H * W;
@@ -50,19 +52,30 @@ __global__ __launch_bounds__(NT) void inplace_stream(unsigned short* img, int nc
             const int k = k0 + d;
             v4u a = r0[d], b = r1[d];
             asm volatile("" ::"v"(a.x), "v"(b.x));
+            const unsigned so = ro[d];
+            if (EARLY) {
+                const unsigned it = (unsigned)(k + D) * NT + threadIdx.x;
+                const unsigned kk = k + D < nchunk ? it : threadIdx.x;
+                const unsigned r = kk / CR, c = kk - r * CR;
+                ro[d] = 2u * r * W + 8u * c;
+                r0[d] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(s + ro[d]));
+                r1[d] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(s + ro[d] + W));
+            }
             unsigned x = a.x ^ b.y;
 #pragma unroll
             for (int q = 0; q < VALU; ++q) x = (x * 0x9E37u + (b.z >> (q & 7))) ^ a.w;
             acc += x;
             b.x ^= (acc & 0u);
             if (BAR) lds_barrier();
-            __builtin_nontemporal_store(b, reinterpret_cast<v4u*>(s + ro[d] + W));
-            const unsigned it = (unsigned)(k + D) * NT + threadIdx.x;
-            const unsigned kk = k + D < nchunk ? it : threadIdx.x;
-            const unsigned r = kk / CR, c = kk - r * CR;
-            ro[d] = 2u * r * W + 8u * c;
-            r0[d] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(s + ro[d]));
-            r1[d] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(s + ro[d] + W));
+            __builtin_nontemporal_store(b, reinterpret_cast<v4u*>(s + so + W));
+            if (!EARLY) {
+                const unsigned it = (unsigned)(k + D) * NT + threadIdx.x;
+                const unsigned kk = k + D < nchunk ? it : threadIdx.x;
+                const unsigned r = kk / CR, c = kk - r * CR;
+                ro[d] = 2u * r * W + 8u * c;
+                r0[d] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(s + ro[d]));
+                r1[d] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(s + ro[d] + W));
+            }
         }
     }
     if (acc == 0xFFFFFFFFu) sink[0] = acc + pad[threadIdx.x & 7];
@@ -117,7 +130,7 @@ int main() {
     CK(hipEventCreate(&e1));
     const double algo = (double)B * NCHUNK * NT * 48.0;   // 32 B read + 16 B written per item
     for (int pass = 0; pass < 2; ++pass) {
-        for (int variant = 0; variant < 14; ++variant) {
+        for (int variant = 0; variant < 19; ++variant) {
             const char* name = "";
             float sum = 0.f, best = 1e9f;
             const int reps = 20;
@@ -138,6 +151,11 @@ int main() {
                 case 11: name = "quarters ring 2"; inplace_quarters<2><<<4 * B, 256>>>(img, NCHUNK, sink); break;
                 case 12: name = "quarters ring 4"; inplace_quarters<4><<<4 * B, 256>>>(img, NCHUNK, sink); break;
                 case 13: name = "ring 2 +barrier +valu 96"; inplace_stream<2, true, 96><<<B, NT>>>(img, NCHUNK, sink); break;
+                case 14: name = "early ring 2 +barrier +valu 48"; inplace_stream<2, true, 48, true><<<B, NT>>>(img, NCHUNK, sink); break;
+                case 15: name = "early ring 3 +barrier +valu 48"; inplace_stream<3, true, 48, true><<<B, NT>>>(img, NCHUNK, sink); break;
+                case 16: name = "early ring 2 +barrier"; inplace_stream<2, true, 0, true><<<B, NT>>>(img, NCHUNK, sink); break;
+                case 17: name = "early ring 1 +barrier +valu 48"; inplace_stream<1, true, 48, true><<<B, NT>>>(img, NCHUNK, sink); break;
+                case 18: name = "early ring 4 +barrier +valu 48"; inplace_stream<4, true, 48, true><<<B, NT>>>(img, NCHUNK, sink); break;
                 }
                 CK(hipGetLastError());
                 CK(hipEventRecord(e1, 0));
