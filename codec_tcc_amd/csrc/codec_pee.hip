@@ -1237,28 +1237,23 @@ __device__ unsigned long long g_lb_trace[LB_TRACE_SLOTS * 12];
 // self-cleaning out-of-place look-back (round 4): no zeroing launch before the pass.  The
 // workspace holds TWO status-word buffers; a call uses buffer `par` and clears its own words
 // of the other one for the next call.  `par` is the parity of the call count, which every
-// workgroup learns from the returning atomic that counts its arrival: per slice 8 shard
-// counters (chunk c counts on shard c % 8, n_g arrivals per call), call index = old / n_g.
+// workgroup learns from the returning atomic that counts its arrival: one counter word per
+// chunk (after the per-slice lines), call index = its old value.  (8 shard counters per slice
+// put 32 same-address atomics of a 2048^2 slice in series, ~1 us on the embed's critical path.)
 // The finished flag is doubled the same way; meta is written without atomics (status by the
 // chunk holding `end`, lm_count from the look-back's second field).  Calls that still zero
 // (in place, ticket modes) use buffer 1 and finished flag 1 and reset the counters, so the
 // next self-cleaning call (index 0: buffer 0) starts clean.
 #define PEE_MODE_SC 8
-#define PEE_CTL_WORDS(B) (32 + 32 * (size_t)(B))
+// ctl: 32 words, 32 per slice (ticket, finished flags), then one arrival counter per chunk
+#define PEE_CTL_WORDS(B, NCH) (32 + 32 * (size_t)(B) + (size_t)(B) * (size_t)(NCH))
 #define PEE_LINE_TICKET 0
 #define PEE_LINE_FIN0 1
 #define PEE_LINE_FIN1 4
-#define PEE_LINE_ARR 8    // 8 x u64 shard counters (words 8..23 of the slice's 32-word line)
-__device__ __forceinline__ u64 pee_arrive(uint32_t* line, int c) {   // returns the shard's old count
-    return atomicAdd(reinterpret_cast<unsigned long long*>(line + PEE_LINE_ARR + 2 * (c & 7)), 1ull);
+__device__ __forceinline__ uint32_t pee_arrive(uint32_t* ctl, int B, int b, int nchunks, int c) {   // old count
+    return atomicAdd(ctl + 32 + 32 * (size_t)B + (size_t)b * nchunks + c, 1u);
 }
-__device__ __forceinline__ int pee_parity_of(u64 old, int c, int nchunks) {
-    const uint32_t ng = (uint32_t)((nchunks - (c & 7) + 7) >> 3);   // chunks of this slice on shard c % 8
-    return (int)((old / ng) & 1ull);
-}
-__device__ __forceinline__ int pee_call_parity(uint32_t* line, int c, int nchunks) {
-    return pee_parity_of(pee_arrive(line, c), c, nchunks);
-}
+__device__ __forceinline__ int pee_parity_of(uint32_t old) { return (int)(old & 1u); }
 #define PEE_SKIP 0xFFFFFFFFu
 #define PEE_STOP 0xFFFFFFFEu
 template <typename T, bool NT, bool INPLACE, bool SC = false>
@@ -1319,7 +1314,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                 // full path
                 uint32_t dn = dnA;
                 if constexpr (sc) {
-                    par = pee_call_parity(line, j, nchunks);
+                    par = pee_parity_of(pee_arrive(ctl, B, b, nchunks, j));
                     dn = par ? dnB : dnA;
                 }
                 cc = (mode & PEE_MODE_NOTICKET) ? (uint32_t)j : atomicAdd(tick, 1u);
@@ -1705,8 +1700,8 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
         if (!INPLACE) pee_load_chunk<T, NT>(src, W, CR, items, j, a0, a1, o0);
         // every slot arrives (copy chunks too); the returned count is used only later, so the
         // map-word loads below are not held back behind the atomic's round trip
-        u64 arr_old = 0ull;
-        if (sc && tid == 0) arr_old = pee_arrive(ctl + 32 + 32 * (size_t)b, j);
+        uint32_t arr_old = 0u;
+        if (sc && tid == 0) arr_old = pee_arrive(ctl, B, b, nchunks, j);
         const u64* lm = lm_all + (size_t)b * lmw;
         const bool noticket = !INPLACE && (mode & PEE_MODE_NOTICKET);
         u64 lwv[4] = {0, 0, 0, 0};   // location-map word of each item (4 bits of it used)
@@ -1732,7 +1727,7 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
         int par = 1;   // status-word buffer (calls that zero first use buffer 1)
         if (sc) {      // wave 0 (the look-back) learns the call parity
             if (tid == 0) {
-                par = pee_parity_of(arr_old, j, nchunks);
+                par = pee_parity_of(arr_old);
                 lb_store(status_all + (1 - par) * stride + (size_t)b * nchunks + j, 0ull);   // next call's word
                 // the in-place look-back flag (codec_pee_extract_flag_offset) reads clear after
                 // this call: an earlier in-place call may have set it, out of place nothing does
@@ -2174,10 +2169,26 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
     int par = 0, last = -1;
     bool live = L > 0;   // uniform: the chunk holding bit L-1 is still to come
 
-    // one chunk, processed in the ring registers, then the ring slot is refilled
+    // one chunk, processed in the ring registers, then the ring slot is refilled.  D == 1
+    // (EARLY): the chunk's data is taken into working registers and the slot refilled at
+    // once, so the next chunk's loads are in flight through this chunk's scan barrier and
+    // compute (tools/ubench_inplace.hip: "early ring 1" streams the in-place pattern ~3 %
+    // faster than a ring of 2 refilled after the stores, with the same one chunk of reads
+    // wasted past `end`)
+    constexpr bool EARLY = D == 1;
+    auto refill = [&](int d) {
+        // in place, once `end` is reached the rest of the group refills from one clamped
+        // address (L2 hits): the group still runs to its end, see the loop below
+        ro[d] = it_a < items && (!INPLACE || live) ? ahead.o : off_last;
+        ss_load_at<T, NT>(src, (uint32_t)W, ro[d], r0[d], r1[d]);
+        ahead.step(dr, (uint32_t)CR, ostep, owrap);
+        it_a += SS_THREADS;
+    };
     auto chunk = [&](int d, int k) {
-        V& v0 = r0[d];
-        V& v1 = r1[d];
+        V w0, w1;
+        if constexpr (EARLY) { w0 = r0[d]; w1 = r1[d]; }
+        V& v0 = EARLY ? w0 : r0[d];
+        V& v1 = EARLY ? w1 : r1[d];
         const uint32_t it = (uint32_t)k * SS_THREADS + tid;
         const bool ok = it < items;
         const uint32_t o0 = ro[d];
@@ -2185,6 +2196,7 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
         // the chunk's registers are waited for here, once, outside any branch (an empty asm
         // reading them): the compiler then counts vmcnt exactly around the branches below
         asm volatile("" ::"v"(v0.x), "v"(v1.x));
+        if constexpr (EARLY) refill(d);
         SS_STAMP(4 * k + 1);
         uint32_t wm = 0;
         bool touched = false;
@@ -2280,12 +2292,7 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
             stv<NT>(ok ? reinterpret_cast<V*>(dst + o0) : sink_v, v0);
             stv<NT>(ok ? reinterpret_cast<V*>(dst + o0 + W) : sink_v + 1, v1);
         }
-        // in place, once `end` is reached the rest of the group refills from one clamped
-        // address (L2 hits): the group still runs to its end, see the loop below
-        ro[d] = it_a < items && (!INPLACE || live) ? ahead.o : off_last;
-        ss_load_at<T, NT>(src, (uint32_t)W, ro[d], v0, v1);
-        ahead.step(dr, (uint32_t)CR, ostep, owrap);
-        it_a += SS_THREADS;
+        if constexpr (!EARLY) refill(d);
         SS_STAMP(4 * k + 3);
     };
 
@@ -3013,7 +3020,7 @@ static PeeWs pee_ws(const codec_pee_params* P) {
     // two status-word buffers (PEE_MODE_SC), then ctl; zeroing calls clear them all together
     L.ctl = L.st + 2 * (size_t)P->B * L.nchunks * 8;
     // diag: 4 cumulative uint32 counters (codec_pee_diag_offset), outside the per-call memset
-    L.diag = align_up(L.ctl + PEE_CTL_WORDS(P->B) * 4, 16);
+    L.diag = align_up(L.ctl + PEE_CTL_WORDS(P->B, L.nchunks) * 4, 16);
     // capacity-control error histogram (codec_pee_capacity; cleared by that call)
     L.hist = align_up(L.diag + 16, 256);
     // slice-serial kernels: per-lane sink for stores that must not land (contents unused)
@@ -3215,8 +3222,10 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
         // ring depth of the in-place embed: it does not know `end` in advance, so the D - 1
         // chunks it has in flight past it are wasted reads; at 256 x 2048^2 the steady state
         // is HBM-bound (~5 TB/s of reads + writes), and D = 2 keeps enough in flight:
-        // 0.0825 -> 0.0789 ms (D = 3: 0.0824; tools/ab_depth.sh).  CODEC_PEE_SS_D=4 restores 4.
-        const long long ss_d = pay_lds ? knob("CODEC_PEE_SS_D", 2) : 4;
+        // 0.0825 -> 0.0789 ms (D = 3: 0.0824; tools/ab_depth.sh).  D = 1 refills early (the
+        // next chunk's loads go out before this chunk's barrier and compute): 0.0746 -> 0.0726
+        // ms (profiles/r04/ip_early_ab.log).  CODEC_PEE_SS_D=2 / 4 restore the late refill.
+        const long long ss_d = pay_lds ? knob("CODEC_PEE_SS_D", 1) : 4;
 #define PES1D(TT, NTV, IP, DD) hipLaunchKernelGGL((k_pee_embed_ss<TT, NTV, IP, DD, true>), dim3((unsigned)P->B), dim3(SS_THREADS), 0, st, \
             static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, tps, \
             reinterpret_cast<const u64*>(payload), P->payload_words, meta, reinterpret_cast<u64*>(lm), P->lm_words, \
@@ -3224,6 +3233,7 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
         if (P->bytes == 2) {
             if (inplace) {
                 if (ss_d == 2 && nt) PES1D(uint16_t, true, true, 2);
+                else if (ss_d == 1 && nt) PES1D(uint16_t, true, true, 1);
                 else if (nt) PES(uint16_t, true, true); else PES(uint16_t, false, true);
             }
             else { if (nt) PES(uint16_t, true, false); else PES(uint16_t, false, false); }
@@ -3250,7 +3260,7 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
         // atomics out of place, so only in place (and the ticket modes) zero it
         if (flat && (mode & PEE_MODE_NOTICKET) && knob("CODEC_PEE_SELFCLEAN", 1)) mode |= PEE_MODE_SC;
         if (!(mode & PEE_MODE_SC))
-            HIP_TRY(pee_zero(st, stw, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4, meta, (size_t)P->B * sizeof(codec_pee_meta),
+            HIP_TRY(pee_zero(st, stw, L.ctl - L.st + PEE_CTL_WORDS(P->B, L.nchunks) * 4, meta, (size_t)P->B * sizeof(codec_pee_meta),
                              inplace ? lm : nullptr, inplace ? (size_t)P->B * P->lm_words * 8 : 0));
         ProfScope prof(st, CODEC_K_PEE_EMBED1);
         const long long total = pee_total_slots(P->B, L.nchunks, pee_group8(P->B, mode, inplace));
@@ -3487,7 +3497,7 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
                               ((int)(knob("CODEC_PEE_X_GROUP", 32) / 8) << 8);
         if (flat && (mode & PEE_MODE_NOTICKET) && knob("CODEC_PEE_SELFCLEAN", 1)) mode |= PEE_MODE_SC;
         if (!(mode & PEE_MODE_SC))
-            HIP_TRY(pee_zero(st, payload_out, (size_t)P->B * P->payload_words * 8, stw, L.ctl - L.st + PEE_CTL_WORDS(P->B) * 4));
+            HIP_TRY(pee_zero(st, payload_out, (size_t)P->B * P->payload_words * 8, stw, L.ctl - L.st + PEE_CTL_WORDS(P->B, L.nchunks) * 4));
         ProfScope prof(st, CODEC_K_PEE_EXTRACT1);
         const long long total = pee_total_slots(P->B, L.nchunks, pee_group8(P->B, mode, inplace));
         long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));

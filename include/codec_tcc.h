@@ -231,7 +231,9 @@ typedef struct codec_pee_meta {
 #define CODEC_PEE_ELOOKBACK 2
 
 /* Zero-initialise the workspace once before its first use (the diagnostic counters live
- * in it; everything else is cleared by the calls themselves). */
+ * in it; everything else is cleared by the calls themselves).  Small out-of-place batches
+ * (B <= 7) keep call-to-call state in it (status words by call parity, per-chunk arrival
+ * counts): use one workspace with one (B, H, W), or zero it again before changing them. */
 size_t codec_pee_workspace_bytes(const codec_pee_params* P);
 /* Byte offset in the workspace of a uint32 flag that codec_pee_extract's IN-PLACE single
  * pass sets (non-zero) when a chunk's cursor look-back gave up (the recovered payload of

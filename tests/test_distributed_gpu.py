@@ -155,6 +155,30 @@ def test_bench_launches_its_own_ranks():
     assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr
 
 
+@pytest.mark.timeout(200)
+def test_bench_failed_rank_on_gpu_box():
+    """VERDICT r3 item 1 on the GPU box: `bench.py --gpus 2 --backend gloo` with rank 1 made to
+    exit right after init_process_group while rank 0 is stuck returns that status within a
+    minute and leaves no rank alive (the CPU suite runs the same cases, test_bench_host.py)."""
+    import time
+
+    from test_bench_host import _gone, _kill_all, _launcher, _rank_pids
+    t0 = time.monotonic()
+    proc = _launcher({"CODEC_BENCH_FAIL_RANK": "1", "CODEC_BENCH_STALL_RANK": "0"})
+    pids = []
+    try:
+        pids, _ = _rank_pids(proc)
+        rc = proc.wait(timeout=120)
+        err = proc.stderr.read()
+        assert rc == 3 and "rank 1 exited with 3" in err, err
+        assert time.monotonic() - t0 < 90
+        assert _gone(pids), pids
+    finally:
+        if proc.poll() is None:
+            proc.kill()
+        _kill_all(pids)
+
+
 def _rccl_worker(port, q):
     """One rank over the nccl (= RCCL) backend: the exchanges' RCCL branches
     (all_gather_into_tensor, all_reduce) on real kernel records."""
