@@ -1962,6 +1962,9 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
                 if ((t & 63) == 0 && (j >> 6) < E.mw) E.maps[(size_t)b * E.mw + (j >> 6)] = bal;
             }
         }
+        // map words past the last round (no window bit): 0, so the whole map is defined (the
+        // rounds above wrote the words of every 1024-bit step that starts below lim)
+        for (int w = ((lim + 1023) / 1024) * 16 + t; w < E.mw; w += 1024) E.maps[(size_t)b * E.mw + w] = 0ull;
         DTS(11);
     }
     if (nsplit > 0 && !collected) {   // the other decision paths: slots still to clear
@@ -2077,7 +2080,10 @@ __global__ __launch_bounds__(256) void k_embed(const Tin* __restrict__ cover, To
     const int b = blockIdx.y;
     load_win(meta + b, &W);
     const int j = blockIdx.x * 256 + threadIdx.x;
-    if ((j & ~63) >= W.tot) return;   // whole wave past the end (uniform)
+    if ((j & ~63) >= W.tot) {   // whole wave past the end (uniform): its map word reads 0
+        if ((threadIdx.x & 63) == 0 && (j >> 6) < mw) maps[(size_t)b * mw + (j >> 6)] = 0ull;
+        return;
+    }
     uint32_t mapbit = 0;
     if (j < W.tot)
         mapbit = embed_bit<Tin, Tout>(cover + (size_t)b * npx, stego + (size_t)b * npx, npx, keep,

@@ -433,3 +433,19 @@ def test_split_decision_timeout_leaves_no_stale_slot(monkeypatch):
         assert torch.equal(enc.meta, ref.meta)
         assert torch.equal(enc.stego.view(torch.int16), ref.stego.view(torch.int16))
         assert torch.equal(enc.maps, ref.maps)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_maps_fully_defined(fused, monkeypatch):
+    """Every word of the location-map rows is written (zero past the bits used), whatever the
+    output buffer held before -- the fused decision's embed and k_embed alike."""
+    if not fused:
+        monkeypatch.setenv("CODEC_FUSED_EMBED", "0")
+    B, H, W = 2, 256, 256
+    covers = torch.from_numpy(np.stack([synth.ct12(H, W, 60 + i) for i in range(B)])).cuda()
+    msgs = [synth.payload(40, 3), synth.payload(400, 4)]   # short and long: many unused words
+    codec = Codec(B, H, W, dtype="uint16", beta=0.4, block=16)
+    pl = K.make_payloads(msgs, covers.device)
+    a = codec.encode(covers, pl, maps=torch.full((B, pl.map_words), -1, dtype=torch.int64, device=covers.device))
+    z = codec.encode(covers, pl, maps=torch.zeros((B, pl.map_words), dtype=torch.int64, device=covers.device))
+    assert torch.equal(a.maps, z.maps) and torch.equal(a.stego.view(torch.int16), z.stego.view(torch.int16))
