@@ -1168,9 +1168,11 @@ struct ListTerm {
 // itself, so no value of this launch can be read by the next one
 #define PLANE_ABANDONED 0x7FF8DEAD00000002ull
 #ifdef DECIDE_TS   // diagnostic build only (tools/decide_phases.py): phase timestamps into the term scratch
-#define DTS(k) do { if (threadIdx.x == 0 && blockIdx.y == 0) reinterpret_cast<long long*>(gterms + (size_t)blockIdx.x * HistCfg<T>::kBins)[HistCfg<T>::kBins - 16 + (k)] = wall_clock64(); } while (0)
+// (b, role: decide_body's slice and workgroup role -- k_decide's blockIdx.x / .y; k_scan_decide
+// runs slice blockIdx.y as role 0)
+#define DTS(k) do { if (threadIdx.x == 0 && role == 0) reinterpret_cast<long long*>(gterms + (size_t)b * HistCfg<T>::kBins)[HistCfg<T>::kBins - 16 + (k)] = wall_clock64(); } while (0)
 // plane workgroups of the split decision: 4 stamps each below the main's 16
-#define PTS(k) do { if (threadIdx.x == 0) reinterpret_cast<long long*>(gterms + (size_t)blockIdx.x * HistCfg<T>::kBins)[HistCfg<T>::kBins - 80 + 4 * (blockIdx.y - 1) + (k)] = wall_clock64(); } while (0)
+#define PTS(k) do { if (threadIdx.x == 0) reinterpret_cast<long long*>(gterms + (size_t)b * HistCfg<T>::kBins)[HistCfg<T>::kBins - 80 + 4 * (role - 1) + (k)] = wall_clock64(); } while (0)
 #else
 #define DTS(k) do { } while (0)
 #define PTS(k) do { } while (0)
