@@ -648,7 +648,8 @@ def bench_quality(args, torch, covers, stego, B, H, W):
            "pixels_changed_mean": float(np.mean([r["pixels_diferentes"] for r in q])),
            "kernels_ms": {k: round(v, 4) for k, v in kern.items()}}
     if "k_quality" in kern:
-        res["roofline"] = _roof("k_quality", B * H * W * 4, kern["k_quality"])   # read cover + stego
+        res["roofline"] = _roof("k_quality", B * H * W * 4, kern["k_quality"],   # read cover + stego
+                                pmc_traffic("k_quality", B, H, W, args.kind))
     return res
 
 

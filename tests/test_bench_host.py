@@ -86,8 +86,14 @@ def test_committed_pmc_summaries_resolve_every_bench_instance():
     for tag, ta in (("k_pee_embed1", {2: "false"}), ("k_pee_extract1", {2: "false"}),
                     ("k_pee_embed_ss", {2: "true", 5: "false"}), ("k_pee_extract_ss", {2: "true"})):
         assert bench.pmc_traffic(tag, 256, 2048, 2048, "ct12", ta) is not None, tag
-    for tag, ta in (("k_pee_embed_res", {}), ("k_pee_extract_ss", {2: "false"})):   # C3 (round 3 kernels)
+    for tag, ta in (("k_pee_embed_res", {}), ("k_pee_extract_ss", {2: "false"}), ("k_scan_decide", {}),
+                    ("k_restore_il", {})):   # C3
         assert bench.pmc_traffic(tag, 256, 512, 512, "ct12", ta) is not None, tag
+    for tag, ta in (("k_pee_embed1", {2: "false"}), ("k_pee_extract1", {2: "false"}), ("k_scan_fast", {})):   # C2
+        assert bench.pmc_traffic(tag, 1, 2048, 2048, "ct12", ta) is not None, tag
+    # every source is this round's
+    for tag, shape in (("k_pee_embed1", (256, 2048, 2048)), ("k_scan_decide", (256, 512, 512)), ("k_scan_fast", (1, 2048, 2048))):
+        assert "profiles/r04/" in bench.pmc_traffic(tag, *shape, "ct12", {2: "false"} if tag == "k_pee_embed1" else {})["source"]
 
 
 def _launcher(env_extra):
