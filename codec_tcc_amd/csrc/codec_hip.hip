@@ -1647,6 +1647,9 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
         // is written to its own list and summed with np_sum_wave.  Thread 0 then walks the
         // round's planes in order exactly like the sequential loop (same early exit).
         const int wv = t >> 6, lane = t & 63;
+        // the class's 16 layouts (one per s) into LDS now (`vals` is free until the windows):
+        // loaded after the decision they were one dependent global round trip (~2 us)
+        if (t < 16 * kLayW) reinterpret_cast<int32_t*>(vals)[t] = lay_all[t];
         const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
         for (int g = wv; g < ngrp; g += 16) {             // bit-plane ballots per rank group
             const int r = g * 64 + lane;
@@ -1824,8 +1827,8 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     __syncthreads();
     {
         const int sl = min(max(ctl_sh[1], 1), 16);
-        if (t < kLayW) lay_sh[t] = (wfast && nsplit > 0) ? reinterpret_cast<const int32_t*>(vals)[(sl - 1) * kLayW + t]
-                                                         : lay_all[(sl - 1) * kLayW + t];
+        if (t < kLayW) lay_sh[t] = wfast ? reinterpret_cast<const int32_t*>(vals)[(sl - 1) * kLayW + t]
+                                         : lay_all[(sl - 1) * kLayW + t];
     }
 
     DTS(3);

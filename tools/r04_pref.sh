@@ -1,0 +1,19 @@
+# decision: layouts preloaded on the wave path + the fused embed's cover prefetch -- LSB parity
+# suites, then C3 / C2 LSB A/B against the previous commit's library (alternating processes)
+cd "$GRAFT_REPO_ROOT" || exit 9
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_api.py -m gpu -x -q \
+  -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_pref.log 2>&1 || { tail -40 gpurun_out/pytest_pref.log; exit 1; }
+tail -2 gpurun_out/pytest_pref.log
+for r in 1 2 3; do
+  for L in new prev; do
+    timeout -k 10 200 python tools/tune_with_lib.py tools/bin/libcodec_$L.so --batch 256 --size 512 --rounds 3 --steps 10 --configs "[{}]" \
+      > gpurun_out/pref_c3_$L.$r.log 2>&1 || { tail gpurun_out/pref_c3_$L.$r.log; exit 1; }
+    echo "c3 $L: $(grep cfg gpurun_out/pref_c3_$L.$r.log)"
+    timeout -k 10 200 python tools/tune_with_lib.py tools/bin/libcodec_$L.so --batch 1 --size 2048 --rounds 3 --steps 10 --configs "[{}]" \
+      > gpurun_out/pref_c2_$L.$r.log 2>&1 || { tail gpurun_out/pref_c2_$L.$r.log; exit 1; }
+    echo "c2 $L: $(grep cfg gpurun_out/pref_c2_$L.$r.log)"
+  done
+done
+DTS_B=256 DTS_SIZE=512 timeout -k 10 200 python tools/decide_phases.py ct12 > gpurun_out/c3_decide_phases.txt 2>&1 || { tail -5 gpurun_out/c3_decide_phases.txt; exit 1; }
+grep -v amdgpu.ids gpurun_out/c3_decide_phases.txt
