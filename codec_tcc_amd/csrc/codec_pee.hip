@@ -2815,7 +2815,9 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
     }
 }
 
-template <typename T, bool NT, bool INPLACE, int D>
+// EARLY: the ring slot is refilled as soon as its data is taken (before the chunk's barrier
+// and compute), as the in-place embed does with D = 1 (k_pee_embed_ss)
+template <typename T, bool NT, bool INPLACE, int D, bool EARLY = false>
 __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restrict__ stego, T* cover, int H, int W,
                                                                const codec_pee_meta* __restrict__ meta_all,
                                                                const u64* __restrict__ lm_all, int lmw,
@@ -2895,15 +2897,26 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
         if (tid == 0 && (p_hi & 63u) == 0u) s_carry[p_par] = 0ull;
     };
 
+    auto refill = [&](int d) {   // branch-free; past chunk klast the last item's address, data unused
+        const bool in = it_a < items_l;
+        ro[d] = in ? ahead.o : off_last;
+        ss_load_at<T, NT>(src, (uint32_t)W, ro[d], r0[d], r1[d]);
+        rl[d] = lm[(4 * (in ? it_a : items_l - 1u)) >> 6];
+        ahead.step(dr, (uint32_t)CR, ostep, owrap);
+        it_a += SS_THREADS;
+    };
     auto chunk = [&](int d, int k) {
-        V& v0 = r0[d];
-        V& v1 = r1[d];
+        V w0, w1;
+        if constexpr (EARLY) { w0 = r0[d]; w1 = r1[d]; }
+        V& v0 = EARLY ? w0 : r0[d];
+        V& v1 = EARLY ? w1 : r1[d];
         const u64 lw = rl[d];
         const uint32_t it = (uint32_t)k * SS_THREADS + tid;
         const bool ok = it < items;
         const uint32_t o0 = ro[d];
         // the chunk's registers are waited for here, once, outside any branch (see k_pee_embed_ss)
         asm volatile("" ::"v"(v0.x), "v"(v1.x), "v"((uint32_t)lw));
+        if constexpr (EARLY) refill(d);
         uint32_t actm = 0;
         u64 wout = 0;
         bool wstore = false;
@@ -2967,14 +2980,7 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
             stv<NT>(ok ? reinterpret_cast<V*>(dst + o0) : sink_v, v0);
             stv<NT>(ok ? reinterpret_cast<V*>(dst + o0 + W) : sink_v + 1, v1);
         }
-        {   // refill (branch-free; past chunk klast the last item's address, data unused)
-            const bool in = it_a < items_l;
-            ro[d] = in ? ahead.o : off_last;
-            ss_load_at<T, NT>(src, (uint32_t)W, ro[d], v0, v1);
-            rl[d] = lm[(4 * (in ? it_a : items_l - 1u)) >> 6];
-            ahead.step(dr, (uint32_t)CR, ostep, owrap);
-            it_a += SS_THREADS;
-        }
+        if constexpr (!EARLY) refill(d);
     };
 
     const int nfull = nproc / D * D;
@@ -3471,7 +3477,18 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
         // ring refills right behind the chunk, 0.0531 -> 0.0517 ms at 256 x 512^2; in place 4
         // (2: 0.0747 -> 0.0761 ms at 256 x 2048^2; 6 is slower everywhere, 0.064 / 0.086)
         const long long xd = knob("CODEC_PEE_SSX_D", inplace ? 4 : 2);
-        if (P->bytes == 2 && nt && xd != 4) {
+        // early refill (the slot reloaded as soon as its data is taken): in place a ring of one
+        // refilled early beats the late ring of 4, 0.0752 -> 0.0726 ms (profiles/r04/ip_xearly_ab.log);
+        // CODEC_PEE_SSX_EARLY=0 restores the late refill (then CODEC_PEE_SSX_D picks 2 / 4 / 6)
+        const bool xe = knob("CODEC_PEE_SSX_EARLY", inplace ? 1 : 0) != 0;
+        const long long xde = knob("CODEC_PEE_SSX_D", inplace ? 1 : 2);
+#define PXSE(IP, DD) hipLaunchKernelGGL((k_pee_extract_ss<uint16_t, true, IP, DD, true>), dim3((unsigned)P->B), dim3(SS_THREADS), 0, st, \
+            static_cast<const uint16_t*>(stego), static_cast<uint16_t*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm), \
+            P->lm_words, reinterpret_cast<u64*>(payload_out), P->payload_words, ctl + 1, static_cast<char*>(workspace) + L.sink)
+        if (P->bytes == 2 && nt && xe) {
+            if (inplace) { if (xde == 1) PXSE(true, 1); else if (xde == 2) PXSE(true, 2); else PXSE(true, 4); }
+            else { if (xde == 1) PXSE(false, 1); else if (xde == 2) PXSE(false, 2); else PXSE(false, 4); }
+        } else if (P->bytes == 2 && nt && xd != 4) {
             if (inplace) { if (xd == 2) PXSD(uint16_t, true, true, 2); else PXSD(uint16_t, true, true, 6); }
             else { if (xd == 2) PXSD(uint16_t, true, false, 2); else PXSD(uint16_t, true, false, 6); }
         } else if (P->bytes == 2) {
@@ -3483,6 +3500,7 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
         }
 #undef PXS
 #undef PXSD
+#undef PXSE
         LAUNCH_CHECK("k_pee_extract_ss");
         if ((P->H & 1) && !inplace) HIP_TRY(pee_copy_last_rows(P, stego, cover_out, st));
         return 0;
