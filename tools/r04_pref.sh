@@ -1,5 +1,5 @@
-# decision: layouts preloaded on the wave path + the fused embed's cover prefetch -- LSB parity
-# suites, then C3 / C2 LSB A/B against the previous commit's library (alternating processes)
+# LSB code change A/B: the LSB parity suites with the new library, then C3 / C2 LSB against the
+# previous commit's library (tools/bin/libcodec_prev.so), alternating processes
 cd "$GRAFT_REPO_ROOT" || exit 9
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_api.py -m gpu -x -q \
@@ -15,5 +15,3 @@ for r in 1 2 3; do
     echo "c2 $L: $(grep cfg gpurun_out/pref_c2_$L.$r.log)"
   done
 done
-DTS_B=256 DTS_SIZE=512 timeout -k 10 200 python tools/decide_phases.py ct12 > gpurun_out/c3_decide_phases.txt 2>&1 || { tail -5 gpurun_out/c3_decide_phases.txt; exit 1; }
-grep -v amdgpu.ids gpurun_out/c3_decide_phases.txt
