@@ -584,8 +584,9 @@ def bench_lsb_inplace(args, torch, dist, world, dev, covers, B, H, W):
            "ms_per_step": round(el / args.steps * 1e3, 4), "roundtrip_ok": cover_ok and pay_ok and status_ok,
            "kernels_ms": {k: round(v, 4) for k, v in kern.items()}}
     rk = next((k for k in ("k_scan_rows_read", "k_scan_read") if k in kern), None)
-    if rk:
-        res["roofline"] = _roof(rk, B * H * W * 2, kern[rk])   # read-only pass over the cover
+    if rk:   # read-only pass over the cover
+        tag = "k_scan_rows" if rk == "k_scan_rows_read" else rk
+        res["roofline"] = _roof(rk, B * H * W * 2, kern[rk], pmc_traffic(tag, B, H, W, args.kind, {3: "false"} if tag == "k_scan_rows" else None))
     return res
 
 
