@@ -1173,9 +1173,12 @@ struct ListTerm {
 #define DTS(k) do { if (threadIdx.x == 0 && role == 0) reinterpret_cast<long long*>(gterms + (size_t)b * HistCfg<T>::kBins)[HistCfg<T>::kBins - 16 + (k)] = wall_clock64(); } while (0)
 // plane workgroups of the split decision: 4 stamps each below the main's 16
 #define PTS(k) do { if (threadIdx.x == 0) reinterpret_cast<long long*>(gterms + (size_t)b * HistCfg<T>::kBins)[HistCfg<T>::kBins - 80 + 4 * (role - 1) + (k)] = wall_clock64(); } while (0)
+// wave path: lane 0 of wave k stamps the end of its first round's work (slot R - 80 + k)
+#define WVTS(k) do { if ((threadIdx.x & 63) == 0 && role == 0) reinterpret_cast<long long*>(gterms + (size_t)b * HistCfg<T>::kBins)[HistCfg<T>::kBins - 80 + (k)] = wall_clock64(); } while (0)
 #else
 #define DTS(k) do { } while (0)
 #define PTS(k) do { } while (0)
+#define WVTS(k) do { } while (0)
 #endif
 // CODEC_DECIDE_WAVES=0 (host env, passed in codec_params.reserved bit 0) forces the
 // block-sequential decision path (A/B and tests)
@@ -1672,6 +1675,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
         if (wv == 15) {
             const double h = -np_sum_wave(RankTerm{tl}, (int)m);
             if (lane == 0) hy_sh = h;
+            WVTS(15);
         }
         const int nb = min(P.nbits, 16);
         if (t == 0) ctl_sh[0] = 0;
@@ -1719,6 +1723,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
                     if (i0 == 0) DTS(7);
                     hxy = -np_sum_wave(ListTerm{tl, L}, (int)m);
                     if (i0 == 0) DTS(6);
+                    if (i0 == 0) WVTS(wv);
                     if (lane == 0) hx_sh[wv] = -(plogp(lut, (uint32_t)(npx - pp), Nd) + plogp(lut, pp, Nd));
                 }
                 if (lane == 0) hxy_sh[wv] = hxy;

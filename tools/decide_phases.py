@@ -53,6 +53,11 @@ def main():
                   np.median(np.max(np.where(act, pr[:, :, 3], pr[:, :, 1]), axis=1) - t0[:, 0]) * 0.01,
                   np.median(raw[:, 8] - raw[:, 0]) * 0.01, np.median(raw[:, 14] - raw[:, 0]) * 0.01))
     w0 = raw[:, 6:8] if not split else None   # wave 0 (plane 0): after its H(X,Y) sum, after its joint-order list
+    if not split:   # per-wave end of the first round's plane (wave 15: H(Y)), after the round start (DTS 2)
+        wvt = ws[terms: terms + B * R * 8].view(np.int64).reshape(B, R)[:, R - 80:R - 64]
+        ok = wvt > raw[:, 2:3]
+        print("wave path, per wave (us after the MI round start; median over slices): " + " ".join(
+            "w%d=%.2f" % (w, np.median((wvt[:, w] - raw[:, 2])[ok[:, w]]) * 0.01) for w in range(16) if ok[:, w].any()))
     if not split: print("wave0: masks %.2f us, counts+scans %.2f us, list %.2f us, sum %.2f us, then to round end %.2f us" % (
         np.median(raw[:, 8] - raw[:, 2]) * 0.01, np.median(raw[:, 9] - raw[:, 8]) * 0.01,
         np.median(w0[:, 1] - raw[:, 9]) * 0.01, np.median(w0[:, 0] - w0[:, 1]) * 0.01,
