@@ -1161,6 +1161,11 @@ struct ListTerm {
 // per SIMD (8 put three on one SIMD: 33.4 -> 32.0 us per slice, tools/decide_phases.py)
 #define DECIDE_RP 7
 #endif
+#ifndef DECIDE_RP2
+// planes per round when each plane takes two waves: 5 (the usual s on 12-bit CT data) on waves
+// 0-9 + the H(Y) wave = 1.5 plane-units per SIMD; a slice needing more planes runs another round
+#define DECIDE_RP2 5
+#endif
 // split decision: a plane workgroup's "no value" (a NaN bit pattern, never a real H(X,Y))
 #define PLANE_NONE 0x7FF8DEAD00000001ull
 // a split decision's main workgroup that stopped waiting for a plane slot marks it ABANDONED
@@ -1653,6 +1658,13 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
         // the class's 16 layouts (one per s) into LDS now (`vals` is free until the windows):
         // loaded after the decision they were one dependent global round trip (~2 us)
         if (t < 16 * kLayW) reinterpret_cast<int32_t*>(vals)[t] = lay_all[t];
+        // paired planes (one buffer of m <= 8192 ranks): each plane's list build and leaf sums
+        // go to two waves (2k, 2k + 1: different SIMDs), DECIDE_RP2 planes per round -- the round
+        // is VALU-issue bound, and two planes on one SIMD were its critical path.
+        // vals: the layouts (ints [0, 1024)), then the pairs' slot exchange and sync counters
+        const bool pair = !(P.reserved & 4) && m <= NP_CHUNK && ngrp >= 2 && wplanes >= 1;
+        int* pcnt = reinterpret_cast<int*>(vals + 896);
+        if (pair && t < 8) pcnt[t] = 0;                  // ordered by the barrier after the masks
         const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
         for (int g = wv; g < ngrp; g += 16) {             // bit-plane ballots per rank group
             const int r = g * 64 + lane;
@@ -1679,7 +1691,118 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
         }
         const int nb = min(P.nbits, 16);
         if (t == 0) ctl_sh[0] = 0;
-        for (int i0 = 0; i0 < nb; i0 += rp) {
+        if (pair) {
+            const int rp2 = min(wplanes, DECIDE_RP2);
+            const int k = wv >> 1, h = wv & 1;
+            double* xbuf = vals + 512 + 64 * k;                        // wave 2k+1's slot sums (k < 5)
+            const int gh = (ngrp + 1) / 2;                             // groups of the first half
+            int base = 0;
+            for (int i0 = 0; i0 < nb; i0 += rp2) {
+                const int i = i0 + k;
+                if (wv < 2 * rp2 && i < nb) {
+                    const uint32_t pp = pops_sh[i];
+                    const bool run = pp != 0 && (long long)pp != npx;
+                    uint16_t* L = jl + (size_t)k * m;
+                    if (run) {
+                        uint32_t ones = 0, onesA = 0;
+                        for (int g = lane; g < ngrp; g += 64) {
+                            const uint32_t c = (uint32_t)__popcll(pm[g * 16 + i]);
+                            ones += c;
+                            onesA += g < gh ? c : 0u;
+                        }
+#pragma unroll
+                        for (int o = 32; o >= 1; o >>= 1) {
+                            ones += __shfl_xor(ones, o, 64);
+                            onesA += __shfl_xor(onesA, o, 64);
+                        }
+                        // half h: groups [g0, g1); the first half's groups are full (64 ranks)
+                        const int g0 = h ? gh : 0, g1 = h ? ngrp : gh;
+                        uint32_t zbase = h ? (uint32_t)gh * 64u - onesA : 0u;
+                        uint32_t obase = (uint32_t)m - ones + (h ? onesA : 0u);
+                        for (int blk = g0; blk < g1; blk += 64) {
+                            const int gl = blk + lane;
+                            const u64 mkl = gl < g1 ? pm[gl * 16 + i] : 0ull;
+                            const int ng = min(64, g1 - blk);
+                            for (int gg = 0; gg < ng; ++gg) {
+                                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mkl, gg);
+                                const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mkl >> 32), gg);
+                                const u64 mk = (u64)lo | ((u64)hi << 32);
+                                const int g = blk + gg;
+                                const int nr = min(64, (int)m - g * 64);
+                                const u64 valid = nr >= 64 ? ~0ull : ((1ull << nr) - 1ull);
+                                const u64 zm = ~mk & valid;
+                                const bool one = (mk >> lane) & 1ull;
+                                const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)((one ? mk : zm) >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)(one ? mk : zm), 0u));
+                                if (lane < nr) L[(one ? obase : zbase) + below] = (uint16_t)(g * 64 + lane);
+                                obase += (uint32_t)__popcll(mk);
+                                zbase += (uint32_t)__popcll(zm);
+                            }
+                        }
+                    }
+                    // sync 1: both halves of the list are written
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (lane == 0) atomicAdd(&pcnt[k], 1);
+                    if (run) {
+                        while (__hip_atomic_load(&pcnt[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < base + 2)
+                            __builtin_amdgcn_s_sleep(1);
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    }
+                    // the chunk tree's bottom slots: wave 2k lane l takes slot l, wave 2k+1 slot l + 64
+                    double v = 0.0;
+                    if (run) {
+                        int a = 0;
+                        const int n = np_node_size((int)m, 7, lane + 64 * h, &a);
+                        v = n > 0 ? np_leaf(ListTerm{tl, L}, a, n) : 0.0;
+                    }
+                    if (h) {   // sync 2: hand the upper slots to wave 2k
+                        if (run) xbuf[lane] = v;
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        if (lane == 0) atomicAdd(&pcnt[k], 1);
+                    } else {
+                        double hxy = 0.0;
+                        if (run) {
+                            while (__hip_atomic_load(&pcnt[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < base + 3)
+                                __builtin_amdgcn_s_sleep(1);
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                            double res = -0.0;                         // np_sum_wave's buffer sum
+                            res += np_combine_wave(v, xbuf[lane], (int)m);
+                            hxy = -res;
+                            if (i0 == 0) WVTS(wv);
+                            if (lane == 0) hx_sh[k] = -(plogp(lut, (uint32_t)(npx - pp), Nd) + plogp(lut, pp, Nd));
+                        }
+                        if (lane == 0) hxy_sh[k] = hxy;
+                    }
+                    base += 3;
+                }
+                __syncthreads();
+                if (t == 0) {
+                    Hy = hy_sh;
+                    const double target0 = P.beta * Hy;
+                    int stop = 0;
+                    for (int kk = 0; kk < rp2 && i0 + kk < nb; ++kk) {
+                        const int ii = i0 + kk;
+                        if (!(need_decision && !decided) && !P.all_mi) { stop = 1; break; }
+                        const uint32_t pp = pops_sh[ii];
+                        double mi = 0.0;
+                        if (pp != 0 && (long long)pp != npx) {                // codec.py:520-523
+                            mi = (hx_sh[kk] + Hy) - hxy_sh[kk];              // codec.py:554
+                            if (!(mi > 0.0)) mi = 0.0;
+                        }
+                        mis_sh[ii] = mi;
+                        if (need_decision && !decided) {
+                            cum += mi;
+                            if (cum >= target0) { s = ii + 1; decided = true; }
+                        }
+                    }
+                    if (!(need_decision && !decided) && !P.all_mi) stop = 1;
+                    ctl_sh[0] = stop;
+                }
+                __syncthreads();
+                if (ctl_sh[0]) break;
+            }
+        }
+        for (int i0 = 0; i0 < nb && !pair; i0 += rp) {
             const int i = i0 + wv;
             if (wv < rp && i < nb) {
                 const uint32_t pp = pops_sh[i];
@@ -3064,7 +3187,8 @@ static int plan_impl(const codec_params* P, const void* cover, void* stego, cons
                               (!need_blocks0 || host_exact_count(P, true) == 0);
         if (fk != 0 && shape_ok && (fk == 2 || (long long)P->B >= device_cu_count())) {
             codec_params Pv = *P;
-            Pv.reserved = (knob("CODEC_DECIDE_WAVES", 1) ? 0 : 1) | (knob("CODEC_DECIDE_WALK", 1) ? 0 : 2);
+            Pv.reserved = (knob("CODEC_DECIDE_WAVES", 1) ? 0 : 1) | (knob("CODEC_DECIDE_WALK", 1) ? 0 : 2) |
+                          (knob("CODEC_DECIDE_PAIRS", 1) ? 0 : 4);
             ProfScope prof(st, CODEC_K_SCAN_DECIDE);
             const bool nt = knob("CODEC_NT", 1) != 0;
 #define SD(NTV) hipLaunchKernelGGL((k_scan_decide<uint16_t, 16, NTV>), dim3(1, P->B), dim3(1024), 0, st, \
@@ -3108,7 +3232,8 @@ static int plan_impl(const codec_params* P, const void* cover, void* stego, cons
     }
     codec_params Pv = *P;
     // bit 0: force the block-sequential decision; bit 1: no walk path for wide slices
-    Pv.reserved = (knob("CODEC_DECIDE_WAVES", 1) ? 0 : 1) | (knob("CODEC_DECIDE_WALK", 1) ? 0 : 2);
+    Pv.reserved = (knob("CODEC_DECIDE_WAVES", 1) ? 0 : 1) | (knob("CODEC_DECIDE_WALK", 1) ? 0 : 2) |
+                          (knob("CODEC_DECIDE_PAIRS", 1) ? 0 : 4);
     // small batches: the per-plane joint entropies go to plane workgroups on otherwise idle
     // CUs (1 + nb workgroups per slice, all co-resident: at most 240 of them, one per CU)
     const int nbp = P->nbits < 16 ? P->nbits : 16;
