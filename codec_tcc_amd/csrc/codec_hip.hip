@@ -1696,6 +1696,12 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
             const int k = wv >> 1, h = wv & 1;
             double* xbuf = vals + 512 + 64 * k;                        // wave 2k+1's slot sums (k < 5)
             const int gh = (ngrp + 1) / 2;                             // groups of the first half
+            // H(X) of every plane meanwhile, on an idle wave (its two table loads stay off the
+            // pairs' critical path); read by thread 0's walk after the round's barrier
+            if (wv == 14 && lane < nb) {
+                const uint32_t pp = pops_sh[lane];
+                hx_sh[lane] = (pp != 0 && (long long)pp != npx) ? -(plogp(lut, (uint32_t)(npx - pp), Nd) + plogp(lut, pp, Nd)) : 0.0;
+            }
             int base = 0;
             for (int i0 = 0; i0 < nb; i0 += rp2) {
                 const int i = i0 + k;
@@ -1769,7 +1775,6 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
                             res += np_combine_wave(v, xbuf[lane], (int)m);
                             hxy = -res;
                             if (i0 == 0) WVTS(wv);
-                            if (lane == 0) hx_sh[k] = -(plogp(lut, (uint32_t)(npx - pp), Nd) + plogp(lut, pp, Nd));
                         }
                         if (lane == 0) hxy_sh[k] = hxy;
                     }
@@ -1786,7 +1791,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
                         const uint32_t pp = pops_sh[ii];
                         double mi = 0.0;
                         if (pp != 0 && (long long)pp != npx) {                // codec.py:520-523
-                            mi = (hx_sh[kk] + Hy) - hxy_sh[kk];              // codec.py:554
+                            mi = (hx_sh[ii] + Hy) - hxy_sh[kk];              // codec.py:554
                             if (!(mi > 0.0)) mi = 0.0;
                         }
                         mis_sh[ii] = mi;
