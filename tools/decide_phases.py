@@ -58,7 +58,8 @@ def main():
         ok = wvt > raw[:, 2:3]
         print("wave path, per wave (us after the MI round start; median over slices): " + " ".join(
             "w%d=%.2f" % (w, np.median((wvt[:, w] - raw[:, 2])[ok[:, w]]) * 0.01) for w in range(16) if ok[:, w].any()))
-    if not split: print("wave0: masks %.2f us, counts+scans %.2f us, list %.2f us, sum %.2f us, then to round end %.2f us" % (
+    # the paired MI round (default) does not stamp wave 0's list/sum slots: skip the breakdown then
+    if not split and (w0 > raw[:, 2:3]).all() and (raw[:, 9] >= raw[:, 8]).all(): print("wave0: masks %.2f us, counts+scans %.2f us, list %.2f us, sum %.2f us, then to round end %.2f us" % (
         np.median(raw[:, 8] - raw[:, 2]) * 0.01, np.median(raw[:, 9] - raw[:, 8]) * 0.01,
         np.median(w0[:, 1] - raw[:, 9]) * 0.01, np.median(w0[:, 0] - w0[:, 1]) * 0.01,
         np.median(raw[:, 3] - w0[:, 0]) * 0.01))
