@@ -404,6 +404,9 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
            "roundtrip_ok": cover_ok and pay_ok and flags_ok and all(r.status == 0 for r in recs),
            "cover_ok": cover_ok, "payload_ok": pay_ok, "lookback_ok": flags_ok,
            "end_candidates_mean": float(np.mean([r.end + 1 for r in recs])),
+           # the scheme's capacity bound: only the (odd, odd) lattice -- a quarter of the
+           # pixels -- can carry bits (the rest is the untouched MED context)
+           "candidates_per_slice": (H // 2) * (W // 2),
            # slices whose payload exceeds the T-capacity (truncated, still exactly reversible;
            # roundtrip_ok then reads False): uniform-noise slices at T=2
            "overflow_slices": int(sum(1 for r in recs if r.status == 1)),

@@ -82,7 +82,9 @@ class PeeCodec:
                 torch.tensor(lengths, dtype=torch.int32, device=self.device))
 
     def capacity(self, covers, tmax: Optional[int] = None):
-        """int32 [B, tmax] device tensor: exact capacity of each slice at T = 1..tmax."""
+        """int32 [B, tmax] device tensor: exact capacity of each slice at T = 1..tmax.
+        Bounded by the candidate lattice: at most (H // 2) * (W // 2) bits per slice -- a
+        quarter of the pixels; the other three quarters are the MED context, never modified."""
         torch = _torch()
         tmax = self.tmax if tmax is None else int(tmax)
         caps = torch.empty((self.B, tmax), dtype=torch.int32, device=self.device)
