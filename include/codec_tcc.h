@@ -5,8 +5,10 @@
  * Boundary contract (mirrors the reference's Python function boundary):
  *   - every pointer argument is a DEVICE pointer owned by the caller (torch tensors);
  *     `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream);
- *   - every call is asynchronous on `stream`, stateless and thread-safe given distinct
- *     streams and buffers; nothing is allocated inside (workspace is caller-provided);
+ *   - every call is asynchronous on `stream` and thread-safe given distinct streams and
+ *     buffers; nothing is allocated inside (workspace is caller-provided).  A workspace is
+ *     one of those buffers: calls that share one are ordered on one stream, since some
+ *     carry state from call to call in it (codec_pee_workspace_bytes);
  *   - return value: 0 on success, < 0 on error (argument error or negated hipError_t);
  *     codec_last_error() returns a thread-local message.  The Python host layer turns a
  *     non-zero status into an exception, as the reference raises ValueError (codec.py:34-37).
