@@ -10,44 +10,56 @@
 //
 // Launch: grid (regions per slice, B), 256 threads; a workgroup streams one contiguous
 // region of one slice, 4 x 16-B vectors of each image per thread per iteration, keeps
-// the moments in registers (v_mad_u64_u32 accumulations), reduces them across the wave
+// the moments in registers (32-bit sums, float64 FMAs for the products: QmAcc), reduces them across the wave
 // with shuffles and adds them to the slice's record with 64-bit atomics (one set per
 // wave), so HBM traffic is the two reads and nothing else.
 #include "codec_common.h"
 
 #define QM_WORDS 10
 
+// per-thread accumulators, exact by bounds (the host caps a thread at QM_MAX_PX pixels):
+// the linear sums in 32 bits (<= 2^16 px x 65535), the products in float64 FMAs (each product
+// <= 2^32 is exact, every partial sum <= 2^16 x 2^32 < 2^53 is an exact integer) -- fewer,
+// full-rate instructions instead of v_mad_u64_u32 and 64-bit adds (256 x 2048^2: 0.723 ->
+// 0.719 ms; the pass is memory-bound either way, profiles/r04/quality_acc_ab.txt)
+#define QM_MAX_PX 65536
+struct QmAcc {
+    uint32_t s[4];   // sum a, sum b, sum |a - b|, #(a != b)
+    double q[3];     // sum a^2, sum b^2, sum ab
+    uint32_t mx[3];  // max |a - b|, max a, max b
+};
+
 template <typename T>
-__device__ __forceinline__ void qm_px(uint32_t a, uint32_t b, u64* m, uint32_t* mx) {
-    m[0] += a;
-    m[1] += b;
-    m[2] += (u64)a * a;
-    m[3] += (u64)b * b;
-    m[4] += (u64)a * b;
+__device__ __forceinline__ void qm_px(uint32_t a, uint32_t b, QmAcc& m) {
+    m.s[0] += a;
+    m.s[1] += b;
+    const double fa = (double)a, fb = (double)b;
+    m.q[0] = fma(fa, fa, m.q[0]);
+    m.q[1] = fma(fb, fb, m.q[1]);
+    m.q[2] = fma(fa, fb, m.q[2]);
     const uint32_t d = a > b ? a - b : b - a;
-    m[5] += d;
-    mx[0] = max(mx[0], d);
-    m[7] += (a != b) ? 1u : 0u;
-    mx[1] = max(mx[1], a);
-    mx[2] = max(mx[2], b);
+    m.s[2] += d;
+    m.mx[0] = max(m.mx[0], d);
+    m.s[3] += min(d, 1u);
+    m.mx[1] = max(m.mx[1], a);
+    m.mx[2] = max(m.mx[2], b);
 }
 
 template <typename T>
-__device__ __forceinline__ void qm_vec(const typename Vec8<T>::type& va, const typename Vec8<T>::type& vb, u64* m,
-                                       uint32_t* mx) {
+__device__ __forceinline__ void qm_vec(const typename Vec8<T>::type& va, const typename Vec8<T>::type& vb, QmAcc& m) {
     if constexpr (sizeof(T) == 2) {
         const uint32_t wa[4] = {va.x, va.y, va.z, va.w}, wb[4] = {vb.x, vb.y, vb.z, vb.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            qm_px<T>(wa[k] & 0xFFFFu, wb[k] & 0xFFFFu, m, mx);
-            qm_px<T>(wa[k] >> 16, wb[k] >> 16, m, mx);
+            qm_px<T>(wa[k] & 0xFFFFu, wb[k] & 0xFFFFu, m);
+            qm_px<T>(wa[k] >> 16, wb[k] >> 16, m);
         }
     } else {
         const uint32_t wa[2] = {va.x, va.y}, wb[2] = {vb.x, vb.y};
 #pragma unroll
         for (int k = 0; k < 2; ++k)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) qm_px<T>((wa[k] >> (8 * e)) & 0xFFu, (wb[k] >> (8 * e)) & 0xFFu, m, mx);
+            for (int e = 0; e < 4; ++e) qm_px<T>((wa[k] >> (8 * e)) & 0xFFu, (wb[k] >> (8 * e)) & 0xFFu, m);
     }
 }
 
@@ -60,8 +72,7 @@ __global__ __launch_bounds__(256) void k_quality(const T* __restrict__ a_all, co
     const T* Bm = b_all + (size_t)b * npx;
     const long long p0 = (long long)blockIdx.x * per_wg;
     const long long p1 = min(npx, p0 + per_wg);
-    u64 m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t mx[3] = {0, 0, 0};
+    QmAcc acc = {{0u, 0u, 0u, 0u}, {0.0, 0.0, 0.0}, {0u, 0u, 0u}};
     if (p0 < p1) {
         if constexpr (VEC) {
             // host guarantees: npx % 8 == 0, per_wg % 8 == 0, 16-B (8-B) aligned slices
@@ -74,13 +85,16 @@ __global__ __launch_bounds__(256) void k_quality(const T* __restrict__ a_all, co
 #pragma unroll
                 for (int u = 0; u < 4; ++u) { xa[u] = ldv<true>(va + i + u * 256); xb[u] = ldv<true>(vb + i + u * 256); }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) qm_vec<T>(xa[u], xb[u], m, mx);
+                for (int u = 0; u < 4; ++u) qm_vec<T>(xa[u], xb[u], acc);
             }
-            for (; i < nv; i += 256) qm_vec<T>(ldv<true>(va + i), ldv<true>(vb + i), m, mx);
+            for (; i < nv; i += 256) qm_vec<T>(ldv<true>(va + i), ldv<true>(vb + i), acc);
         } else {
-            for (long long q = p0 + threadIdx.x; q < p1; q += 256) qm_px<T>(A[q], Bm[q], m, mx);
+            for (long long q = p0 + threadIdx.x; q < p1; q += 256) qm_px<T>(A[q], Bm[q], acc);
         }
     }
+    // widen: the wave reduction sums 64 threads' values
+    u64 m[8] = {acc.s[0], acc.s[1], (u64)acc.q[0], (u64)acc.q[1], (u64)acc.q[2], acc.s[2], 0ull, acc.s[3]};
+    uint32_t mx[3] = {acc.mx[0], acc.mx[1], acc.mx[2]};
     // wave reduction, then one atomic set per wave
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -121,6 +135,7 @@ int codec_quality_moments(int32_t B, int32_t H, int32_t W, int32_t bytes, const 
     long long per = knob("CODEC_QUALITY_PX_PER_WG", 131072);
     per = (per + 7) / 8 * 8;
     if (per < 2048) per = 2048;
+    if (per > 256LL * QM_MAX_PX) per = 256LL * QM_MAX_PX;   // the accumulators' exactness bound
     const long long wps = (npx + per - 1) / per;
     dim3 grid((unsigned)wps, B);
     ProfScope prof(st, CODEC_K_QUALITY);

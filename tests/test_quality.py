@@ -77,10 +77,13 @@ def test_moment_math_random_pairs():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dt,h,w,bsz", [("uint16", 512, 512, 3), ("uint16", 37, 53, 2), ("uint8", 64, 96, 4),
-                                        ("uint8", 33, 31, 1), ("uint16", 2048, 2048, 2)])
+                                        ("uint8", 33, 31, 1), ("uint16", 2048, 2048, 2),
+                                        ("u16full", 512, 512, 2), ("u16full", 2048, 2048, 1)])
 def test_gpu_moments_exact(dt, h, w, bsz):
+    """Exact integer moments; "u16full" = uniform 16-bit noise (products up to 65535^2, the
+    kernel's per-thread float64 sums at their largest)."""
     torch = pytest.importorskip("torch")
-    gen = synth.ct12 if dt == "uint16" else synth.GENERATORS["u8"]
+    gen = {"uint16": synth.ct12, "u16full": synth.GENERATORS["u16"]}.get(dt, synth.GENERATORS["u8"])
     rng = np.random.default_rng(h * w)
     a = np.stack([gen(h, w, 10 + i) for i in range(bsz)])
     b = a.copy()
