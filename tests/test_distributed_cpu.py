@@ -217,3 +217,23 @@ def test_exchanges_gloo_world2(n_slices):
     for p in procs:
         p.join(timeout=60)
     assert all(ok for _r, ok in res), res
+
+
+@pytest.mark.parametrize("world,n_slices", [(4, 11), (8, 19)])
+def test_exchanges_gloo_more_ranks(world, n_slices):
+    """The same exchanges rehearsed at 4 and 8 ranks (the driver's scaling run uses up to 8
+    GPUs), uneven shards (11 = 3 + 3 + 3 + 2; 19 over 8 ranks: three of 3, five of 2)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_slices, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=180) for _ in procs]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(ok for _r, ok in res), res
