@@ -290,8 +290,9 @@ def _profile(lib, _lib, fn, steps):
     return {k: float(np.mean(v)) for k, v in out.items()}
 
 
-def _timed(torch, dist, world, dev, fn, steps):
-    """Barrier + synchronize on both sides of exactly `steps` calls; max over ranks (s)."""
+def _timed(torch, dist, world, dev, fn, steps, local=None):
+    """Barrier + synchronize on both sides of exactly `steps` calls; max over ranks (s).
+    `local` (a dict) receives this rank's own figure under "s" (the per-rank record)."""
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -299,6 +300,8 @@ def _timed(torch, dist, world, dev, fn, steps):
     for _ in range(steps):
         fn()
     torch.cuda.synchronize()
+    if local is not None:   # this rank's own work, before the closing barrier waits for the others
+        local["s"] = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -391,7 +394,8 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
         step = g.replay
         for _ in range(args.warmup):
             step()
-    el = _timed(torch, dist, world, dev, step, steps)
+    mine = {}
+    el = _timed(torch, dist, world, dev, step, steps, local=mine)
     # correctness of the state the timed steps left (outside the timed region): restored
     # cover, recovered payload bits, per-slice status and the decode-side look-back flag
     recs = PeeEncoded(stego, lm, meta, packed[1], pw).records()
@@ -401,6 +405,7 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
     flags_ok = all(r.status in (0, 1) for r in recs) and not codec.lookback_failed(pw)
     res = {"value": round(B * H * W * world * steps / el / 1e6, 1), "unit": "Mpixels/s",
            "ms_per_step": round(el / steps * 1e3, 4), "T": T,
+           "_rank_ms_per_step": round(mine["s"] / steps * 1e3, 4),
            "roundtrip_ok": cover_ok and pay_ok and flags_ok and all(r.status == 0 for r in recs),
            "cover_ok": cover_ok, "payload_ok": pay_ok, "lookback_ok": flags_ok,
            "end_candidates_mean": float(np.mean([r.end + 1 for r in recs])),
@@ -427,7 +432,9 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
             bool(torch.equal(own, D.pack_pee_records(meta, lm, xch.width))) and \
             bool(torch.equal(om, meta)) and bool(torch.equal(ol, D.map_prefix(meta, lm, ol.shape[1])))
         t_g = _timed(torch, dist, world, dev, lambda: (xch.start(meta, lm), xch.join_records()), steps) / steps
-        t_k = _timed(torch, dist, world, dev, kernels, steps) / steps
+        mine_k = {}
+        t_k = _timed(torch, dist, world, dev, kernels, steps, local=mine_k) / steps
+        res["_rank_kernels_only_ms"] = round(mine_k["s"] / steps * 1e3, 4)
         res["distributed"] = {
             "allgather_ms": round(t_g * 1e3, 4),
             "allgather_bytes": xch.gathered_bytes,
@@ -657,6 +664,44 @@ def bench_quality(args, torch, covers, stego, B, H, W):
     return res
 
 
+def _strip_private(d):
+    """Drop the `_`-prefixed per-rank fields from a leg's result (recursively)."""
+    if isinstance(d, dict):
+        return {k: _strip_private(v) for k, v in d.items() if not k.startswith("_")}
+    return d
+
+
+def rank_record(torch, dist, rank, local, dev, backend, head, c4):
+    """What this rank ran on: enough for a reader of the N > 1 JSON line
+    to check that N ranks ran on N distinct devices over the named backend."""
+    p = torch.cuda.get_device_properties(dev)
+    import socket
+    rec = {"rank": rank, "local_rank": local, "device": dev.index, "pid": os.getpid(),
+           "host": socket.gethostname(),
+           "pci": f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:"
+                  f"{getattr(p, 'pci_device_id', 0):02x}",
+           "gpu": p.name, "arch": getattr(p, "gcnArchName", ""),
+           "backend": dist.get_backend(), "world_size": dist.get_world_size(),
+           "ms_per_step": head.get("_rank_ms_per_step"),
+           "kernels_only_ms": head.get("_rank_kernels_only_ms")}
+    if c4 is not None:
+        rec["c4_ms_per_step"] = c4.get("_rank_ms_per_step")
+    return rec
+
+
+def gather_rank_records(torch, dist, world, rec, backend):
+    """Every rank's record, in rank order (one all_gather_object after the timed loops).
+    Over RCCL the devices must be distinct (host, PCI address): RCCL itself refuses two ranks
+    on one GPU, and a duplicate here would mean the launcher mapped ranks wrongly."""
+    recs = [None] * world
+    dist.all_gather_object(recs, rec)
+    if backend == "nccl":
+        seen = {(r["host"], r["pci"]) for r in recs}
+        if len(seen) != world:
+            raise RuntimeError(f"bench.py: {world} RCCL ranks on {len(seen)} distinct devices: {recs}")
+    return recs
+
+
 def _free_port() -> int:
     import socket
     s = socket.socket()
@@ -845,6 +890,10 @@ def main():
         quality = bench_quality(args, torch, covers, stego, B, H, W) if rank == 0 else None
         del stego
     c4 = bench_c4(args, torch, dist, world, rank, dev) if (world > 1 and args.c3) else None
+    ranks = None
+    if world > 1:
+        ranks = gather_rank_records(torch, dist, world,
+                                    rank_record(torch, dist, rank, local, dev, args.backend, head, c4), args.backend)
     c3 = bench_c3(args, torch, dist, world, dev, rank) if (rank == 0 and args.c3) else None
     c2 = bench_c2(args, torch, dev, rank) if (rank == 0 and args.c2 and world == 1) else None
 
@@ -887,6 +936,10 @@ def main():
                 out["cpu_baseline"]["pool"] = pools["pee"]
             if "lsb" in pools and "reference_path" in out["cpu_baseline"]:
                 out["cpu_baseline"]["reference_path"]["pool"] = pools["lsb"]
+        out = _strip_private(out)
+        if ranks is not None:
+            out["ranks"] = ranks
+            out["distinct_devices"] = len({(r["host"], r["pci"]) for r in ranks})
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()   # rank 0 ran its C3 leg alone: every rank leaves the group together

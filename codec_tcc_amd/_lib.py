@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# CODEC_TCC_LIB: an alternative build of the same library (A/B benchmarking, tools/ab_bench.sh)
+# CODEC_TCC_LIB: an alternative build of the same library (A/B benchmarking, tools/archive/ab_bench.sh)
 _DEFAULT_PATH = os.path.join(_HERE, "libcodec_hip.so")
 LIB_PATH = os.environ.get("CODEC_TCC_LIB") or _DEFAULT_PATH
 
@@ -91,6 +91,7 @@ _SIGS = {
     "codec_pee_workspace_bytes": (C.c_size_t, [C.POINTER(PeeParams)]),
     "codec_pee_extract_flag_offset": (C.c_size_t, [C.POINTER(PeeParams)]),
     "codec_pee_diag_offset": (C.c_size_t, [C.POINTER(PeeParams)]),
+    "codec_pee_reset": (C.c_int, [C.POINTER(PeeParams), _VP, C.c_size_t, _VP]),
     "codec_debug_res_trace": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     "codec_pee_embed": (C.c_int, [C.POINTER(PeeParams), _VP, _VP, _VP, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),
     "codec_pee_extract": (C.c_int, [C.POINTER(PeeParams), _VP, _VP, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),
@@ -159,9 +160,15 @@ def _check_digest(path: str):
     the digest of csrc/*, include/codec_tcc.h and the build flags.  No rebuild here: on the
     GPU box the prebuilt library is the product, and a mismatch there is an error."""
     from . import build
-    have, want = build.library_digest(path), build.source_digest()
+    # the flags the library was built with travel inside it (ADVICE r4): a build for another
+    # CODEC_OFFLOAD_ARCH / CODEC_BUILD_DEFS loads without that environment, and a mismatch
+    # names the sources as the cause only when they are
+    flags = build.library_flags(path)
+    have, want = build.library_digest(path), build.source_digest(flags)
     if have != want:
-        raise RuntimeError(f"{path} was not built from these sources (library digest {have}, sources {want}): "
+        extra = "" if flags is None or flags == build.FLAGS else \
+            f" (built with flags {' '.join(flags)}; this environment's are {' '.join(build.FLAGS)})"
+        raise RuntimeError(f"{path} was not built from these sources (library digest {have}, sources {want}){extra}: "
                            "rebuild it with `python -c 'import __graft_entry__ as g; g.build()'`")
 
 

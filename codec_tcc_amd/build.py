@@ -35,6 +35,7 @@ EXTRA = os.environ.get("CODEC_BUILD_DEFS", "").split()
 FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", f"--offload-arch={ARCH}",
          "-Wall", "-Wno-unused-function"] + EXTRA
 DIGEST_TAG = b"codec-src-sha256:"
+FLAGS_TAG = b"codec-build-flags:"   # the flags the digest covers, embedded beside it
 
 
 def hipcc() -> str:
@@ -63,9 +64,14 @@ def _digest(paths, flags) -> str:
     return h.hexdigest()
 
 
-def source_digest() -> str:
-    """Digest of everything the library is compiled from (sources, headers, flags)."""
-    return _digest(SRCS + _common_deps(), FLAGS)
+def source_digest(flags=None) -> str:
+    """Digest of everything the library is compiled from (sources, headers, flags); `flags`
+    defaults to this process's build flags (CODEC_OFFLOAD_ARCH / CODEC_BUILD_DEFS)."""
+    missing = [p for p in SRCS + _common_deps() if not os.path.exists(p)]
+    if missing:
+        raise RuntimeError(f"cannot check libcodec_hip.so against its sources: {', '.join(missing)} absent "
+                           "(an installed package without csrc/? rebuild in a source tree)")
+    return _digest(SRCS + _common_deps(), FLAGS if flags is None else flags)
 
 
 def library_digest(path: str = OUT):
@@ -81,6 +87,24 @@ def library_digest(path: str = OUT):
         return None
     hexd = data[i + len(DIGEST_TAG): i + len(DIGEST_TAG) + 64]
     return hexd.decode("ascii", "replace")
+
+
+def _c_escape(text: str) -> str:
+    return text.replace("\\", "\\\\").replace('"', '\\"')
+
+
+def library_flags(path: str = OUT):
+    """The build flags embedded in a built library (list), or None when it has none."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    i = data.find(FLAGS_TAG)
+    if i < 0:
+        return None
+    j = data.find(b"\0", i)
+    return data[i + len(FLAGS_TAG): j].decode("utf-8", "replace").split("\x1f")
 
 
 def _obj_stale(src: str, force: bool) -> bool:
@@ -125,6 +149,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     with open(dsrc, "w") as f:
         f.write("// generated by codec_tcc_amd/build.py: digest of the library's sources and flags\n"
                 f'static const char k_digest[] = "{DIGEST_TAG.decode()}{source_digest()}";\n'
+                f'extern "C" const char k_codec_build_flags[] = "{FLAGS_TAG.decode()}'
+                + "\\037".join(_c_escape(f) for f in FLAGS) + '";\n'
                 'extern "C" const char* codec_build_digest(void) '
                 f"{{ return k_digest + {len(DIGEST_TAG)}; }}\n")
     dobj = os.path.join(HERE, "build_obj", "codec_digest.o")

@@ -14,6 +14,10 @@
 //            -> k_pee_recover (prefix tiles: bits + restored pixels)
 #include "codec_common.h"
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 #define PEE_TILE 1024
 
 struct PeeCand {
@@ -1047,11 +1051,20 @@ struct ExtractCount {
 #define PEE_LB_PARTIAL 1   // embed: a partial sum of the published words may end the wait (past `end`)
 #endif
 // Status words carry two counts (round 4): bits 0-31 the chunk's (or prefix's) expandable /
-// inner count, bits 32-61 its unsafe-candidate count (the embed's location-map bits, so the
+// inner count, bits 32-55 its unsafe-candidate count (the embed's location-map bits, so the
 // chunk holding `end` learns lm_count from the look-back itself: no meta atomics, no memset).
 // The two fields are summed separately (64-bit each), so a sum can never carry between them.
+// Bits 56-61 (self-cleaning calls only, round 5): the call's epoch tag, the low 6 bits of the
+// chunk's arrival count.  A waiter accepts a word only with its own tag, so a word left by
+// another call -- a chunk whose arrival count drifted from its slice's (a desynchronised
+// workspace) reads the other parity's buffer -- is "not published" and the bounded spin ends
+// in the pixel-count fallback: exact, never a stale prefix.  The high field then needs
+// < 2^24 candidates per slice (PEE_SC_MAX_NC; larger slices take the zeroing path).
 #define LB_LO(w) ((w) & 0xFFFFFFFFull)
-#define LB_HI(w) (((w) >> 32) & 0x3FFFFFFFull)
+#define LB_HI(w) (((w) >> 32) & 0xFFFFFFull)
+#define LB_TAG_SHIFT 56
+#define LB_TAGW(t) ((u64)(uint32_t)(t) << LB_TAG_SHIFT)
+#define PEE_SC_MAX_NC ((1LL << 24) - 2)
 struct LbSum {
     u64 e, u;   // summed low / high fields of the predecessors
 };
@@ -1061,20 +1074,23 @@ __device__ __forceinline__ u64 wave_sum_u64(u64 v) {
     return v;
 }
 // TWO: also sum the high field (the self-cleaning embed's unsafe counts); otherwise only the
-// low one, as the zeroing paths need (fewer registers in the headline kernels)
+// low one, as the zeroing paths need (fewer registers in the headline kernels).
+// tag >= 0 (self-cleaning calls): only words carrying this epoch tag count as published, and
+// the finished flag `done` counts as set only when it holds done_val (tag + 1 there).
 template <bool TWO = false, typename F>
 __device__ LbSum lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, uint32_t spin_max, const F& count,
-                              uint32_t* done = nullptr, uint32_t sat = 0) {
+                              uint32_t* done = nullptr, uint32_t sat = 0, int tag = -1, uint32_t done_val = 1u) {
     const int lane = threadIdx.x & 63;
     LbSum ex{0ull, 0ull};
     int p = c - 1;            // the highest predecessor not summed yet
     uint32_t spins = 0;
+    const u64 tagw = tag >= 0 ? LB_TAGW(tag) : 0ull;
     for (;;) {
         u64 wv[LB_WIN];
 #pragma unroll
         for (int r = 0; r < LB_WIN; ++r) {
             const int idx = p - 64 * r - lane;
-            wv[r] = idx >= 0 ? lb_load(st + idx) : LB_INC;
+            wv[r] = idx >= 0 ? lb_load(st + idx) : (LB_INC | tagw);
         }
         bool reload = false;
 #pragma unroll
@@ -1083,12 +1099,13 @@ __device__ LbSum lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, uin
             const int idx = pr - lane;
             u64 w = wv[r];
             uint32_t fl = (uint32_t)(w >> 62);
+            if (tag >= 0 && (uint32_t)((w >> LB_TAG_SHIFT) & 63u) != (uint32_t)tag) fl = 0u;   // another call's word
             const u64 inc = __ballot(fl == 2u);
             const u64 notready = __ballot(fl == 0u);
             const int first = inc ? (int)__builtin_ctzll(inc) : 64;        // nearest inclusive
             const u64 need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);  // lanes 0..first
             if (notready & need) {
-                if (done && ld_agent(done)) return LbSum{(u64)sat, 0ull};
+                if (done && ld_agent(done) == done_val) return LbSum{(u64)sat, 0ull};
                 if (done && (PEE_LB_PARTIAL)) {
                     // the published words already bound the prefix from below (aggregates of
                     // disjoint chunks, or an inclusive prefix): reaching `sat` (= L) places this
@@ -1114,7 +1131,7 @@ __device__ LbSum lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, uin
                         m &= m - 1ull;
                         const u64 a = count(pr - l);   // packed like a status word's value
                         if (lane == l) {
-                            const u64 mine = LB_AGG | a;
+                            const u64 mine = LB_AGG | a | tagw;
                             atomicCAS(reinterpret_cast<unsigned long long*>(st + idx), (unsigned long long)w,
                                       (unsigned long long)mine);
                             w = mine;
@@ -1236,24 +1253,27 @@ __device__ unsigned long long g_lb_trace[LB_TRACE_SLOTS * 12];
 #define PEE_MODE_NOTICKET 2
 // self-cleaning out-of-place look-back (round 4): no zeroing launch before the pass.  The
 // workspace holds TWO status-word buffers; a call uses buffer `par` and clears its own words
-// of the other one for the next call.  `par` is the parity of the call count, which every
-// workgroup learns from the returning atomic that counts its arrival: one counter word per
-// chunk (after the per-slice lines), call index = its old value.  (8 shard counters per slice
-// put 32 same-address atomics of a 2048^2 slice in series, ~1 us on the embed's critical path.)
-// The finished flag is doubled the same way; meta is written without atomics (status by the
-// chunk holding `end`, lm_count from the look-back's second field).  Calls that still zero
-// (in place, ticket modes) use buffer 1 and finished flag 1 and reset the counters, so the
-// next self-cleaning call (index 0: buffer 0) starts clean.
+// of the other one for the next call.  The finished flag is doubled the same way; meta is
+// written without atomics (status by the chunk holding `end`, lm_count from the look-back's
+// second field).
+// Round 5: the call's epoch comes from the host (the library counts self-cleaning calls per
+// workspace, pee_ws_epoch) as a kernel argument, so every chunk of a call agrees on it by
+// construction -- round 4 derived it from a per-chunk arrival counter, which a call abandoned
+// mid-kernel could leave out of step with the slice's other chunks.  par = epoch & 1; every
+// status word and finished flag also carries the epoch tag epoch % 63 + 1 (1..63), and a
+// waiter accepts only its own tag: a word or flag left by any other call -- an abandoned one,
+// a zeroing call (tag 0), a call whose clear never ran -- reads as "not published", so the
+// worst a stale state can cost is the bounded wait and the pixel-count fallback, never a
+// wrong prefix.  Calls that still zero (in place, ticket modes) use buffer 1 and flag 1 with
+// tag 0.  A call captured into a graph would replay one epoch forever, so capture takes the
+// zeroing path (codec_pee_embed_ts / codec_pee_extract).
 #define PEE_MODE_SC 8
-// ctl: 32 words, 32 per slice (ticket, finished flags), then one arrival counter per chunk
-#define PEE_CTL_WORDS(B, NCH) (32 + 32 * (size_t)(B) + (size_t)(B) * (size_t)(NCH))
+// ctl: 32 words, then 32 per slice (ticket, finished flags)
+#define PEE_CTL_WORDS(B, NCH) (32 + 32 * (size_t)(B))
 #define PEE_LINE_TICKET 0
 #define PEE_LINE_FIN0 1
 #define PEE_LINE_FIN1 4
-__device__ __forceinline__ uint32_t pee_arrive(uint32_t* ctl, int B, int b, int nchunks, int c) {   // old count
-    return atomicAdd(ctl + 32 + 32 * (size_t)B + (size_t)b * nchunks + c, 1u);
-}
-__device__ __forceinline__ int pee_parity_of(uint32_t old) { return (int)(old & 1u); }
+__device__ __forceinline__ int pee_sc_tag(int epoch) { return epoch % 63 + 1; }
 #define PEE_SKIP 0xFFFFFFFFu
 #define PEE_STOP 0xFFFFFFFEu
 template <typename T, bool NT, bool INPLACE, bool SC = false>
@@ -1262,12 +1282,12 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                                                     const u64* __restrict__ payload_all, int pw, int nchunks, int B,
                                                     u64* status_all, uint32_t* ctl, codec_pee_meta* meta_all,
                                                     u64* __restrict__ lm_all, int lmw, int mode, uint32_t spin_max,
-                                                    int dbg_skip, uint32_t* diag, const int32_t* __restrict__ tps) {
+                                                    int dbg_skip, uint32_t* diag, const int32_t* __restrict__ tps,
+                                                    int sc_epoch, int dbg_stale) {
     typedef typename Vec8<T>::type V;
     __shared__ u64 sh64[8];
     __shared__ uint32_t sh[8];
     __shared__ uint32_t s_v, s_excl, s_uexcl, s_uns[4];
-    __shared__ int s_par;
     constexpr bool sc = !INPLACE && SC;   // self-cleaning: a separate instantiation (PEE_MODE_SC)
     __shared__ uint32_t lm32[4 * PEE_TILE / 32];
     __shared__ u64 s_pay[192];   // the slice's payload words when pw <= 192 (see below)
@@ -1297,29 +1317,29 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
         T* dst = stego + b * npx;
         V a0[4], a1[4];
         size_t o0[4];
-        // out of place the finished flags are read BEFORE the chunk's pixels are requested, so
-        // waiting for them does not wait for the pixels too (vmcnt counts in issue order)
-        const uint32_t dnA = !INPLACE ? ld_agent(line + (sc ? PEE_LINE_FIN0 : PEE_LINE_FIN1)) : 0u;   // every lane
-        uint32_t dnB = 0u;
-        if constexpr (sc) dnB = ld_agent(line + PEE_LINE_FIN1);
+        // this call's status-word buffer, epoch tag and finished-flag value (self-cleaning:
+        // from the host's epoch; zeroing calls: buffer 1, untagged, flag value 1)
+        const int par = sc ? (sc_epoch & 1) : 1;
+        const int tag = sc ? pee_sc_tag(sc_epoch) : -1;
+        const u64 tagw = sc ? LB_TAGW(tag) : 0ull;
+        const uint32_t fin_val = sc ? (uint32_t)tag + 1u : 1u;
+        uint32_t* fin_flag = line + (par ? PEE_LINE_FIN1 : PEE_LINE_FIN0);
+        // out of place the finished flag is read BEFORE the chunk's pixels are requested, so
+        // waiting for it does not wait for the pixels too (vmcnt counts in issue order)
+        const uint32_t dnA = !INPLACE ? ld_agent(fin_flag) : 0u;   // every lane
         // out of place: the slot's own chunk j is loaded while the ticket is in flight (the
         // ticket equals j unless workgroups were dispatched out of order)
         if (!INPLACE) pee_load_chunk<T, NT>(src, W, CR, items, j, a0, a1, o0);
         if (tid == 0) {
             uint32_t cc = PEE_SKIP;
-            int par = 1;
             if (!INPLACE) {
                 // a flag seen set was set before this chunk started, so `end` lies in an
                 // earlier chunk; a flag set meanwhile but not seen only costs this chunk the
-                // full path
-                uint32_t dn = dnA;
-                if constexpr (sc) {
-                    par = pee_parity_of(pee_arrive(ctl, B, b, nchunks, j));
-                    dn = par ? dnB : dnA;
-                }
+                // full path.  It counts only when it holds this call's value (tag + 1).
+                const bool dn = dnA == fin_val;
                 cc = (mode & PEE_MODE_NOTICKET) ? (uint32_t)j : atomicAdd(tick, 1u);
                 if (dn) {   // `end` already placed: this chunk is a plain copy
-                    lb_store(status_all + par * stride + (size_t)b * nchunks + cc, LB_INC | (u64)L);
+                    lb_store(status_all + par * stride + (size_t)b * nchunks + cc, LB_INC | (u64)L | tagw);
                     cc |= 0x80000000u;
                 }
             } else {
@@ -1334,15 +1354,12 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
                 }
             }
             s_v = cc;
-            s_par = par;
         }
         if (tid < 4 * PEE_TILE / 32) lm32[tid] = 0;
         lds_barrier();
         LB_STAMP(1);
         const uint32_t cv = s_v;
-        const int par = s_par;
         u64* st = status_all + par * stride + (size_t)b * nchunks;
-        uint32_t* fin_flag = line + (par ? PEE_LINE_FIN1 : PEE_LINE_FIN0);
         if (INPLACE) {
             if (cv == PEE_STOP) return;
             if (cv >= (uint32_t)nchunks) { lds_barrier(); continue; }
@@ -1350,9 +1367,13 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
         const bool copy_only = !INPLACE && (cv & 0x80000000u);
         const int c = (int)(cv & 0x7FFFFFFFu);
         if (sc && tid == 0) {   // clear this chunk's word (and chunk 0: the flag) of the next call's buffer
-            lb_store(status_all + (1 - par) * stride + (size_t)b * nchunks + c, 0ull);
-            if (c == 0) __hip_atomic_store(line + (par ? PEE_LINE_FIN0 : PEE_LINE_FIN1), 0u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+            // dbg_stale (tests): plant a stale but valid-looking state there instead -- an
+            // inclusive prefix 0 and a set finished flag, both with this call's tag
+            const bool stale = b == 0 && c == dbg_stale;
+            lb_store(status_all + (1 - par) * stride + (size_t)b * nchunks + c, stale ? (LB_INC | tagw) : 0ull);
+            if (c == 0 || stale)
+                __hip_atomic_store(line + (par ? PEE_LINE_FIN0 : PEE_LINE_FIN1), stale ? fin_val : 0u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
         if (INPLACE || c != j) pee_load_chunk<T, NT>(src, W, CR, items, c, a0, a1, o0);
         if (copy_only) {
@@ -1417,20 +1438,21 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
         u64 pwv = 0;
         if (pay_st && tid >= 64) pwv = payload_all[(size_t)b * pw + min(tid - 64, pw - 1)];
         if (c == 0) {
-            if (tid == 0) { if (publish) lb_store(st, LB_INC | aggw); s_excl = 0; s_uexcl = 0; }
+            if (tid == 0) { if (publish) lb_store(st, LB_INC | aggw | tagw); s_excl = 0; s_uexcl = 0; }
         } else {
-            if (tid == 0 && publish) lb_store(st + c, LB_AGG | aggw);
+            if (tid == 0 && publish) lb_store(st + c, LB_AGG | aggw | tagw);
             if (tid < 64) {
                 bool to = false, fb = false;
                 LbSum ex;
                 if (INPLACE) ex = lb_exclusive(st, c, &to, &fb, spin_max, NoFallback(), fin_flag, L);
-                else ex = lb_exclusive<sc>(st, c, &to, &fb, spin_max, EmbedCount<T>{src, W, CR, items, Tthr, maxval}, fin_flag, L);
+                else ex = lb_exclusive<sc>(st, c, &to, &fb, spin_max, EmbedCount<T>{src, W, CR, items, Tthr, maxval}, fin_flag, L,
+                                           tag, fin_val);
                 if (tid == 0) {
                     if constexpr (sc) {
                         // inclusive prefix; past `end` saturated to L (successors only compare it with L)
                         const u64 ie = ex.e + agg;
-                        const u64 iu = (ex.u + agg_u) & 0x3FFFFFFFull;
-                        if (publish) lb_store(st + c, LB_INC | (ie >= L ? (u64)L : ie) | (iu << 32));
+                        const u64 iu = (ex.u + agg_u) & 0xFFFFFFull;
+                        if (publish) lb_store(st + c, LB_INC | (ie >= L ? (u64)L : ie) | (iu << 32) | tagw);
                         s_excl = (uint32_t)min(ex.e, (u64)0xFFFFFFFFull);
                         s_uexcl = (uint32_t)ex.u;
                     } else {
@@ -1547,7 +1569,7 @@ __global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover,
         if (tid == 0) {   // `end` is in this chunk (or there is none): later chunks need no cursor
             const bool fin = (excl < L && excl + agg >= L) || (L == 0 && c == 0) || (last && excl + agg < L);
             if (fin) {
-                __hip_atomic_store(fin_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(fin_flag, fin_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (INPLACE) atomicAdd(ctl, 1u);
                 if (sc) {   // no meta atomics (nothing zeroed it): the chunk holding `end` writes them
                     M->status = (last && excl + agg < L) ? 1 : 0;
@@ -1645,7 +1667,8 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
                                                       const codec_pee_meta* __restrict__ meta_all,
                                                       const u64* __restrict__ lm_all, int lmw, int nchunks, int B,
                                                       u64* status_all, uint32_t* ctl, u64* __restrict__ payload_all,
-                                                      int pw, int mode, uint32_t spin_max, int dbg_skip, uint32_t* diag) {
+                                                      int pw, int mode, uint32_t spin_max, int dbg_skip, uint32_t* diag,
+                                                      int sc_epoch, int dbg_stale) {
     typedef typename Vec8<T>::type V;
     __shared__ u64 sh64[8];
     __shared__ uint32_t s_v, s_excl;
@@ -1698,10 +1721,6 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
         // out of place chunk j is loaded while the ticket is in flight (a plain copy when past
         // `end`); in place only the ticketed chunk is read
         if (!INPLACE) pee_load_chunk<T, NT>(src, W, CR, items, j, a0, a1, o0);
-        // every slot arrives (copy chunks too); the returned count is used only later, so the
-        // map-word loads below are not held back behind the atomic's round trip
-        uint32_t arr_old = 0u;
-        if (sc && tid == 0) arr_old = pee_arrive(ctl, B, b, nchunks, j);
         const u64* lm = lm_all + (size_t)b * lmw;
         const bool noticket = !INPLACE && (mode & PEE_MODE_NOTICKET);
         u64 lwv[4] = {0, 0, 0, 0};   // location-map word of each item (4 bits of it used)
@@ -1724,11 +1743,15 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
             c = (int)s_v;
             if (INPLACE || c != j) pee_load_chunk<T, NT>(src, W, CR, items, c, a0, a1, o0);
         }
-        int par = 1;   // status-word buffer (calls that zero first use buffer 1)
-        if (sc) {      // wave 0 (the look-back) learns the call parity
+        // status-word buffer and epoch tag (calls that zero first use buffer 1, untagged)
+        const int par = sc ? (sc_epoch & 1) : 1;
+        const int tag = sc ? pee_sc_tag(sc_epoch) : -1;
+        const u64 tagw = sc ? LB_TAGW(tag) : 0ull;
+        if (sc) {
             if (tid == 0) {
-                par = pee_parity_of(arr_old);
-                lb_store(status_all + (1 - par) * stride + (size_t)b * nchunks + j, 0ull);   // next call's word
+                // the next call's word (dbg_stale, tests: a stale inclusive prefix 0 instead)
+                lb_store(status_all + (1 - par) * stride + (size_t)b * nchunks + j,
+                         (b == 0 && j == dbg_stale) ? (LB_INC | tagw) : 0ull);
                 // the in-place look-back flag (codec_pee_extract_flag_offset) reads clear after
                 // this call: an earlier in-place call may have set it, out of place nothing does
                 if (b == 0 && j == 0) __hip_atomic_store(ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1738,7 +1761,6 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
                     __hip_atomic_store(ctl + 32 + 32 * (size_t)b + (par ? PEE_LINE_FIN0 : PEE_LINE_FIN1), 0u,
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            par = __shfl(par, 0, 64);
         }
         if (c <= cend) {
             uint32_t actm = 0, innm = 0;
@@ -1771,19 +1793,20 @@ __global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, 
             u64 ptot;
             const u64 pex = block_excl_scan64_lds<256>(packed, sh64, &ptot);
             const uint32_t agg = (uint32_t)((ptot & 0xFFFFu) + ((ptot >> 16) & 0xFFFFu) + ((ptot >> 32) & 0xFFFFu) + (ptot >> 48));
-            u64* st = status_all + par * stride + (size_t)b * nchunks;   // par: valid in wave 0
+            u64* st = status_all + par * stride + (size_t)b * nchunks;
             const bool publish = c < cend && !(b == 0 && c == dbg_skip);
             if (c == 0) {
-                if (tid == 0) { if (publish) lb_store(st, LB_INC | (u64)agg); s_excl = 0; }
+                if (tid == 0) { if (publish) lb_store(st, LB_INC | (u64)agg | tagw); s_excl = 0; }
             } else {
-                if (tid == 0 && publish) lb_store(st + c, LB_AGG | (u64)agg);
+                if (tid == 0 && publish) lb_store(st + c, LB_AGG | (u64)agg | tagw);
                 if (tid < 64) {
                     bool to = false, fb = false;
                     LbSum ex;
                     if (INPLACE) ex = lb_exclusive(st, c, &to, &fb, spin_max, NoFallback());
-                    else ex = lb_exclusive(st, c, &to, &fb, spin_max, ExtractCount<T>{src, lm, W, CR, items, end, Tthr});
+                    else ex = lb_exclusive(st, c, &to, &fb, spin_max, ExtractCount<T>{src, lm, W, CR, items, end, Tthr},
+                                           nullptr, 0u, sc ? tag : -1);
                     if (tid == 0) {
-                        if (publish) lb_store(st + c, LB_INC | (ex.e + agg));
+                        if (publish) lb_store(st + c, LB_INC | ((ex.e + agg) & 0xFFFFFFFFull) | tagw);
                         s_excl = (uint32_t)ex.e;
                         if (to) { atomicOr(ctl + 1, 1u); atomicAdd(diag + 3, 1u); }   // codec_pee_extract_flag_offset
                         if (fb) atomicAdd(diag + 1, 1u);
@@ -3091,6 +3114,71 @@ static hipError_t pee_zero(hipStream_t st, void* a, size_t abytes, void* b = nul
     return hipGetLastError();
 }
 
+// ---- workspace registry.  Small out-of-place batches
+// (PEE_MODE_SC) carry two status-word buffers and finished flags from call to call in the
+// workspace, and the capacity pass leaves its bins clear for the next call, at offsets that
+// depend on the shape.  The library remembers, per (device, workspace pointer), the shape of
+// the last call that used it and the epoch of its self-cleaning calls: a call of another
+// shape zeroes the workspace (one launch, the cumulative diagnostic counters kept) before it
+// runs, so a workspace sized for the largest batch and reused for a smaller tail batch stays
+// exact; the first self-cleaning call seen on a pointer zeroes its state region; and every
+// self-cleaning call gets the next epoch (parity + tag, see PEE_MODE_SC).
+struct PeeWsShape {
+    int B, H, W, bytes;
+    uint32_t epoch;   // self-cleaning calls issued on this workspace (their status-word epoch)
+    bool sc_clean;    // the self-cleaning state region is known clean (zeroed here, or kept by SC calls)
+};
+static std::mutex g_pee_ws_mu;
+static std::map<std::pair<int, uintptr_t>, PeeWsShape> g_pee_ws;
+static std::pair<int, uintptr_t> pee_ws_key(const void* ws) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    return {dev, (uintptr_t)ws};
+}
+// the whole workspace but the diagnostic counters
+static hipError_t pee_ws_zero(void* ws, const PeeWs& L, hipStream_t st) {
+    char* w = static_cast<char*>(ws);
+    return pee_zero(st, w, L.diag, w + L.hist, L.total - L.hist);
+}
+// every workspace-taking PEE call, after its argument checks
+static hipError_t pee_ws_enter(void* ws, const codec_pee_params* P, const PeeWs& L, hipStream_t st) {
+    bool changed = false;
+    {
+        std::lock_guard<std::mutex> g(g_pee_ws_mu);
+        auto k = pee_ws_key(ws);
+        auto it = g_pee_ws.find(k);
+        const PeeWsShape now{P->B, P->H, P->W, P->bytes, 0u, it != g_pee_ws.end()};   // zeroed below if seen
+        if (it == g_pee_ws.end()) {
+            g_pee_ws.emplace(k, now);
+        } else if (it->second.B != now.B || it->second.H != now.H || it->second.W != now.W ||
+                   it->second.bytes != now.bytes) {
+            it->second = now;
+            changed = true;
+        }
+    }
+    return changed ? pee_ws_zero(ws, L, st) : hipSuccess;
+}
+// the self-cleaning words' unsafe-count field holds < 2^24 (LB_HI): bigger slices zero
+// instead; so does a call being captured into a graph (a replay would repeat one epoch)
+static bool pee_sc_fits(const codec_pee_params* P, hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+    return (long long)(P->H / 2) * (P->W / 2) <= PEE_SC_MAX_NC;
+}
+// this self-cleaning call's epoch (mod 126: parity and tag epoch % 63 + 1 both cycle in it);
+// *fresh: the state region is not known clean (first self-cleaning call on a pointer never
+// zeroed here): the caller zeroes it before the launch
+static int pee_ws_epoch(const void* ws, bool* fresh) {
+    std::lock_guard<std::mutex> g(g_pee_ws_mu);
+    auto it = g_pee_ws.find(pee_ws_key(ws));
+    if (it == g_pee_ws.end()) { *fresh = true; return 0; }   // not reached: pee_ws_enter registered it
+    *fresh = !it->second.sc_clean;
+    it->second.sc_clean = true;
+    const uint32_t e = it->second.epoch;
+    it->second.epoch = (e + 1u) % 126u;
+    return (int)e;
+}
+
 // row H-1 of every slice, src -> dst (one strided 2-D copy)
 static hipError_t pee_copy_last_rows(const codec_pee_params* P, const void* src, void* dst, hipStream_t st) {
     const size_t row = (size_t)P->W * P->bytes, pitch = (size_t)P->H * row, off = (size_t)(P->H - 1) * row;
@@ -3137,6 +3225,7 @@ int codec_pee_capacity(const codec_pee_params* P, const void* cover, int32_t tma
     if (t_out && !lengths) return set_err(CODEC_EINVAL, "codec_pee_capacity: t_out needs lengths");
     const PeeWs L = pee_ws(P);
     if (workspace_bytes < L.total) return set_err(CODEC_EINVAL, "workspace too small");
+    HIP_TRY(pee_ws_enter(workspace, P, L, as_stream(stream)));   // another shape's state: zeroed first
     hipStream_t st = as_stream(stream);
     uint32_t* hist = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.hist);
     // no memset: bins and arrival counters are zero on entry (zeroed workspace; each slice's
@@ -3166,6 +3255,19 @@ size_t codec_pee_diag_offset(const codec_pee_params* P) {
     return pee_ws(P).diag;
 }
 
+int codec_pee_reset(const codec_pee_params* P, void* workspace, size_t workspace_bytes, void* stream) {
+    int rc = pee_check(P);
+    if (rc) return rc;
+    if (!workspace) return set_err(CODEC_EINVAL, "codec_pee_reset: NULL workspace");
+    const PeeWs L = pee_ws(P);
+    if (workspace_bytes < L.total) return set_err(CODEC_EINVAL, "workspace too small");
+    hipStream_t st = as_stream(stream);
+    HIP_TRY(pee_zero(st, workspace, L.total));   // diagnostics included: a fresh workspace
+    std::lock_guard<std::mutex> g(g_pee_ws_mu);
+    g_pee_ws[pee_ws_key(workspace)] = PeeWsShape{P->B, P->H, P->W, P->bytes, 0u, true};
+    return 0;
+}
+
 int codec_pee_embed(const codec_pee_params* P, const void* cover, void* stego, const uint64_t* payload,
                     const int32_t* lengths, codec_pee_meta* meta, uint64_t* lm, void* workspace,
                     size_t workspace_bytes, void* stream) {
@@ -3181,6 +3283,7 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
         return set_err(CODEC_EINVAL, "codec_pee_embed: NULL pointer argument");
     const PeeWs L = pee_ws(P);
     if (workspace_bytes < L.total) return set_err(CODEC_EINVAL, "workspace too small");
+    HIP_TRY(pee_ws_enter(workspace, P, L, as_stream(stream)));   // another shape's state: zeroed first
     hipStream_t st = as_stream(stream);
     uint32_t* cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.cnt);
     uint32_t* off = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.off);
@@ -3198,7 +3301,7 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
     // scan + prefix embed takes 0.85 ms).
     // CODEC_PEE_ONEPASS: 0 forces the two-pass path; CODEC_PEE_1P_CHUNK_MAJOR=0: slice-major.
     // Out of place the chunk is the slot's own (CODEC_PEE_1P_NOTICKET=1, default): the per-slice
-    // ticket atomic cost 2-3 % (0.78 -> 0.76 ms at 256 x 2048^2, tools/tune_pee_mode2_cfg.json);
+    // ticket atomic cost 2-3 % (0.78 -> 0.76 ms at 256 x 2048^2, tools/archive/tune_pee_mode2_cfg.json);
     // extract drops it too, and then loads the chunk's location-map words together with
     // its pixels (0.76 -> 0.74 ms).
     // CODEC_PEE_1P_GROUP (slices, multiple of 8; default 32): the batch is walked in groups of
@@ -3206,7 +3309,7 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
     // of 32 (full chunk-major) or 1 (slice-major, whose look-back waits on the in-flight loads
     // of the 64 chunks before it): embed 0.81 -> 0.74 ms at 256 x 2048^2
     // (tools/tune_pee_group*_cfg.json); extract (CODEC_PEE_X_GROUP, default 32 as well)
-    // 0.74 -> 0.73 ms (tools/tune_pee_xnt_cfg.json).
+    // 0.74 -> 0.73 ms (tools/archive/tune_pee_xnt_cfg.json).
     // Small out-of-place batches run the single pass too (one launch instead of scan + locate
     // + prefix embed, which are launch/latency bound there; tools/pee_small_batch.py, 2048²
     // embed+extract step: B=1 50 -> 32 us, B=4 65 -> 47, B=8 93 -> 74, B=31 229 -> 207).
@@ -3228,7 +3331,7 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
         // ring depth of the in-place embed: it does not know `end` in advance, so the D - 1
         // chunks it has in flight past it are wasted reads; at 256 x 2048^2 the steady state
         // is HBM-bound (~5 TB/s of reads + writes), and D = 2 keeps enough in flight:
-        // 0.0825 -> 0.0789 ms (D = 3: 0.0824; tools/ab_depth.sh).  D = 1 refills early (the
+        // 0.0825 -> 0.0789 ms (D = 3: 0.0824; tools/archive/ab_depth.sh).  D = 1 refills early (the
         // next chunk's loads go out before this chunk's barrier and compute): 0.0746 -> 0.0726
         // ms (profiles/r04/ip_early_ab.log).  CODEC_PEE_SS_D=2 / 4 restore the late refill.
         const long long ss_d = pay_lds ? knob("CODEC_PEE_SS_D", 1) : 4;
@@ -3264,10 +3367,14 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
         // small out-of-place batches (flat slots, no ticket) clean up after themselves: no
         // zeroing launch (C2: one launch of ~2 us fewer per call); meta is written without
         // atomics out of place, so only in place (and the ticket modes) zero it
-        if (flat && (mode & PEE_MODE_NOTICKET) && knob("CODEC_PEE_SELFCLEAN", 1)) mode |= PEE_MODE_SC;
+        if (flat && (mode & PEE_MODE_NOTICKET) && knob("CODEC_PEE_SELFCLEAN", 1) && pee_sc_fits(P, st)) mode |= PEE_MODE_SC;
         if (!(mode & PEE_MODE_SC))
             HIP_TRY(pee_zero(st, stw, L.ctl - L.st + PEE_CTL_WORDS(P->B, L.nchunks) * 4, meta, (size_t)P->B * sizeof(codec_pee_meta),
                              inplace ? lm : nullptr, inplace ? (size_t)P->B * P->lm_words * 8 : 0));
+        bool sc_fresh = false;
+        const int sc_epoch = (mode & PEE_MODE_SC) ? pee_ws_epoch(workspace, &sc_fresh) : 0;
+        if (sc_fresh)   // a pointer never seen: start its self-cleaning state clean
+            HIP_TRY(pee_zero(st, stw, L.ctl - L.st + PEE_CTL_WORDS(P->B, L.nchunks) * 4));
         ProfScope prof(st, CODEC_K_PEE_EMBED1);
         const long long total = pee_total_slots(P->B, L.nchunks, pee_group8(P->B, mode, inplace));
         long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));
@@ -3275,11 +3382,12 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
         g = (g + 7) / 8 * 8;   // keep every workgroup on one slot lane (pee_slot)
         const uint32_t spin_max = (uint32_t)debug_knob("CODEC_PEE_LB_SPINS", inplace ? (1 << 22) : (1 << 14));
         const int dbg_skip = (int)debug_knob("CODEC_PEE_DEBUG_SKIP", 0) - 1;
+        const int dbg_stale = (int)debug_knob("CODEC_PEE_DEBUG_STALE", 0) - 1;
         uint32_t* diag = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.diag);
 #define PE1S(TT, NTV, IP, SCV) hipLaunchKernelGGL((k_pee_embed1<TT, NTV, IP, SCV>), dim3((unsigned)g), dim3(256), 0, st, \
             static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, \
             reinterpret_cast<const u64*>(payload), P->payload_words, L.nchunks, P->B, stw, ctl, meta, \
-            reinterpret_cast<u64*>(lm), P->lm_words, mode, spin_max, dbg_skip, diag, tps)
+            reinterpret_cast<u64*>(lm), P->lm_words, mode, spin_max, dbg_skip, diag, tps, sc_epoch, dbg_stale)
 #define PE1(TT, NTV, IP) do { if (!(IP) && (mode & PEE_MODE_SC)) PE1S(TT, NTV, false, true); else PE1S(TT, NTV, IP, false); } while (0)
         if (P->bytes == 2) {
             if (inplace) { if (nt) PE1(uint16_t, true, true); else PE1(uint16_t, false, true); }
@@ -3306,7 +3414,7 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
         dim3 grid((ntiles + per - 1) / per, P->B);
         if (vec) {
             const long long tot = (long long)ntiles * P->B;
-            long long gw = knob("CODEC_PEE_SCAN_GS_WGS", 32768);   // tools/tune_pee.py
+            long long gw = knob("CODEC_PEE_SCAN_GS_WGS", 32768);   // tools/archive/tune_pee.py
             if (gw > (tot + 3) / 4) gw = (tot + 3) / 4;
             if (gw < 1) gw = 1;
 #define PSCAN(TT, NTV) hipLaunchKernelGGL((k_pee_scan<TT, NTV>), dim3((unsigned)gw), dim3(256), 0, st, static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, cnt, L.ntiles_max, P->B, tps)
@@ -3372,6 +3480,7 @@ int codec_pee_embed_auto(const codec_pee_params* P, const void* cover, void* ste
     if (tmax < 1 || tmax > PEE_TMAX_MAX) return set_err(CODEC_EINVAL, "tmax must be in 1..64");
     const PeeWs L = pee_ws(P);
     if (workspace_bytes < L.total) return set_err(CODEC_EINVAL, "workspace too small");
+    HIP_TRY(pee_ws_enter(workspace, P, L, as_stream(stream)));   // another shape's state: zeroed first
     hipStream_t st = as_stream(stream);
     const bool inplace = cover == stego;
     const bool vec = (P->W % 8) == 0 && ((uintptr_t)cover % 16) == 0 && ((uintptr_t)stego % 16) == 0;
@@ -3455,6 +3564,7 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
         return set_err(CODEC_EINVAL, "codec_pee_extract: NULL pointer argument");
     const PeeWs L = pee_ws(P);
     if (workspace_bytes < L.total) return set_err(CODEC_EINVAL, "workspace too small");
+    HIP_TRY(pee_ws_enter(workspace, P, L, as_stream(stream)));   // another shape's state: zeroed first
     hipStream_t st = as_stream(stream);
     uint32_t* cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.cnt);
     uint32_t* off = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.off);
@@ -3513,9 +3623,13 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
                         : (knob("CODEC_PEE_X_CHUNK_MAJOR", knob("CODEC_PEE_1P_CHUNK_MAJOR", 1)) ? PEE_MODE_CMAJOR : 0) |
                               (knob("CODEC_PEE_X_NOTICKET", 1) ? PEE_MODE_NOTICKET : 0) |
                               ((int)(knob("CODEC_PEE_X_GROUP", 32) / 8) << 8);
-        if (flat && (mode & PEE_MODE_NOTICKET) && knob("CODEC_PEE_SELFCLEAN", 1)) mode |= PEE_MODE_SC;
+        if (flat && (mode & PEE_MODE_NOTICKET) && knob("CODEC_PEE_SELFCLEAN", 1) && pee_sc_fits(P, st)) mode |= PEE_MODE_SC;
         if (!(mode & PEE_MODE_SC))
             HIP_TRY(pee_zero(st, payload_out, (size_t)P->B * P->payload_words * 8, stw, L.ctl - L.st + PEE_CTL_WORDS(P->B, L.nchunks) * 4));
+        bool sc_fresh = false;
+        const int sc_epoch = (mode & PEE_MODE_SC) ? pee_ws_epoch(workspace, &sc_fresh) : 0;
+        if (sc_fresh)   // a pointer never seen: start its self-cleaning state clean
+            HIP_TRY(pee_zero(st, stw, L.ctl - L.st + PEE_CTL_WORDS(P->B, L.nchunks) * 4));
         ProfScope prof(st, CODEC_K_PEE_EXTRACT1);
         const long long total = pee_total_slots(P->B, L.nchunks, pee_group8(P->B, mode, inplace));
         long long g = knob(inplace ? "CODEC_PEE_IP_WGS" : "CODEC_PEE_1P_WGS", inplace ? 2048 : (1 << 30));
@@ -3523,11 +3637,12 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
         g = (g + 7) / 8 * 8;
         const uint32_t spin_max = (uint32_t)debug_knob("CODEC_PEE_LB_SPINS", inplace ? (1 << 22) : (1 << 14));
         const int dbg_skip = (int)debug_knob("CODEC_PEE_DEBUG_SKIP", 0) - 1;
+        const int dbg_stale = (int)debug_knob("CODEC_PEE_DEBUG_STALE", 0) - 1;
         uint32_t* diag = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.diag);
 #define PX1S(TT, NTV, IP, SCV) hipLaunchKernelGGL((k_pee_extract1<TT, NTV, IP, SCV>), dim3((unsigned)g), dim3(256), 0, st, \
             static_cast<const TT*>(stego), static_cast<TT*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm), \
             P->lm_words, L.nchunks, P->B, stw, ctl, reinterpret_cast<u64*>(payload_out), P->payload_words, mode, spin_max, \
-            dbg_skip, diag)
+            dbg_skip, diag, sc_epoch, dbg_stale)
 #define PX1(TT, NTV, IP) do { if (!(IP) && (mode & PEE_MODE_SC)) PX1S(TT, NTV, false, true); else PX1S(TT, NTV, IP, false); } while (0)
         if (P->bytes == 2) {
             if (inplace) { if (nt) PX1(uint16_t, true, true); else PX1(uint16_t, false, true); }

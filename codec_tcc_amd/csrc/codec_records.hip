@@ -48,7 +48,9 @@ __global__ __launch_bounds__(REC_NT) void k_pee_pack_records(const codec_pee_met
     u64* pay = r + REC_HDR;
     if (cnt >= 0 && cnt <= 2 * width) {
         uint32_t* idx = reinterpret_cast<uint32_t*>(pay);
-        for (int s = cnt + tid; s < 2 * width; s += REC_NT) idx[s] = 0u;
+        // every slot zeroed first (the record buffer is reused step to step), then the indices
+        for (int s = tid; s < 2 * width; s += REC_NT) idx[s] = 0u;
+        __syncthreads();
         uint32_t base = 0;
         for (int w0 = 0; w0 < dw && base < (uint32_t)cnt; w0 += REC_NT) {
             const int w = w0 + tid;
@@ -63,6 +65,14 @@ __global__ __launch_bounds__(REC_NT) void k_pee_pack_records(const codec_pee_met
                 v &= v - 1ull;
             }
             base += tot;
+        }
+        // fewer set bits in [0, end] than meta.lm_count says (a hand-built meta, an ELOOKBACK
+        // slice): the record carries the indices found, its header's lm_count is corrected to
+        // their number and flagged, so the receiver decodes exactly that map
+        if (base < (uint32_t)cnt && tid == 0) {
+            codec_pee_meta* rm = reinterpret_cast<codec_pee_meta*>(r);
+            rm->lm_count = (int)base;
+            rm->flags |= CODEC_PEE_RECORD_RECOUNTED;
         }
     } else {
         for (int w = tid; w < width; w += REC_NT) {

@@ -220,6 +220,8 @@ class RecordExchange:
 PEE_META_WORDS = (_lib.PEE_META_BYTES + 7) // 8
 PEE_END_FIELD = 3          # int32 index of codec_pee_meta.end
 PEE_LMCOUNT_FIELD = 9      # int32 index of codec_pee_meta.lm_count
+PEE_FLAGS_FIELD = 12       # int32 index of codec_pee_meta.flags
+RECORD_RECOUNTED = 2       # CODEC_PEE_RECORD_RECOUNTED
 assert PEE_META_WORDS == _lib.PEE_RECORD_HDR_WORDS
 
 
@@ -267,6 +269,11 @@ def pack_pee_records(meta, lm, width: int, out=None):
     tensors run the HIP kernel; CPU tensors (the gloo tests' synthetic records) a row loop
     of the same rule."""
     import torch
+    if meta.dtype != torch.uint8 or meta.dim() != 2 or int(meta.shape[1]) != _lib.PEE_META_BYTES:
+        raise ValueError(f"meta must be uint8 [B, {_lib.PEE_META_BYTES}], got {meta.dtype} {tuple(meta.shape)}")
+    if lm.dtype != torch.int64 or lm.dim() != 2 or int(lm.shape[0]) != int(meta.shape[0]):
+        raise ValueError(f"lm must be int64 [B, lm_words] with B = {int(meta.shape[0])}, got {lm.dtype} {tuple(lm.shape)}")
+    meta, lm = meta.contiguous(), lm.contiguous()   # a sliced view must not reach the kernel (ADVICE r4)
     B, lmw = int(meta.shape[0]), int(lm.shape[1])
     if out is None:
         out = torch.empty((B, PEE_META_WORDS + int(width)), dtype=torch.int64, device=meta.device)
@@ -288,6 +295,10 @@ def pack_pee_records(meta, lm, width: int, out=None):
             slots = np.zeros(2 * width, dtype=np.uint32)
             slots[: idx.size] = idx
             out[b, PEE_META_WORDS:] = torch.from_numpy(slots.view(np.int64))
+            if idx.size < cnt:   # fewer bits than lm_count says: the kernel's recount rule
+                hdr = out[b, :PEE_META_WORDS].view(torch.int32)
+                hdr[PEE_LMCOUNT_FIELD] = int(idx.size)
+                hdr[PEE_FLAGS_FIELD] |= RECORD_RECOUNTED
         else:
             n = min(width, lmw)
             out[b, PEE_META_WORDS: PEE_META_WORDS + n] = torch.from_numpy(pref[b, :n].view(np.int64))

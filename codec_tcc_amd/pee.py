@@ -68,6 +68,25 @@ class PeeCodec:
         self.workspace = torch.zeros(int(ws), dtype=torch.uint8, device=self.device)
         self.t_slices = torch.empty(self.B, dtype=torch.int32, device=self.device) if self.auto else None
 
+    def reset(self):
+        """Re-zero the workspace (codec_pee_reset, on the current stream): the state small
+        out-of-place batches carry from call to call starts afresh, and the cumulative
+        diagnostics read zero.  Called automatically after a failed call (include/codec_tcc.h,
+        codec_pee_workspace_bytes: recovery rules)."""
+        _lib.check(_lib.load().codec_pee_reset(C.byref(self._params(1)), self.workspace.data_ptr(),
+                                               self.workspace.numel(), _stream()), "codec_pee_reset")
+
+    def _guarded(self, fn, *args):
+        """Run one workspace call; on any exception re-zero the workspace, then re-raise."""
+        try:
+            return fn(*args)
+        except BaseException:
+            try:
+                self.reset()
+            except Exception:   # the original error is the one to report
+                pass
+            raise
+
     def _params(self, payload_words: int) -> _lib.PeeParams:
         return _lib.PeeParams(B=self.B, H=self.H, W=self.W, bytes=self.bytes, T=self.T, maxval=self.maxval,
                               payload_words=int(payload_words), lm_words=self.lm_words)
@@ -88,9 +107,9 @@ class PeeCodec:
         torch = _torch()
         tmax = self.tmax if tmax is None else int(tmax)
         caps = torch.empty((self.B, tmax), dtype=torch.int32, device=self.device)
-        _lib.check(_lib.load().codec_pee_capacity(C.byref(self._params(1)), covers.data_ptr(), tmax, None,
-                                                  caps.data_ptr(), None, self.workspace.data_ptr(),
-                                                  self.workspace.numel(), _stream()), "codec_pee_capacity")
+        self._guarded(lambda: _lib.check(_lib.load().codec_pee_capacity(
+            C.byref(self._params(1)), covers.data_ptr(), tmax, None, caps.data_ptr(), None, self.workspace.data_ptr(),
+            self.workspace.numel(), _stream()), "codec_pee_capacity"))
         return caps
 
     def embed(self, covers, payloads, *, stego=None, lm=None, meta=None, packed=None, check: bool = True) -> PeeEncoded:
@@ -110,21 +129,27 @@ class PeeCodec:
             meta = torch.empty((self.B, _lib.PEE_META_BYTES), dtype=torch.uint8, device=self.device)
         P = self._params(words.shape[1])
         lib = _lib.load()
-        if self.auto:   # capacity control: per-slice T on the device (fused into the embed
-            # launch where it runs slice-serial, else one read-only capacity pass first)
-            _lib.check(lib.codec_pee_embed_auto(C.byref(P), covers.data_ptr(), stego.data_ptr(), words.data_ptr(),
-                                                lens_t.data_ptr(), self.tmax, self.t_slices.data_ptr(),
-                                                meta.data_ptr(), lm.data_ptr(), self.workspace.data_ptr(),
-                                                self.workspace.numel(), _stream()), "codec_pee_embed_auto")
-        else:
-            _lib.check(lib.codec_pee_embed_ts(C.byref(P), covers.data_ptr(), stego.data_ptr(), words.data_ptr(),
-                                              lens_t.data_ptr(), None, meta.data_ptr(), lm.data_ptr(),
-                                              self.workspace.data_ptr(), self.workspace.numel(), _stream()),
-                       "codec_pee_embed")
+
+        def launch():
+            if self.auto:   # capacity control: per-slice T on the device (fused into the embed
+                # launch where it runs slice-serial, else one read-only capacity pass first)
+                _lib.check(lib.codec_pee_embed_auto(C.byref(P), covers.data_ptr(), stego.data_ptr(), words.data_ptr(),
+                                                    lens_t.data_ptr(), self.tmax, self.t_slices.data_ptr(),
+                                                    meta.data_ptr(), lm.data_ptr(), self.workspace.data_ptr(),
+                                                    self.workspace.numel(), _stream()), "codec_pee_embed_auto")
+            else:
+                _lib.check(lib.codec_pee_embed_ts(C.byref(P), covers.data_ptr(), stego.data_ptr(), words.data_ptr(),
+                                                  lens_t.data_ptr(), None, meta.data_ptr(), lm.data_ptr(),
+                                                  self.workspace.data_ptr(), self.workspace.numel(), _stream()),
+                           "codec_pee_embed")
+        self._guarded(launch)
         enc = PeeEncoded(stego=stego, lm=lm, meta=meta, lengths=list(lengths), payload_words=int(words.shape[1]),
                          config=self.config)
         if check:
-            _raise_lookback(enc.records())
+            recs = enc.records()
+            if any(r.status not in (0, 1) for r in recs):   # not a capacity overflow: start clean
+                self.reset()
+            _raise_lookback(recs)
         return enc
 
     def extract(self, stego, meta, lm, *, payload_words: int, cover=None, payload=None):
@@ -134,9 +159,9 @@ class PeeCodec:
         if payload is None:
             payload = torch.empty((self.B, int(payload_words)), dtype=torch.int64, device=self.device)
         P = self._params(payload_words)
-        _lib.check(_lib.load().codec_pee_extract(C.byref(P), stego.data_ptr(), meta.data_ptr(), lm.data_ptr(),
-                                                 cover.data_ptr(), payload.data_ptr(), self.workspace.data_ptr(),
-                                                 self.workspace.numel(), _stream()), "codec_pee_extract")
+        self._guarded(lambda: _lib.check(_lib.load().codec_pee_extract(
+            C.byref(P), stego.data_ptr(), meta.data_ptr(), lm.data_ptr(), cover.data_ptr(), payload.data_ptr(),
+            self.workspace.data_ptr(), self.workspace.numel(), _stream()), "codec_pee_extract"))
         return payload, cover
 
     def lookback_failed(self, payload_words: int = 1) -> bool:
@@ -164,6 +189,7 @@ class PeeCodec:
         words, cover = self.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words)
         host = words.cpu().numpy()
         if self.lookback_failed(enc.payload_words):
+            self.reset()
             raise RuntimeError("codec_pee_extract: in-place cursor look-back timed out; the recovered "
                                "payload is invalid (the restored cover is exact)")
         return [framing.unpack_bits(host[i], enc.lengths[i]) for i in range(self.B)], cover

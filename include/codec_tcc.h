@@ -8,7 +8,9 @@
  *   - every call is asynchronous on `stream` and thread-safe given distinct streams and
  *     buffers; nothing is allocated inside (workspace is caller-provided).  A workspace is
  *     one of those buffers: calls that share one are ordered on one stream, since some
- *     carry state from call to call in it (codec_pee_workspace_bytes);
+ *     carry state from call to call in it (codec_pee_workspace_bytes states the recovery
+ *     rules: shape changes are detected and re-zeroed, stale state is never read as valid,
+ *     codec_pee_reset after a failed call);
  *   - return value: 0 on success, < 0 on error (argument error or negated hipError_t);
  *     codec_last_error() returns a thread-local message.  The Python host layer turns a
  *     non-zero status into an exception, as the reference raises ValueError (codec.py:34-37).
@@ -234,9 +236,23 @@ typedef struct codec_pee_meta {
 
 /* Zero-initialise the workspace once before its first use (the diagnostic counters live
  * in it; everything else is cleared by the calls themselves).  Small out-of-place batches
- * (B <= 7) keep call-to-call state in it (status words by call parity, per-chunk arrival
- * counts): use one workspace with one (B, H, W), or zero it again before changing them. */
+ * (B <= 7) keep call-to-call state in it (per-chunk arrival counts; status words by call
+ * parity, each carrying the call's epoch tag).  Recovery rules:
+ *   - shape change: the library remembers per (device, workspace pointer) the shape of the
+ *     last call; a call of another (B, H, W, bytes) zeroes the workspace first (one extra
+ *     launch; the diagnostic counters are kept), so one workspace sized for the largest
+ *     batch may serve smaller batches in turn;
+ *   - desynchronised counters (a call that never completed, a graph replayed against a
+ *     workspace another shape has used): a chunk reads only status words carrying its own
+ *     epoch tag, so a stale word counts as "not published", the bounded wait ends in the
+ *     pixel-count fallback and the results stay exact (slower; codec_pee_diag_offset counts
+ *     the fallbacks).  codec_pee_reset restores the fast path;
+ *   - after any failed call (non-zero return, ELOOKBACK status, a raised exception in the
+ *     host layer) call codec_pee_reset before reusing the workspace: PeeCodec does so. */
 size_t codec_pee_workspace_bytes(const codec_pee_params* P);
+/* Re-zero the whole workspace (diagnostic counters included) on `stream` and record P's
+ * shape as its owner.  No reference counterpart (workspace management only). */
+int codec_pee_reset(const codec_pee_params* P, void* workspace, size_t workspace_bytes, void* stream);
 /* Byte offset in the workspace of a uint32 flag that codec_pee_extract's IN-PLACE single
  * pass sets (non-zero) when a chunk's cursor look-back gave up (the recovered payload of
  * that call is not valid); cleared at the start of every codec_pee_extract.  0 on bad
@@ -301,6 +317,9 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
  * Slice b's map travels exactly when width >= min(ceil(lm_count / 2), ceil((end + 1) / 64)).
  * meta/lm: codec_pee_embed outputs ([B], [B][lm_words]); records: [B][HDR + width]. */
 #define CODEC_PEE_RECORD_HDR_WORDS 8
+/* set in a packed record's meta.flags when the map held fewer set bits in [0, end] than
+ * meta.lm_count said (the record's lm_count is then the number found and travels sparse) */
+#define CODEC_PEE_RECORD_RECOUNTED 2
 int codec_pee_pack_records(int32_t B, int32_t lm_words, const codec_pee_meta* meta, const uint64_t* lm,
                            int32_t width, uint64_t* records, void* stream);
 /* Inverse for n gathered records: meta_out[n] (may be NULL) and lm_out[n][lm_cols] (may be

@@ -216,6 +216,7 @@ int main() {
         EXPECT_ZERO(codec_pee_workspace_bytes(&P));
         EXPECT_ZERO(codec_pee_extract_flag_offset(&P));
         EXPECT_ZERO(codec_pee_diag_offset(&P));
+        EXPECT_NEG(codec_pee_reset(&P, p, 1u << 30, nullptr));
         EXPECT_NEG(codec_pee_embed(&P, p, p, w64, i32, pmeta, w64, p, 1u << 30, nullptr));
         EXPECT_NEG(codec_pee_embed_ts(&P, p, p, w64, i32, i32, pmeta, w64, p, 1u << 30, nullptr));
         EXPECT_NEG(codec_pee_capacity(&P, p, 4, i32, i32, i32, p, 1u << 30, nullptr));
@@ -253,6 +254,9 @@ int main() {
         EXPECT_NEG(codec_pee_extract(&P, p, pmeta, w64, p, nullptr, p, ws, nullptr));
         EXPECT_NEG(codec_pee_extract(&P, p, pmeta, w64, p, w64, nullptr, ws, nullptr));
         EXPECT_NEG(codec_pee_extract(&P, p, pmeta, w64, p, w64, p, ws - 1, nullptr));
+        EXPECT_NEG(codec_pee_reset(nullptr, p, ws, nullptr));
+        EXPECT_NEG(codec_pee_reset(&P, nullptr, ws, nullptr));
+        EXPECT_NEG(codec_pee_reset(&P, p, ws - 1, nullptr));
     }
     // exchange records
     EXPECT_NEG(codec_pee_pack_records(-1, 4, pmeta, w64, 1, w64, nullptr));

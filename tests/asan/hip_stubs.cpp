@@ -44,6 +44,10 @@ hipError_t hipMemcpyFromSymbol(void*, const void*, size_t, size_t, hipMemcpyKind
     return hipErrorNoDevice;
 }
 hipError_t hipGetDevice(int*) { return hipErrorNoDevice; }
+hipError_t hipStreamIsCapturing(hipStream_t, hipStreamCaptureStatus* s) {
+    if (s) *s = hipStreamCaptureStatusNone;
+    return hipErrorNoDevice;
+}
 hipError_t hipDeviceGetAttribute(int*, hipDeviceAttribute_t, int) { return hipErrorNoDevice; }
 hipError_t hipEventCreate(hipEvent_t*) { return hipErrorNoDevice; }
 hipError_t hipEventDestroy(hipEvent_t) { return hipErrorNoDevice; }

@@ -149,10 +149,69 @@ def test_bench_launches_its_own_ranks():
     assert out["pee"]["distributed"]["narrow_gathers"] == 0
     assert out["lsb"]["roundtrip_ok"] is True and out["lsb"]["exchange_ok"] is True, out["lsb"]
     assert out["c4"]["roundtrip_ok"] is True and out["c4"]["exchange_ok"] is True, out["c4"]
+    # the per-rank records: one per rank, in rank order, over the named backend
+    rk = out["ranks"]
+    assert [r["rank"] for r in rk] == [0, 1] and all(r["world_size"] == 2 and r["backend"] == "gloo" for r in rk)
+    assert all(r["ms_per_step"] > 0 and r["kernels_only_ms"] > 0 and r["pci"] for r in rk), rk
+    assert out["distinct_devices"] == 1          # both gloo ranks share the box's one GPU
+    assert not any(k.startswith("_") for k in out["pee"]), out["pee"].keys()
     # a launcher that started a different number of ranks is refused
     bad = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2"],
                          env=dict(env, WORLD_SIZE="1", RANK="0"), cwd=repo, capture_output=True, text=True, timeout=120)
     assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr
+
+
+@pytest.mark.timeout(900)
+def test_bench_eight_ranks_rehearsal():
+    """the driver's 8-GPU run rehearsed at 8 ranks on the box's one GPU
+    (gloo): `bench.py --gpus 8` starts 8 fresh rank processes before any GPU call, every
+    exchange (headline MED-PEE, LSB, the C4 leg's 256 x 512^2 per rank) round-trips exactly
+    with no narrow gather, the `ranks` array names all 8 ranks, and no rank pid survives."""
+    import json
+    import subprocess
+    import sys
+    import threading
+
+    from test_bench_host import _gone, _kill_all
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    cmd = [sys.executable, "-u", os.path.join(repo, "bench.py"), "--gpus", "8", "--backend", "gloo", "--batch", "4",
+           "--size", "512", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0", "--c2", "0", "--no-profile",
+           "--payload-chars", "256"]
+    proc = subprocess.Popen(cmd, env=env, cwd=repo, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    pids, err = [], []
+
+    def drain():                 # keep the launcher's stderr moving; pick up the rank pids
+        for line in proc.stderr:
+            err.append(line)
+            if line.startswith("bench.py: rank pids "):
+                pids.extend(int(x) for x in line.split()[3:])
+    t = threading.Thread(target=drain, daemon=True)
+    t.start()
+    try:
+        out_s = proc.stdout.read()
+        rc = proc.wait(timeout=840)
+        t.join(timeout=10)
+        assert rc == 0, "".join(err)[-4000:]
+        assert len(pids) == 8, pids
+        lines = [ln for ln in out_s.splitlines() if ln.startswith("{")]
+        assert len(lines) == 1, out_s[-2000:]
+        out = json.loads(lines[0])
+        assert out["n_gpus"] == 8 and out["config"]["global_batch"] == 32
+        assert out["roundtrip_ok"] is True and out["pee"]["exchange_ok"] is True, out["pee"]
+        assert out["pee"]["distributed"]["narrow_gathers"] == 0
+        assert out["lsb"]["roundtrip_ok"] is True and out["lsb"]["exchange_ok"] is True, out["lsb"]
+        assert out["c4"]["roundtrip_ok"] is True and out["c4"]["exchange_ok"] is True, out["c4"]
+        assert out["c4"]["distributed"]["narrow_gathers"] == 0
+        rk = out["ranks"]
+        assert [r["rank"] for r in rk] == list(range(8)), rk
+        assert all(r["world_size"] == 8 and r["backend"] == "gloo" and r["ms_per_step"] > 0 for r in rk), rk
+        assert len({r["pid"] for r in rk}) == 8 and {r["pid"] for r in rk} == set(pids)
+        assert _gone(pids), pids
+    finally:
+        if proc.poll() is None:
+            proc.kill()
+        _kill_all(pids)
 
 
 @pytest.mark.timeout(200)

@@ -99,7 +99,7 @@ def test_library_digest_ties_binary_to_sources(monkeypatch, tmp_path):
         build.build()
     assert build.library_digest() == build.source_digest()
     monkeypatch.setattr(_lib, "_lib", None)                 # force a fresh load
-    monkeypatch.setattr(build, "source_digest", lambda: "0" * 64)
+    monkeypatch.setattr(build, "source_digest", lambda *a, **k: "0" * 64)
     with pytest.raises(RuntimeError, match="not built from these sources"):
         _lib.load()
     monkeypatch.undo()
@@ -112,6 +112,25 @@ def test_library_digest_ties_binary_to_sources(monkeypatch, tmp_path):
         _lib.load(str(fake))
     monkeypatch.undo()
     assert _lib.load().codec_build_digest().decode() == build.source_digest()
+
+
+def test_library_digest_uses_the_flags_it_was_built_with(monkeypatch):
+    """the build flags travel inside the library, so a process whose environment
+    would build with other flags (CODEC_OFFLOAD_ARCH / CODEC_BUILD_DEFS) still loads it; a
+    tree without the sources fails with a clear message, not an OSError."""
+    from codec_tcc_amd import build
+    if build.needs_build():
+        build.build()
+    assert build.library_flags() == build.FLAGS
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(build, "FLAGS", build.FLAGS + ["-DSOME_OTHER_BUILD"])
+    assert _lib.load() is not None
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(build, "SRCS", build.SRCS + [os.path.join(REPO, "codec_tcc_amd", "csrc", "absent.hip")])
+    with pytest.raises(RuntimeError, match="absent"):
+        _lib.load()
+    monkeypatch.undo()
+    assert _lib.load() is not None
 
 
 def test_library_exports_every_header_symbol():

@@ -383,6 +383,148 @@ def test_gpu_selfclean_across_calls(h, w, bsz, monkeypatch):
     assert pw is not None and codec.diagnostics()["embed_unrecovered_chunks"] == 0
 
 
+def _check_step(codec, covers, payloads, T, enc=None):
+    """Embed (unless given) + extract out of place; every output equal to the oracle."""
+    import torch
+    from codec_tcc_amd import framing
+    from codec_tcc_amd.pee import lm_bits
+    if enc is None:
+        enc = codec.embed(torch.from_numpy(covers).cuda(), payloads)
+    recs = enc.records()
+    stego = enc.stego.cpu().numpy()
+    got_bits = []
+    for i in range(len(covers)):
+        st, side = P.pee_embed(covers[i], payloads[i], T, truncate=True)
+        assert recs[i].end == side["end"] and recs[i].status == side["status"], i
+        assert recs[i].lm_count == int(side["lm"].sum()), i
+        np.testing.assert_array_equal(stego[i], st)
+        np.testing.assert_array_equal(lm_bits(enc, i), side["lm"])
+        got_bits.append(payloads[i][: side["L"]])
+    words, cover = codec.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words)
+    want, _ = framing.pack_bits(got_bits, words=enc.payload_words)
+    np.testing.assert_array_equal(words.cpu().numpy().view(np.uint64), want.view(np.uint64))
+    np.testing.assert_array_equal(cover.cpu().numpy(), covers)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [0, 1, 3])
+def test_gpu_stale_workspace_state_stays_exact(chunk, monkeypatch):
+    """the self-cleaning state a call leaves for the next one is made stale
+    on purpose (CODEC_PEE_DEBUG_STALE: chunk `chunk` of slice 0 plants, instead of clearing,
+    an inclusive prefix 0 in the next call's status word and sets the next call's finished
+    flag -- what a call abandoned mid-kernel, or one whose clears never ran, would leave).
+    Both carry the planting call's epoch tag, so the next call reads them as "not published"
+    (a chunk past them waits for the real word; with CODEC_PEE_DEBUG_SKIP the real word never
+    comes and the bounded wait ends in the pixel-count fallback).  Every out-of-place embed
+    and extract equals the oracle -- never a stego built from the stale prefix -- and
+    reset() leaves nothing that needs a fallback."""
+    torch = pytest.importorskip("torch")
+    from codec_tcc_amd.pee import PeeCodec
+    monkeypatch.setenv("CODEC_PEE_ONEPASS", "1")
+    bsz, h, w, T = 2, 512, 512, 2                 # 16 chunks per slice, flat self-cleaning slots
+    codec = PeeCodec(bsz, h, w, T=T)
+
+    def batch(k):
+        covers = np.stack([synth.ct12(h, w, 700 + 10 * k + i) for i in range(bsz)])
+        return covers, [_bits(P.capacity(c, T) - 7 * i, 900 + 10 * k + i) for i, c in enumerate(covers)]
+
+    _check_step(codec, *batch(0), T)
+    monkeypatch.setenv("CODEC_DEBUG", "1")
+    monkeypatch.setenv("CODEC_PEE_LB_SPINS", "64")
+    monkeypatch.setenv("CODEC_PEE_DEBUG_STALE", str(chunk + 1))
+    for k in range(1, 5):                         # every call plants stale state for the next one
+        _check_step(codec, *batch(k), T)
+    assert codec.repaired() == 0, codec.diagnostics()   # stale words ignored, the real ones awaited
+    # the planted chunk's successor never publishes either: the wait must end in the fallback,
+    # not in the planted prefix 0
+    monkeypatch.setenv("CODEC_PEE_DEBUG_SKIP", str(chunk + 2))
+    for k in range(5, 8):
+        _check_step(codec, *batch(k), T)
+    d = codec.diagnostics()
+    assert d["embed_fallback_chunks"] >= 1 and d["extract_fallback_chunks"] >= 1, d
+    assert d["embed_unrecovered_chunks"] == 0 == d["extract_unrecovered_chunks"], d
+    monkeypatch.delenv("CODEC_PEE_DEBUG_SKIP")
+    monkeypatch.delenv("CODEC_PEE_DEBUG_STALE")
+    codec.reset()
+    for k in range(8, 10):
+        _check_step(codec, *batch(k), T)
+    assert codec.repaired() == 0, codec.diagnostics()
+    del torch
+
+
+@pytest.mark.gpu
+def test_gpu_workspace_reused_across_batch_sizes(monkeypatch):
+    """a workspace sized for the largest batch serves a smaller tail batch (B = 3,
+    then 2, then 3 ... on ONE workspace, through the C ABI) -- the library notices the shape
+    change and re-zeroes the self-cleaning state, so every call equals the oracle."""
+    import ctypes as C
+
+    import torch
+    from codec_tcc_amd import _lib, framing
+    from codec_tcc_amd.codec import _stream
+    from codec_tcc_amd.pee import PeeCodec
+    monkeypatch.setenv("CODEC_PEE_ONEPASS", "1")
+    h, w, T = 256, 512, 2
+    big = PeeCodec(3, h, w, T=T)
+    ws = big.workspace
+    lib = _lib.load()
+    for k, bsz in enumerate([3, 2, 2, 3, 1, 3, 2]):
+        covers = np.stack([synth.ct12(h, w, 40 + 10 * k + i) for i in range(bsz)])
+        pays = [_bits(P.capacity(c, T) - 11 * i - k, 70 + 10 * k + i) for i, c in enumerate(covers)]
+        packed, lengths = framing.pack_bits([np.asarray(p) for p in pays])
+        words = torch.from_numpy(packed).cuda()
+        lens = torch.tensor(lengths, dtype=torch.int32, device="cuda")
+        prm = _lib.PeeParams(B=bsz, H=h, W=w, bytes=2, T=T, maxval=65535, payload_words=int(words.shape[1]),
+                             lm_words=big.lm_words)
+        assert lib.codec_pee_workspace_bytes(C.byref(prm)) <= ws.numel()
+        cov = torch.from_numpy(covers).cuda()
+        stego = torch.empty_like(cov)
+        lm = torch.empty((bsz, big.lm_words), dtype=torch.int64, device="cuda")
+        meta = torch.empty((bsz, _lib.PEE_META_BYTES), dtype=torch.uint8, device="cuda")
+        _lib.check(lib.codec_pee_embed_ts(C.byref(prm), cov.data_ptr(), stego.data_ptr(), words.data_ptr(),
+                                          lens.data_ptr(), None, meta.data_ptr(), lm.data_ptr(), ws.data_ptr(),
+                                          ws.numel(), _stream()), "embed")
+        out = torch.empty((bsz, int(words.shape[1])), dtype=torch.int64, device="cuda")
+        rest = torch.empty_like(cov)
+        _lib.check(lib.codec_pee_extract(C.byref(prm), stego.data_ptr(), meta.data_ptr(), lm.data_ptr(),
+                                         rest.data_ptr(), out.data_ptr(), ws.data_ptr(), ws.numel(), _stream()),
+                   "extract")
+        st_h = stego.cpu().numpy()
+        for i in range(bsz):
+            st, _side = P.pee_embed(covers[i], pays[i], T, truncate=True)
+            np.testing.assert_array_equal(st_h[i], st, err_msg=f"call {k} slice {i}")
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint64), packed.view(np.uint64))
+        np.testing.assert_array_equal(rest.cpu().numpy(), covers)
+    assert big.repaired() == 0
+
+
+@pytest.mark.gpu
+def test_gpu_reset_after_failed_call(monkeypatch):
+    """A call that fails (here: an in-place look-back made to time out, status ELOOKBACK)
+    re-zeroes the workspace before the exception leaves PeeCodec.embed: the cumulative
+    counters read zero again and the next calls are exact."""
+    torch = pytest.importorskip("torch")
+    from codec_tcc_amd.pee import PeeCodec
+    monkeypatch.setenv("CODEC_DEBUG", "1")
+    monkeypatch.setenv("CODEC_PEE_ONEPASS", "1")
+    monkeypatch.setenv("CODEC_PEE_LB_SPINS", "256")
+    bsz, h, w, T = 2, 256, 256, 2
+    covers = np.stack([synth.ct12(h, w, 520 + i) for i in range(bsz)])
+    payloads = [_bits(P.capacity(c, T) - 3, 80 + i) for i, c in enumerate(covers)]
+    codec = PeeCodec(bsz, h, w, T=T)
+    monkeypatch.setenv("CODEC_PEE_DEBUG_SKIP", "2")
+    work = torch.from_numpy(covers).cuda()
+    enc = codec.embed(work, payloads, stego=work, check=False)
+    assert codec.diagnostics()["embed_unrecovered_chunks"] >= 1       # the failure is recorded ...
+    work = torch.from_numpy(covers).cuda()
+    with pytest.raises(RuntimeError, match="look-back"):
+        codec.embed(work, payloads, stego=work)
+    assert codec.diagnostics()["embed_unrecovered_chunks"] == 0       # ... and reset with the raise
+    monkeypatch.delenv("CODEC_PEE_DEBUG_SKIP")
+    del enc
+    _check_step(codec, covers, payloads, T)
+
+
 @pytest.mark.gpu
 def test_gpu_fault_knobs_inert_without_master_switch(monkeypatch):
     """a leaked CODEC_PEE_DEBUG_SKIP / CODEC_PEE_LB_SPINS has no effect
