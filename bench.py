@@ -9,8 +9,9 @@ stream after embed, overlapped with extract).  `value` / `ms_per_step` are that 
 
 Side legs in the same JSON line: `lsb` (the reference's own bit-plane LSB pixel path,
 src/codec.py:412-487 + 752-793, bit-exact with it), `inplace` (the PEE step with stego =
-cover), `quality` (src/mse.py metrics of the LSB stego), `c3` (256 x 512^2), `c2`
-(1 x 2048^2).  Prints ONE JSON line (rank 0).
+cover), `quality` / `pee.quality` (src/mse.py metrics of the LSB and the MED-PEE stego),
+`c3` (256 x 512^2), `c2` (1 x 2048^2); at N > 1 `ranks` (what each rank ran on).  Prints ONE
+JSON line (rank 0).
 
     python bench.py                              # N=1, 256 x 2048^2 ct12, K=20, W=3
     torchrun --nproc-per-node N bench.py --gpus N
@@ -466,6 +467,8 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
         name, ta = targs.get(tag, (tag, None))
         return pmc_traffic(name, B, H, W, kind, ta)
 
+    if not inplace:
+        res["_stego"] = stego      # the headline's stego quality (bench_quality, outside the timings)
     if inplace:
         # algorithmic bytes: every 8-px x 2-row item up to the one holding `end` is read
         # (candidates + their neighbours), its candidate row written back
@@ -647,8 +650,9 @@ def bench_c2(args, torch, dev, rank):
 
 
 def bench_quality(args, torch, covers, stego, B, H, W):
-    """Stego quality of the LSB leg's output (reference src/mse.py metrics): one read-only
-    pass over cover + stego (k_quality), metrics from exact moments on the host."""
+    """Stego quality of a leg's output -- the headline MED-PEE stego (`pee.quality`) and the
+    LSB one (`quality`) -- with the reference's src/mse.py metrics: one read-only pass over
+    cover + stego (k_quality), metrics from exact moments on the host."""
     from codec_tcc_amd import _lib
     from codec_tcc_amd import quality as Q
     q = Q.quality(covers, stego)
@@ -880,6 +884,10 @@ def main():
     covers = make_covers(torch, args.kind, B, H, W, dev, seed=rank * B)
 
     head = bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, exchange=world > 1)
+    pee_stego = head.pop("_stego")
+    if rank == 0:   # MED-PEE stego quality (src/mse.py metrics) beside the LSB one
+        head["quality"] = bench_quality(args, torch, covers, pee_stego, B, H, W)
+    del pee_stego
     inplace = bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, inplace=True)
     lsb = None
     quality = None

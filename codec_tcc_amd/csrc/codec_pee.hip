@@ -2056,6 +2056,40 @@ __device__ __forceinline__ void ss_scan(uint32_t n, uint32_t (*wtot)[16], int pa
     *wbase = wb;
 }
 
+// Chained wave scan (round 5; in-place embed): the chunk's one workgroup
+// barrier replaced by per-wave LDS words.  Chunk k: every wave publishes its count of
+// expandable candidates in agg[k % 4][wave], tagged with k, then waits only for the words it
+// needs -- the LOWER waves' of chunk k (its rank prefix inside the chunk) and every wave's of
+// chunk k - 1 (the running count: chunk k's start) -- read with one LDS load per lane and summed
+// by DPP row scans (lanes 0-15: chunk k - 1, lanes 16-31: chunk k).  A wave never waits for a
+// higher wave of its own chunk, so the fast waves run ahead instead of idling at a barrier;
+// every wave publishes before it waits, so nothing can deadlock, and a wave is never more than
+// two chunks ahead of another (chunk k needs all of k - 1), so four slots cannot be overwritten
+// while still read.  Same ranks as ss_scan_small, one chunk later for the running total.
+__device__ __forceinline__ uint32_t chain_tag(int k) { return ((uint32_t)(k & 0x7FFF) | 0x8000u) << 16; }
+__device__ __forceinline__ void ss_chain_scan(uint32_t wt, uint32_t (*agg)[16], int k, int wv, int lane,
+                                              uint32_t* tot_prev, uint32_t* pre) {
+    if (lane == 0)
+        __hip_atomic_store(&agg[k & 3][wv], chain_tag(k) | wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const bool prev = lane < 16 && k > 0;
+    const bool cur = lane >= 16 && lane < 16 + wv;
+    uint32_t* slot = prev ? &agg[(k - 1) & 3][lane & 15] : &agg[k & 3][lane & 15];
+    const uint32_t want = prev ? chain_tag(k - 1) : chain_tag(k);
+    uint32_t v;
+    for (;;) {   // wave-uniform exit
+        v = (prev || cur) ? __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : want;
+        if (!__ballot((v & 0xFFFF0000u) != want)) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    int y = (prev || cur) ? (int)(v & 0xFFFFu) : 0;
+    y += __builtin_amdgcn_update_dpp(0, y, 0x111, 0xF, 0xF, true);   // row_shr:1 (lane 0 of a row reads 0)
+    y += __builtin_amdgcn_update_dpp(0, y, 0x112, 0xF, 0xF, true);   // row_shr:2
+    y += __builtin_amdgcn_update_dpp(0, y, 0x114, 0xF, 0xF, true);   // row_shr:4
+    y += __builtin_amdgcn_update_dpp(0, y, 0x118, 0xF, 0xF, true);   // row_shr:8
+    *tot_prev = (uint32_t)__builtin_amdgcn_readlane(y, 15);
+    *pre = wv ? (uint32_t)__builtin_amdgcn_readlane(y, 15 + wv) : 0u;
+}
+
 // counters of the fused capacity phase (AUTO): the top tmax * 1024 words of the pad, below
 // its last word; the payload (PAY_LDS) sits at the bottom
 #define SS_AUTO_CNT_BASE(tmax) (SS_PAD_WORDS - 1 - (tmax) * SS_THREADS)
@@ -2066,7 +2100,7 @@ __device__ __forceinline__ void ss_scan(uint32_t n, uint32_t (*wtot)[16], int pa
 // lane-private LDS counters, then takes the smallest T <= tmax whose capacity holds the
 // slice's payload (pee_select_slice's rule).  The embed that follows re-reads the slice from
 // the MALL (C3: 134 MB batch); no second launch, no global histogram, no arrival counter.
-template <typename T, bool NT, bool INPLACE, int D, bool PAY_LDS, bool AUTO = false>
+template <typename T, bool NT, bool INPLACE, int D, bool PAY_LDS, bool AUTO = false, bool CHAIN = false>
 __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict__ cover, T* stego, int H, int W, int T0,
                                                              int maxval, const int32_t* __restrict__ lengths,
                                                              const int32_t* __restrict__ tps,
@@ -2075,9 +2109,11 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
                                                              u64* __restrict__ lm_all, int lmw, char* __restrict__ sink,
                                                              int tmax, int32_t* __restrict__ t_out) {
     typedef typename Vec8<T>::type V;
+    static_assert(!CHAIN || (INPLACE && D == 1 && PAY_LDS && !AUTO), "the chained scan serves the in-place early ring");
     __shared__ uint32_t ss_pad[SS_PAD_WORDS];
     __shared__ uint32_t wtot[2][16];
     __shared__ uint32_t red[2][16];
+    __shared__ uint32_t agg[CHAIN ? 4 : 1][16];   // CHAIN: tagged per-wave counts, ss_chain_scan
     __shared__ int s_end;
     __shared__ uint32_t s_bins[AUTO ? PEE_TMAX_MAX : 1];
     __shared__ int s_T;
@@ -2186,11 +2222,14 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
     if (PAY_LDS) {   // the payload in LDS once: no dependent global round trip per chunk
         const int nw = min(pw, (int)((L + 63u) >> 6));
         for (int w = tid; w < nw; w += SS_THREADS) pay[w] = payload[w];
+        if (CHAIN && tid < 64) agg[tid >> 4][tid & 15] = 0u;
         lds_barrier();
     }
     uint32_t running = 0, rest = 0, unsafe_n = 0;
     int par = 0, last = -1;
-    bool live = L > 0;   // uniform: the chunk holding bit L-1 is still to come
+    // uniform (CHAIN: per wave): the chunk holding bit L-1 may still be to come
+    bool live = L > 0;
+    uint32_t run_at = 0;   // CHAIN: running count at the start of chunk `last`
 
     // one chunk, processed in the ring registers, then the ring slot is refilled.  D == 1
     // (EARLY): the chunk's data is taken into working registers and the slot refilled at
@@ -2241,9 +2280,25 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
             }
             if (!ok) esm = 0u;
             const uint32_t n = (uint32_t)__popc(esm);
-            last = k;
             uint32_t ex, tot, wb;
-            ss_scan_small(n, wtot, par, &ex, &tot, &wb);
+            if constexpr (CHAIN) {
+                uint32_t wt, tprev, pre;
+                ex = wave_excl_small(n, &wt);
+                ss_chain_scan(wt, agg, k, wv, lane, &tprev, &pre);
+                running += tprev;              // the start of chunk k
+                ex += pre;
+                wb = pre;
+                tot = 0u;                      // added at chunk k + 1
+                if (running >= L) esm = 0u;    // chunk k lies past `end` (m = 0 below: nothing moves)
+                else { last = k; run_at = running; }
+                // the next chunk is needed unless this wave's own inclusive prefix already reaches L
+                // (monotone in the wave index: the waves that stop are an upper range of them, so
+                // no wave waits on one that stopped)
+                live = running + pre + wt < L;
+            } else {
+                last = k;
+                ss_scan_small(n, wtot, par, &ex, &tot, &wb);
+            }
             SS_STAMP(4 * k + 2);
             par ^= 1;
             // this lane's expandable candidates take ranks [rs, rs + n): their payload bits
@@ -2284,7 +2339,7 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
             touched = procm != 0;
             // the lane holding rank L-1 (1 <= L - rs <= n): `end` is its last processed
             // expandable candidate; one lane of the slice, once
-            if (m != 0 && L - rs <= n) s_end = (int)(4 * it) + 31 - __clz(procm & esm);
+            if (m != 0 && L - rs <= (uint32_t)__popc(esm)) s_end = (int)(4 * it) + 31 - __clz(procm & esm);
             const uint32_t nib = procm & ~safem;
             unsafe_n += (uint32_t)__popc(nib);
             // location-map word (4 it) / 64 = 16 lanes x 4 candidate bits: each half is the
@@ -2294,9 +2349,13 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
             wm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
             wm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
             wm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0x141, 0xF, 0xF, false);   // row_half_mirror
-            running += tot;
-            if (running >= L) live = false;
-        } else if (SS_LOCKSTEP && (k % SS_LOCKSTEP) == SS_LOCKSTEP - 1) {
+            if constexpr (CHAIN) {
+                if (last != k) wm = 0u;        // past `end`: no map word (stores go to the sink)
+            } else {
+                running += tot;
+                if (running >= L) live = false;
+            }
+        } else if (!CHAIN && SS_LOCKSTEP && (k % SS_LOCKSTEP) == SS_LOCKSTEP - 1) {
             // past `end` (out of place) the chunk is a plain copy: not classified (capacity
             // stays a lower bound, CODEC_PEE_PARTIAL, as on the look-back path).  Without a
             // barrier the oldest waves (scheduled first) run ahead and finish, and the youngest
@@ -2306,7 +2365,8 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
         }
         // stores, unconditional (lanes 0 / 8 of a DPP row store the map word's low / high half)
         const uint32_t wix = (4 * it) >> 6;
-        *(ok && (!INPLACE || was_live) && (lane & 7) == 0 && (int)wix < lmw
+        const bool map_live = CHAIN ? (was_live && last == k) : was_live;
+        *(ok && (!INPLACE || map_live) && (lane & 7) == 0 && (int)wix < lmw
               ? reinterpret_cast<uint32_t*>(lm + wix) + ((lane >> 3) & 1)
               : reinterpret_cast<uint32_t*>(sink_w)) = wm;
         if (INPLACE) {
@@ -2347,6 +2407,14 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
     if (b == 0)
         for (int i = tid; i < SS_TRACE_N; i += SS_THREADS) g_ss_trace[i] = ss_trace[i];
 #endif
+    if constexpr (CHAIN) {
+        // every wave processed the chunk holding `end` (or the last chunk): wave 0's `last` is
+        // it, and the count through it is the start of that chunk plus its 16 published words
+        if (tid == 0 && last >= 0) {
+            running = run_at;
+            for (int w = 0; w < 16; ++w) running += agg[last & 3][w] & 0xFFFFu;
+        }
+    }
     if (tid == 0) {
         uint32_t un = 0, re = 0;
         for (int w = 0; w < 16; ++w) { un += red[0][w]; re += red[1][w]; }
@@ -3339,9 +3407,16 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
             static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, tps, \
             reinterpret_cast<const u64*>(payload), P->payload_words, meta, reinterpret_cast<u64*>(lm), P->lm_words, \
             static_cast<char*>(workspace) + L.sink, 0, nullptr)
+        // chained wave scan instead of the chunk barrier (round 5; CODEC_PEE_SS_CHAIN)
+        const bool chain = knob("CODEC_PEE_SS_CHAIN", 0) != 0;
+#define PES1C(TT, NTV) hipLaunchKernelGGL((k_pee_embed_ss<TT, NTV, true, 1, true, false, true>), dim3((unsigned)P->B), dim3(SS_THREADS), 0, st, \
+            static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, tps, \
+            reinterpret_cast<const u64*>(payload), P->payload_words, meta, reinterpret_cast<u64*>(lm), P->lm_words, \
+            static_cast<char*>(workspace) + L.sink, 0, nullptr)
         if (P->bytes == 2) {
             if (inplace) {
                 if (ss_d == 2 && nt) PES1D(uint16_t, true, true, 2);
+                else if (ss_d == 1 && nt && chain) PES1C(uint16_t, true);
                 else if (ss_d == 1 && nt) PES1D(uint16_t, true, true, 1);
                 else if (nt) PES(uint16_t, true, true); else PES(uint16_t, false, true);
             }
@@ -3353,6 +3428,7 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
 #undef PES
 #undef PES1
 #undef PES1D
+#undef PES1C
         LAUNCH_CHECK("k_pee_embed_ss");
         if ((P->H & 1) && !inplace) HIP_TRY(pee_copy_last_rows(P, cover, stego, st));
         return 0;
@@ -3414,7 +3490,7 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
         dim3 grid((ntiles + per - 1) / per, P->B);
         if (vec) {
             const long long tot = (long long)ntiles * P->B;
-            long long gw = knob("CODEC_PEE_SCAN_GS_WGS", 32768);   // tools/archive/tune_pee.py
+            long long gw = knob("CODEC_PEE_SCAN_GS_WGS", 32768);   // tools/tune_pee.py
             if (gw > (tot + 3) / 4) gw = (tot + 3) / 4;
             if (gw < 1) gw = 1;
 #define PSCAN(TT, NTV) hipLaunchKernelGGL((k_pee_scan<TT, NTV>), dim3((unsigned)gw), dim3(256), 0, st, static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, cnt, L.ntiles_max, P->B, tps)

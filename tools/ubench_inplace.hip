@@ -81,6 +81,94 @@ __global__ __launch_bounds__(NT) void inplace_stream(unsigned short* img, int nc
     if (acc == 0xFFFFFFFFu) sink[0] = acc + pad[threadIdx.x & 7];
 }
 
+// round 5: the embed's per-chunk scan barrier replaced by a chained
+// wave scan -- per chunk every wave publishes its count in LDS (tagged with the chunk), then
+// waits only for the LOWER waves' counts of this chunk and every wave's count of the previous
+// chunk (the running total), read in one LDS load per lane and summed with DPP row scans.
+// PAIR: the barrier kept, but one per two chunks (two chunks classified between scans).
+__device__ __forceinline__ unsigned chain_tag(int k) { return ((unsigned)(k & 0x7FFF) | 0x8000u) << 16; }
+template <int D, int VALU, bool EARLY, bool CHAIN, bool PAIR>
+__global__ __launch_bounds__(NT) void inplace_chain(unsigned short* img, int nchunk, unsigned* sink) {
+    __shared__ unsigned pad[21 * 1024 - 64];
+    __shared__ unsigned agg[4][16];
+    const size_t npx = (size_t)H * W;
+    unsigned short* s = img + blockIdx.x * npx;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (threadIdx.x == 0) pad[0] = 0;
+    if (threadIdx.x < 64) agg[threadIdx.x >> 4][threadIdx.x & 15] = 0u;
+    __syncthreads();
+    v4u r0[D], r1[D];
+    unsigned ro[D];
+    unsigned acc = 0, running = 0;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const unsigned it = d * NT + threadIdx.x;
+        const unsigned r = it / CR, c = it - r * CR;
+        ro[d] = 2u * r * W + 8u * c;
+        r0[d] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(s + ro[d]));
+        r1[d] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(s + ro[d] + W));
+    }
+    const int nfull = nchunk / D * D;
+    for (int k0 = 0; k0 < nfull; k0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int k = k0 + d;
+            v4u a = r0[d], b = r1[d];
+            asm volatile("" ::"v"(a.x), "v"(b.x));
+            const unsigned so = ro[d];
+            if (EARLY) {
+                const unsigned it = (unsigned)(k + D) * NT + threadIdx.x;
+                const unsigned kk = k + D < nchunk ? it : threadIdx.x;
+                const unsigned r = kk / CR, c = kk - r * CR;
+                ro[d] = 2u * r * W + 8u * c;
+                r0[d] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(s + ro[d]));
+                r1[d] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(s + ro[d] + W));
+            }
+            unsigned x = a.x ^ b.y;
+#pragma unroll
+            for (int q = 0; q < VALU; ++q) x = (x * 0x9E37u + (b.z >> (q & 7))) ^ a.w;
+            const unsigned n = x & 3u;
+            const unsigned wt = (unsigned)__popcll(__ballot(n & 1u)) + 2u * (unsigned)__popcll(__ballot(n & 2u));
+            if (CHAIN) {
+                if (lane == 0)
+                    __hip_atomic_store(&agg[k & 3][wv], chain_tag(k) | wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const bool prev = lane < 16 && k > 0, cur = lane >= 16 && lane < 16 + wv;
+                unsigned* slot = prev ? &agg[(k - 1) & 3][lane] : &agg[k & 3][(lane - 16) & 15];
+                const unsigned want = prev ? chain_tag(k - 1) : chain_tag(k);
+                unsigned v = 0;
+                for (;;) {
+                    v = (prev || cur) ? __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : want;
+                    if (!__ballot((v & 0xFFFF0000u) != want)) break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                int y = (prev || cur) ? (int)(v & 0xFFFFu) : 0;
+                y += __builtin_amdgcn_update_dpp(0, y, 0x111, 0xF, 0xF, true);
+                y += __builtin_amdgcn_update_dpp(0, y, 0x112, 0xF, 0xF, true);
+                y += __builtin_amdgcn_update_dpp(0, y, 0x114, 0xF, 0xF, true);
+                y += __builtin_amdgcn_update_dpp(0, y, 0x118, 0xF, 0xF, true);
+                running += (unsigned)__builtin_amdgcn_readlane(y, 15);
+                const unsigned pre = wv ? (unsigned)__builtin_amdgcn_readlane(y, 15 + wv) : 0u;
+                acc += running + pre;
+            } else if (!PAIR || (k & 1)) {
+                lds_barrier();
+                acc += wt;
+            }
+            acc += x;
+            b.x ^= (acc & 0u);
+            __builtin_nontemporal_store(b, reinterpret_cast<v4u*>(s + so + W));
+            if (!EARLY) {
+                const unsigned it = (unsigned)(k + D) * NT + threadIdx.x;
+                const unsigned kk = k + D < nchunk ? it : threadIdx.x;
+                const unsigned r = kk / CR, c = kk - r * CR;
+                ro[d] = 2u * r * W + 8u * c;
+                r0[d] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(s + ro[d]));
+                r1[d] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(s + ro[d] + W));
+            }
+        }
+    }
+    if (acc == 0xFFFFFFFFu) sink[0] = acc + pad[threadIdx.x & 7];
+}
+
 // 4 workgroups of 256 threads per slice, each a contiguous quarter of the slice's chunks
 template <int D>
 __global__ __launch_bounds__(256) void inplace_quarters(unsigned short* img, int nchunk, unsigned* sink) {
@@ -130,7 +218,7 @@ int main() {
     CK(hipEventCreate(&e1));
     const double algo = (double)B * NCHUNK * NT * 48.0;   // 32 B read + 16 B written per item
     for (int pass = 0; pass < 2; ++pass) {
-        for (int variant = 0; variant < 19; ++variant) {
+        for (int variant = 0; variant < 27; ++variant) {
             const char* name = "";
             float sum = 0.f, best = 1e9f;
             const int reps = 20;
@@ -156,6 +244,14 @@ int main() {
                 case 16: name = "early ring 2 +barrier"; inplace_stream<2, true, 0, true><<<B, NT>>>(img, NCHUNK, sink); break;
                 case 17: name = "early ring 1 +barrier +valu 48"; inplace_stream<1, true, 48, true><<<B, NT>>>(img, NCHUNK, sink); break;
                 case 18: name = "early ring 4 +barrier +valu 48"; inplace_stream<4, true, 48, true><<<B, NT>>>(img, NCHUNK, sink); break;
+                case 19: name = "early ring 1 +chain +valu 48"; inplace_chain<1, 48, true, true, false><<<B, NT>>>(img, NCHUNK, sink); break;
+                case 20: name = "early ring 2 +chain +valu 48"; inplace_chain<2, 48, true, true, false><<<B, NT>>>(img, NCHUNK, sink); break;
+                case 21: name = "ring 2 +chain +valu 48"; inplace_chain<2, 48, false, true, false><<<B, NT>>>(img, NCHUNK, sink); break;
+                case 22: name = "early ring 1 +chain"; inplace_chain<1, 0, true, true, false><<<B, NT>>>(img, NCHUNK, sink); break;
+                case 23: name = "early ring 2 +pair +valu 48"; inplace_chain<2, 48, true, false, true><<<B, NT>>>(img, NCHUNK, sink); break;
+                case 24: name = "early ring 1 +bar2 +valu 48"; inplace_chain<1, 48, true, false, false><<<B, NT>>>(img, NCHUNK, sink); break;
+                case 25: name = "early ring 2 +chain"; inplace_chain<2, 0, true, true, false><<<B, NT>>>(img, NCHUNK, sink); break;
+                case 26: name = "early ring 4 +pair +valu 48"; inplace_chain<4, 48, true, false, true><<<B, NT>>>(img, NCHUNK, sink); break;
                 }
                 CK(hipGetLastError());
                 CK(hipEventRecord(e1, 0));
