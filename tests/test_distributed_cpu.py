@@ -237,3 +237,45 @@ def test_exchanges_gloo_more_ranks(world, n_slices):
             if p.is_alive():
                 p.kill()
     assert all(ok for _r, ok in res), res
+
+
+def _ranks_worker(rank, world, port, same_device, q):
+    """bench.gather_rank_records over gloo: every rank gets every record in rank order; with
+    the RCCL check on, two ranks naming one (host, PCI) device is an error."""
+    import sys
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    rec = {"rank": rank, "host": "h", "pci": "0000:%02x:00" % (0 if same_device else rank), "ms_per_step": 1.0 + rank}
+    out = bench.gather_rank_records(torch, dist, world, rec, "gloo")
+    ok = [r["rank"] for r in out] == list(range(world)) and out[rank] == rec
+    try:
+        bench.gather_rank_records(torch, dist, world, rec, "nccl")
+        ok &= not same_device
+    except RuntimeError as e:
+        ok &= same_device and "distinct devices" in str(e)
+    q.put((rank, bool(ok)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("same_device", [False, True])
+def test_rank_records_gathered_and_checked(same_device):
+    """the per-rank records of the N > 1 bench line arrive in rank order,
+    and over RCCL a shared device is refused."""
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ranks_worker, args=(r, world, port, same_device, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=120) for _ in procs]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(ok for _r, ok in res), res
