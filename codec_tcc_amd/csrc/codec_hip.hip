@@ -806,8 +806,7 @@ template <typename T, int SB, bool NT, bool STORE, int DIAG = 0, bool PIPE = tru
 __device__ __forceinline__ void scan_rows_body(ScanRowsSmem<T>& SS, const T* __restrict__ cover, T* __restrict__ stego,
                                                int H, int W, int bands_per_wg,
                                                uint32_t* __restrict__ ghist_all,
-                                               u64* __restrict__ gkey, uint32_t* __restrict__ gor,
-                                               long long store_lim = 0x7FFFFFFFFFFFFFFFLL) {
+                                               u64* __restrict__ gkey, uint32_t* __restrict__ gor) {
     typedef typename Vec8<T>::type V;
     constexpr int G = SB / 8;                 // lanes (vectors) per block row segment
     constexpr int LG = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : 3;
@@ -881,14 +880,10 @@ __device__ __forceinline__ void scan_rows_body(ScanRowsSmem<T>& SS, const T* __r
             if (c >= CR) { c -= CR; ++r; }
         }
         if constexpr (STORE) {
-            // store_lim (k_scan_decide's split copy; a multiple of the step): vectors from there
-            // on are copied by the decision's idle waves instead (uniform per iteration)
-            if (base < store_lim) {
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const long long i = base + (long long)u * NT_ + threadIdx.x;
-                    if (whole || i < nvec) stv<NT>(d + i, v[u]);
-                }
+            for (int u = 0; u < U; ++u) {
+                const long long i = base + (long long)u * NT_ + threadIdx.x;
+                if (whole || i < nvec) stv<NT>(d + i, v[u]);
             }
         }
         // block LSB counts: a lane's U vectors often sit in one block (W = 2048: rows q,
@@ -1273,7 +1268,6 @@ struct DecideSmem {
     int32_t lay_sh[sizeof(codec_layout) / 4];
     SliceWin Wsh;
     int seg_end[16], seg_p[16], seg_q0[16], seg_s0[16];
-    int copy_next, rdone;   // fused split copy: next unit to claim; pair leaders done this decision
 };
 
 // what the fused kernel hands the decision: the slice's OR word and block key, and -- when the
@@ -1284,9 +1278,6 @@ struct FusedScan {
     uint32_t orv;
     u64 key;
     bool lds_ok;
-    // split copy (round 5): the scan stored the slice's vectors [0, copy_from) of nvec; the rest
-    // of the cover -> stego copy is done by the decision (decide_body's copy_rest)
-    long long copy_from, nvec;
 };
 
 template <typename T, bool EMBED>
@@ -1345,38 +1336,6 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     const bool pay_in_lds = EMBED && E.pw <= kPaySh;
     if (EMBED && pay_in_lds && role == 0)
         for (int w = t; w < E.pw; w += 1024) pay_sh[w] = E.payload[(size_t)b * E.pw + w];
-    // ---- fused split copy (round 5): the vectors [copy_from, nvec) of the
-    // slice's cover -> stego copy that the scan left out, claimed in units of 512 vectors (8 KiB)
-    // by one wave at a time: first by the waves the paired MI round leaves idle, while the round
-    // runs (stop_at: the round's pair leaders have all reported), then by every wave before the
-    // fused embed (which must follow the copy: it rewrites window pixels of the same stego).
-    const bool split_copy = EMBED && fz != nullptr && fz->copy_from < fz->nvec;
-    if (split_copy && t == 0) { S.copy_next = 0; S.rdone = 0; }
-    auto copy_rest = [&](const int* stop_ctr, int stop_at) {   // wave-uniform
-        typedef typename Vec8<T>::type V;
-        const int lane = t & 63;
-        const V* cs = reinterpret_cast<const V*>(static_cast<const T*>(E.cover) + (size_t)b * npx);
-        V* ss = reinterpret_cast<V*>(static_cast<T*>(E.stego) + (size_t)b * npx);
-        for (;;) {
-            if (stop_ctr && __hip_atomic_load(stop_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= stop_at) break;
-            int u = 0;
-            if (lane == 0) u = atomicAdd(&S.copy_next, 1);
-            u = __shfl(u, 0, 64);
-            const long long v0c = fz->copy_from + (long long)u * 512;
-            if (v0c >= fz->nvec) break;
-            V x[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const long long i = v0c + k * 64 + lane;
-                if (i < fz->nvec) x[k] = ldv<true>(cs + i);
-            }
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const long long i = v0c + k * 64 + lane;
-                if (i < fz->nvec) stv<true>(ss + i, x[k]);
-            }
-        }
-    };
     // ---- bins that can be non-zero: [0, Rp), Rp = next power of two above OR(pixels)
     const uint32_t orv = fz ? fz->orv : gor[b];
     int Rp = orv ? (1 << (32 - __clz((int)orv))) : 1;
@@ -1744,7 +1703,6 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
                 hx_sh[lane] = (pp != 0 && (long long)pp != npx) ? -(plogp(lut, (uint32_t)(npx - pp), Nd) + plogp(lut, pp, Nd)) : 0.0;
             }
             int base = 0;
-            int rexp = 0;   // pair leaders expected to have reported before this round
             for (int i0 = 0; i0 < nb; i0 += rp2) {
                 const int i = i0 + k;
                 if (wv < 2 * rp2 && i < nb) {
@@ -1819,15 +1777,9 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
                             if (i0 == 0) WVTS(wv);
                         }
                         if (lane == 0) hxy_sh[k] = hxy;
-                        if (split_copy && lane == 0) atomicAdd(&S.rdone, 1);   // this pair is done
                     }
                     base += 3;
-                } else if (split_copy) {
-                    // a wave without a plane this round streams part of the split copy until
-                    // every pair of the round has reported (leaders counted cumulatively)
-                    copy_rest(&S.rdone, rexp + min(rp2, nb - i0));
                 }
-                if (split_copy) rexp += min(rp2, nb - i0);
                 __syncthreads();
                 if (t == 0) {
                     Hy = hy_sh;
@@ -2092,7 +2044,6 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     }
     if constexpr (EMBED) {
         const SliceWin& W = Wsh;
-        if (split_copy) copy_rest(nullptr, 0);   // what the idle waves left: every wave, then the barrier
         __syncthreads();
         DTS(10);
         const T* cv = static_cast<const T*>(E.cover) + (size_t)b * npx;
@@ -2210,23 +2161,19 @@ __global__ __launch_bounds__(1024) void k_scan_decide(const T* __restrict__ cove
                                                       int exact_cap, int exact_edge_only, const double* __restrict__ lut,
                                                       long long lut_len, const codec_layout* __restrict__ table,
                                                       const int32_t* __restrict__ slice_class,
-                                                      codec_slice_meta* __restrict__ meta_all, EmbedArgs E,
-                                                      long long copy_lim) {
+                                                      codec_slice_meta* __restrict__ meta_all, EmbedArgs E) {
     union FusedSmem {
         ScanRowsSmem<T> s;
         DecideSmem<T, true> d;
     };
     __shared__ FusedSmem U;
     const int b = blockIdx.y;
-    scan_rows_body<T, SB, NT, true, 0, true, 4, true>(U.s, cover, stego, P.H, P.W, bands_per_wg, ghist_all, gkey, gor,
-                                                       copy_lim);
+    scan_rows_body<T, SB, NT, true, 0, true, 4, true>(U.s, cover, stego, P.H, P.W, bands_per_wg, ghist_all, gkey, gor);
     // scan_rows_body ended with a barrier after its last LDS write (the block key)
     FusedScan fz;
     fz.lds = U.s.lds;
     fz.orv = U.s.wor;
     fz.key = U.s.wkey;
-    fz.nvec = (long long)P.H * (P.W / 8);
-    fz.copy_from = min(copy_lim, fz.nvec);
     const int Rp = fz.orv ? (1 << (32 - __clz((int)fz.orv))) : 1;
     fz.lds_ok = sizeof(T) == 2 && U.s.wrap == 0u && Rp <= 4096;
     if (!fz.lds_ok) {   // uniform: the global histogram path (wrap fix-ups are already there)
@@ -3249,14 +3196,9 @@ static int plan_impl(const codec_params* P, const void* cover, void* stego, cons
                           (knob("CODEC_DECIDE_PAIRS", 1) ? 0 : 4);
             ProfScope prof(st, CODEC_K_SCAN_DECIDE);
             const bool nt = knob("CODEC_NT", 1) != 0;
-            // split copy (round 5): the scan stores the first CODEC_SCAN_DECIDE_COPY eighths of each
-            // slice's stego (a multiple of the scan's 4096-vector step), the decision the rest
-            const long long nvec = (long long)P->H * (P->W / 8);
-            const long long eighths = std::min(8LL, std::max(0LL, knob("CODEC_SCAN_DECIDE_COPY", 8)));
-            const long long copy_lim = eighths >= 8 ? nvec : (nvec * eighths / 8) / 4096 * 4096;
 #define SD(NTV) hipLaunchKernelGGL((k_scan_decide<uint16_t, 16, NTV>), dim3(1, P->B), dim3(1024), 0, st, \
                 static_cast<const uint16_t*>(cover), static_cast<uint16_t*>(stego), nbands, Pv, hist, orv, terms, keys, \
-                exact, L.exact_cap, 1, log2_lut, (long long)lut_len, table, slice_class, meta, *E, copy_lim)
+                exact, L.exact_cap, 1, log2_lut, (long long)lut_len, table, slice_class, meta, *E)
             if (nt) SD(true); else SD(false);
 #undef SD
             const hipError_t ef = hipGetLastError();

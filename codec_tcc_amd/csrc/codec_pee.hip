@@ -2056,47 +2056,6 @@ __device__ __forceinline__ void ss_scan(uint32_t n, uint32_t (*wtot)[16], int pa
     *wbase = wb;
 }
 
-// Chained wave scan (round 5; in-place embed): the chunk's one workgroup
-// barrier replaced by per-wave LDS words.  Chunk k: every wave publishes its count of
-// expandable candidates in agg[k % 4][wave], tagged with k, then waits only for the words it
-// needs -- the LOWER waves' of chunk k (its rank prefix inside the chunk) and every wave's of
-// chunk k - 1 (the running count: chunk k's start) -- read with one LDS load per lane and summed
-// by DPP row scans (lanes 0-15: chunk k - 1, lanes 16-31: chunk k).  A wave never waits for a
-// higher wave of its own chunk, so the fast waves run ahead instead of idling at a barrier;
-// every wave publishes before it waits, so nothing can deadlock, and a wave is never more than
-// two chunks ahead of another (chunk k needs all of k - 1), so four slots cannot be overwritten
-// while still read.  Same ranks as ss_scan_small, one chunk later for the running total.
-__device__ __forceinline__ uint32_t chain_tag(int k) { return ((uint32_t)(k & 0x7FFF) | 0x8000u) << 16; }
-// The wait is bounded (2^22 polls, ~0.2 s): by the argument above it always ends, but a wave
-// that ever gave up sets *stuck, and the kernel flags its slice instead of hanging the GPU.
-#define SS_CHAIN_SPIN_MAX (1u << 22)
-__device__ __forceinline__ void ss_chain_scan(uint32_t wt, uint32_t (*agg)[16], int k, int wv, int lane,
-                                              uint32_t* tot_prev, uint32_t* pre, bool* stuck) {
-    // the wave's earlier LDS writes (the extract's payload-bit ORs of chunk k - 1) complete
-    // before its word of chunk k is visible: "published chunk k" implies "done with k - 1"
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0)
-        __hip_atomic_store(&agg[k & 3][wv], chain_tag(k) | wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const bool prev = lane < 16 && k > 0;
-    const bool cur = lane >= 16 && lane < 16 + wv;
-    uint32_t* slot = prev ? &agg[(k - 1) & 3][lane & 15] : &agg[k & 3][lane & 15];
-    const uint32_t want = prev ? chain_tag(k - 1) : chain_tag(k);
-    uint32_t v;
-    for (uint32_t spins = 0;; ++spins) {   // wave-uniform exit
-        v = (prev || cur) ? __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : want;
-        if (!__ballot((v & 0xFFFF0000u) != want)) break;
-        if (spins >= SS_CHAIN_SPIN_MAX) { *stuck = true; break; }
-        __builtin_amdgcn_s_sleep(1);
-    }
-    int y = (prev || cur) ? (int)(v & 0xFFFFu) : 0;
-    y += __builtin_amdgcn_update_dpp(0, y, 0x111, 0xF, 0xF, true);   // row_shr:1 (lane 0 of a row reads 0)
-    y += __builtin_amdgcn_update_dpp(0, y, 0x112, 0xF, 0xF, true);   // row_shr:2
-    y += __builtin_amdgcn_update_dpp(0, y, 0x114, 0xF, 0xF, true);   // row_shr:4
-    y += __builtin_amdgcn_update_dpp(0, y, 0x118, 0xF, 0xF, true);   // row_shr:8
-    *tot_prev = (uint32_t)__builtin_amdgcn_readlane(y, 15);
-    *pre = wv ? (uint32_t)__builtin_amdgcn_readlane(y, 15 + wv) : 0u;
-}
-
 // counters of the fused capacity phase (AUTO): the top tmax * 1024 words of the pad, below
 // its last word; the payload (PAY_LDS) sits at the bottom
 #define SS_AUTO_CNT_BASE(tmax) (SS_PAD_WORDS - 1 - (tmax) * SS_THREADS)
@@ -2107,7 +2066,7 @@ __device__ __forceinline__ void ss_chain_scan(uint32_t wt, uint32_t (*agg)[16], 
 // lane-private LDS counters, then takes the smallest T <= tmax whose capacity holds the
 // slice's payload (pee_select_slice's rule).  The embed that follows re-reads the slice from
 // the MALL (C3: 134 MB batch); no second launch, no global histogram, no arrival counter.
-template <typename T, bool NT, bool INPLACE, int D, bool PAY_LDS, bool AUTO = false, bool CHAIN = false>
+template <typename T, bool NT, bool INPLACE, int D, bool PAY_LDS, bool AUTO = false>
 __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict__ cover, T* stego, int H, int W, int T0,
                                                              int maxval, const int32_t* __restrict__ lengths,
                                                              const int32_t* __restrict__ tps,
@@ -2116,11 +2075,9 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
                                                              u64* __restrict__ lm_all, int lmw, char* __restrict__ sink,
                                                              int tmax, int32_t* __restrict__ t_out) {
     typedef typename Vec8<T>::type V;
-    static_assert(!CHAIN || (INPLACE && D == 1 && PAY_LDS && !AUTO), "the chained scan serves the in-place early ring");
     __shared__ uint32_t ss_pad[SS_PAD_WORDS];
     __shared__ uint32_t wtot[2][16];
     __shared__ uint32_t red[2][16];
-    __shared__ uint32_t agg[CHAIN ? 4 : 1][16];   // CHAIN: tagged per-wave counts, ss_chain_scan
     __shared__ int s_end;
     __shared__ uint32_t s_bins[AUTO ? PEE_TMAX_MAX : 1];
     __shared__ int s_T;
@@ -2229,15 +2186,11 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
     if (PAY_LDS) {   // the payload in LDS once: no dependent global round trip per chunk
         const int nw = min(pw, (int)((L + 63u) >> 6));
         for (int w = tid; w < nw; w += SS_THREADS) pay[w] = payload[w];
-        if (CHAIN && tid < 64) agg[tid >> 4][tid & 15] = 0u;
         lds_barrier();
     }
     uint32_t running = 0, rest = 0, unsafe_n = 0;
     int par = 0, last = -1;
-    // uniform (CHAIN: per wave): the chunk holding bit L-1 may still be to come
-    bool live = L > 0;
-    uint32_t run_at = 0;   // CHAIN: running count at the start of chunk `last`
-    bool stuck = false;    // CHAIN: a bounded wait gave up (never expected; flags the slice)
+    bool live = L > 0;   // uniform: the chunk holding bit L-1 is still to come
 
     // one chunk, processed in the ring registers, then the ring slot is refilled.  D == 1
     // (EARLY): the chunk's data is taken into working registers and the slot refilled at
@@ -2288,25 +2241,9 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
             }
             if (!ok) esm = 0u;
             const uint32_t n = (uint32_t)__popc(esm);
+            last = k;
             uint32_t ex, tot, wb;
-            if constexpr (CHAIN) {
-                uint32_t wt, tprev, pre;
-                ex = wave_excl_small(n, &wt);
-                ss_chain_scan(wt, agg, k, wv, lane, &tprev, &pre, &stuck);
-                running += tprev;              // the start of chunk k
-                ex += pre;
-                wb = pre;
-                tot = 0u;                      // added at chunk k + 1
-                if (running >= L) esm = 0u;    // chunk k lies past `end` (m = 0 below: nothing moves)
-                else { last = k; run_at = running; }
-                // the next chunk is needed unless this wave's own inclusive prefix already reaches L
-                // (monotone in the wave index: the waves that stop are an upper range of them, so
-                // no wave waits on one that stopped)
-                live = running + pre + wt < L;
-            } else {
-                last = k;
-                ss_scan_small(n, wtot, par, &ex, &tot, &wb);
-            }
+            ss_scan_small(n, wtot, par, &ex, &tot, &wb);
             SS_STAMP(4 * k + 2);
             par ^= 1;
             // this lane's expandable candidates take ranks [rs, rs + n): their payload bits
@@ -2347,7 +2284,7 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
             touched = procm != 0;
             // the lane holding rank L-1 (1 <= L - rs <= n): `end` is its last processed
             // expandable candidate; one lane of the slice, once
-            if (m != 0 && L - rs <= (uint32_t)__popc(esm)) s_end = (int)(4 * it) + 31 - __clz(procm & esm);
+            if (m != 0 && L - rs <= n) s_end = (int)(4 * it) + 31 - __clz(procm & esm);
             const uint32_t nib = procm & ~safem;
             unsafe_n += (uint32_t)__popc(nib);
             // location-map word (4 it) / 64 = 16 lanes x 4 candidate bits: each half is the
@@ -2357,13 +2294,9 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
             wm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
             wm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
             wm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0x141, 0xF, 0xF, false);   // row_half_mirror
-            if constexpr (CHAIN) {
-                if (last != k) wm = 0u;        // past `end`: no map word (stores go to the sink)
-            } else {
-                running += tot;
-                if (running >= L) live = false;
-            }
-        } else if (!CHAIN && SS_LOCKSTEP && (k % SS_LOCKSTEP) == SS_LOCKSTEP - 1) {
+            running += tot;
+            if (running >= L) live = false;
+        } else if (SS_LOCKSTEP && (k % SS_LOCKSTEP) == SS_LOCKSTEP - 1) {
             // past `end` (out of place) the chunk is a plain copy: not classified (capacity
             // stays a lower bound, CODEC_PEE_PARTIAL, as on the look-back path).  Without a
             // barrier the oldest waves (scheduled first) run ahead and finish, and the youngest
@@ -2373,8 +2306,7 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
         }
         // stores, unconditional (lanes 0 / 8 of a DPP row store the map word's low / high half)
         const uint32_t wix = (4 * it) >> 6;
-        const bool map_live = CHAIN ? (was_live && last == k) : was_live;
-        *(ok && (!INPLACE || map_live) && (lane & 7) == 0 && (int)wix < lmw
+        *(ok && (!INPLACE || was_live) && (lane & 7) == 0 && (int)wix < lmw
               ? reinterpret_cast<uint32_t*>(lm + wix) + ((lane >> 3) & 1)
               : reinterpret_cast<uint32_t*>(sink_w)) = wm;
         if (INPLACE) {
@@ -2409,20 +2341,12 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
         unsafe_n += __shfl_xor(unsafe_n, o, 64);
         rest += __shfl_xor(rest, o, 64);
     }
-    if (lane == 0) { red[0][wv] = (CHAIN && stuck) ? 0xFFFFFFFFu : unsafe_n; red[1][wv] = rest; }
+    if (lane == 0) { red[0][wv] = unsafe_n; red[1][wv] = rest; }
     lds_barrier();
 #ifdef PEE_SS_TRACE
     if (b == 0)
         for (int i = tid; i < SS_TRACE_N; i += SS_THREADS) g_ss_trace[i] = ss_trace[i];
 #endif
-    if constexpr (CHAIN) {
-        // every wave processed the chunk holding `end` (or the last chunk): wave 0's `last` is
-        // it, and the count through it is the start of that chunk plus its 16 published words
-        if (tid == 0 && last >= 0) {
-            running = run_at;
-            for (int w = 0; w < 16; ++w) running += agg[last & 3][w] & 0xFFFFu;
-        }
-    }
     if (tid == 0) {
         uint32_t un = 0, re = 0;
         for (int w = 0; w < 16; ++w) { un += red[0][w]; re += red[1][w]; }
@@ -2437,11 +2361,6 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
         if (L == 0) { M->end = -1; M->tile_end = -1; M->status = 0; }
         else if (running < L) { M->end = nc - 1; M->tile_end = ntiles - 1; M->status = 1; }   // truncated
         else { M->end = s_end; M->tile_end = s_end / PEE_TILE; M->status = 0; }
-        if (CHAIN) {
-            bool any_stuck = false;
-            for (int w = 0; w < 16; ++w) any_stuck |= red[0][w] == 0xFFFFFFFFu;
-            if (any_stuck) M->status = CODEC_PEE_ELOOKBACK;   // not a valid stego: the host raises
-        }
     }
 }
 
@@ -2920,29 +2839,20 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
 }
 
 // EARLY: the ring slot is refilled as soon as its data is taken (before the chunk's barrier
-// and compute), as the in-place embed does with D = 1 (k_pee_embed_ss).
-// CHAIN (in place, early ring of one; round 5): ss_chain_scan instead of the chunk barrier.
-// The payload bits of chunk k are OR-ed into LDS slot k % 4 and written out by wave 0 two
-// chunks later: at chunk k + 2 wave 0 has seen every wave's word of chunk k + 1, published
-// after that wave's ORs of chunk k, so the slot is complete; wave 0 re-zeroes it before it
-// publishes chunk k + 3, and the ORs of chunk k + 4 wait for that word.  The carried partial
-// word stays with wave 0.  Every global store stays unconditional (sink-redirected).
-template <typename T, bool NT, bool INPLACE, int D, bool EARLY = false, bool CHAIN = false>
+// and compute), as the in-place embed does with D = 1 (k_pee_embed_ss)
+template <typename T, bool NT, bool INPLACE, int D, bool EARLY = false>
 __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restrict__ stego, T* cover, int H, int W,
                                                                const codec_pee_meta* __restrict__ meta_all,
                                                                const u64* __restrict__ lm_all, int lmw,
                                                                u64* __restrict__ payload_all, int pw,
                                                                uint32_t* __restrict__ lb_flag, char* __restrict__ sink) {
     typedef typename Vec8<T>::type V;
-    static_assert(!CHAIN || (INPLACE && D == 1 && EARLY), "the chained scan serves the in-place early ring");
     __shared__ uint32_t ss_pad[SS_PAD_WORDS];
     __shared__ uint32_t wtot[2][16];
-    __shared__ u64 pbuf[CHAIN ? 4 : 2][SS_THREADS * 4 / 64 + 2];
+    __shared__ u64 pbuf[2][SS_THREADS * 4 / 64 + 2];
     __shared__ u64 s_carry[2];
-    __shared__ uint32_t agg[CHAIN ? 4 : 1][16];
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
-    const int lane = tid & 63, wv = tid >> 6;
     const int CR = W / 8;
     const uint32_t items = (uint32_t)(H / 2) * (uint32_t)CR;
     const int nchunks = (int)((items + SS_THREADS - 1) / SS_THREADS);
@@ -2963,11 +2873,7 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
         ss_pad[SS_PAD_WORDS - 1] = 0u;
         if (b == 0) *lb_flag = 0u;   // codec_pee_extract_flag_offset: no look-back here, never set
     }
-    if (tid < SS_THREADS * 4 / 64 + 2)
-#pragma unroll
-        for (int i = 0; i < (CHAIN ? 4 : 2); ++i) pbuf[i][tid] = 0ull;
-    if (CHAIN && tid < 64) agg[tid >> 4][tid & 15] = 0u;
-    if (CHAIN) lds_barrier();
+    if (tid < SS_THREADS * 4 / 64 + 2) pbuf[0][tid] = pbuf[1][tid] = 0ull;
     V r0[D], r1[D];
     u64 rl[D];
     const uint32_t dq = SS_THREADS / (uint32_t)CR, dr = SS_THREADS % (uint32_t)CR;
@@ -3014,36 +2920,6 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
         if (tid == 0 && (p_hi & 63u) == 0u) s_carry[p_par] = 0ull;
     };
 
-    // CHAIN: chunk kk's words ([lo, hi) in rank space, slot kk % 4), written by wave 0 with two
-    // unconditional stores per lane (a chunk touches <= 66 words); other waves run the same
-    // code into the sink.  s_carry[0]: wave 0's partial word, carried from chunk to chunk.
-    auto emit_chain = [&](int kk, uint32_t lo, uint32_t hi, bool any) {
-        const bool w0 = wv == 0 && any;
-        const int nw = any ? (int)(((lo & 63u) + (hi - lo) + 63u) >> 6) : 0;
-        u64* pb = pbuf[kk & 3];
-        const u64 carry = s_carry[0];
-        u64 keep = 0ull;
-        bool kept = false;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int i = h * 64 + lane;
-            u64 wv64 = i < nw ? pb[i] : 0ull;
-            if (i == 0) wv64 |= carry;
-            const uint32_t a = (lo >> 6) + (uint32_t)i;
-            const bool full = i < nw && (a + 1u) * 64u <= hi;
-            if (i < nw && !full) { keep = wv64; kept = true; }
-            *(w0 && full && (int)a < pw ? payload + a : sink_w) = wv64;
-            if (w0 && i < nw) pb[i] = 0ull;
-        }
-        if (w0) {   // the new carry: the last word when partial, else zero
-            const u64 km = __ballot(kept);
-            const u64 kv = km ? __shfl(keep, (int)__builtin_ctzll(km), 64) : 0ull;
-            if (lane == 0) s_carry[0] = (hi & 63u) ? kv : 0ull;
-        }
-    };
-    uint32_t r_m1 = 0, r_m2 = 0;   // CHAIN: running count at the start of chunks k - 1, k - 2
-    bool stuck = false;            // CHAIN: a bounded wait gave up (sets the decode-side flag)
-
     auto refill = [&](int d) {   // branch-free; past chunk klast the last item's address, data unused
         const bool in = it_a < items_l;
         ro[d] = in ? ahead.o : off_last;
@@ -3085,23 +2961,9 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
             const uint32_t n = (uint32_t)__popc(innm);
             // pbuf[par] was last read (and re-zeroed below) by these same threads two chunks ago
             uint32_t ex, tot, wb;
-            if constexpr (CHAIN) {
-                uint32_t wt, tprev, pre;
-                ex = wave_excl_small(n, &wt);
-                ss_chain_scan(wt, agg, k, wv, lane, &tprev, &pre, &stuck);
-                running += tprev;                        // the start of chunk k
-                ex += pre;
-                wb = pre;
-                tot = 0u;
-                emit_chain(k - 2, r_m2, r_m1, k >= 2);   // complete: every wave published chunk k - 1
-                r_m2 = r_m1;
-                r_m1 = running;
-                par = k & 3;                             // this chunk's LDS slot
-            } else {
-                ss_scan_small(n, wtot, par, &ex, &tot, &wb);
-                if (pend) emit(&wout, &wabs, &wstore);          // the previous chunk's words
-                if (tid < SS_THREADS * 4 / 64 + 2 && pend) pbuf[p_par][tid] = 0ull;
-            }
+            ss_scan_small(n, wtot, par, &ex, &tot, &wb);
+            if (pend) emit(&wout, &wabs, &wstore);          // the previous chunk's words
+            if (tid < SS_THREADS * 4 / 64 + 2 && pend) pbuf[p_par][tid] = 0ull;
             // this lane's inner candidates take ranks [rs, rs + n): their bits form one <= 4-bit
             // field, OR-ed into at most two words of the chunk's LDS buffer
             const uint32_t rs = running + ex;
@@ -3124,19 +2986,17 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
                 atomicOr(&pb32[wi], field << sh);
                 if (sh > 28u && (field >> (32u - sh))) atomicOr(&pb32[wi + 1], field >> (32u - sh));
             }
-            if constexpr (!CHAIN) {
-                pend = true;
-                p_lo = running;
-                p_hi = running + tot;
-                p_par = par;
-                par ^= 1;
-                running += tot;
-            }
-        } else if (!CHAIN && SS_LOCKSTEP && (k % SS_LOCKSTEP) == SS_LOCKSTEP - 1) {
+            pend = true;
+            p_lo = running;
+            p_hi = running + tot;
+            p_par = par;
+            par ^= 1;
+            running += tot;
+        } else if (SS_LOCKSTEP && (k % SS_LOCKSTEP) == SS_LOCKSTEP - 1) {
             lds_barrier();   // copy chunks: keep the waves in step (see k_pee_embed_ss; 0.91 -> 0.78 ms)
         }
         // stores, unconditional (redirected to the sink when they must not land)
-        if constexpr (!CHAIN) *(wstore ? payload + wabs : sink_w) = wout;
+        *(wstore ? payload + wabs : sink_w) = wout;
         if (INPLACE) {
             stv<NT>(ok && actm ? reinterpret_cast<V*>(dst + o0 + W) : sink_v, v1);
         } else {
@@ -3156,19 +3016,7 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
         if (nfull + d < nproc) chunk(d, nfull + d);
     // the last chunk's words, its partial last word, then zeros to the end of the payload row
     lds_barrier();
-    if constexpr (CHAIN) {
-        // chunks K - 2 and K - 1 (K = nproc) are still in LDS; every wave is past them
-        const int K = nproc;
-        uint32_t tl = 0;
-        if (K >= 1)
-            for (int w = 0; w < 16; ++w) tl += agg[(K - 1) & 3][w] & 0xFFFFu;
-        emit_chain(K - 2, r_m2, r_m1, K >= 2);
-        emit_chain(K - 1, r_m1, r_m1 + tl, K >= 1);
-        running = K >= 1 ? r_m1 + tl : 0u;
-        if (stuck && lane == 0) atomicOr(lb_flag, 1u);   // codec_pee_extract_flag_offset: payload invalid
-        lds_barrier();
-        if (tid == 0 && (running & 63u) && (int)(running >> 6) < pw) payload[running >> 6] = s_carry[0];
-    } else if (pend) {
+    if (pend) {
         u64 wout = 0;
         bool wstore = false;
         uint32_t wabs = 0;
@@ -3491,16 +3339,9 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
             static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, tps, \
             reinterpret_cast<const u64*>(payload), P->payload_words, meta, reinterpret_cast<u64*>(lm), P->lm_words, \
             static_cast<char*>(workspace) + L.sink, 0, nullptr)
-        // chained wave scan instead of the chunk barrier (round 5; CODEC_PEE_SS_CHAIN)
-        const bool chain = knob("CODEC_PEE_SS_CHAIN", 0) != 0;
-#define PES1C(TT, NTV) hipLaunchKernelGGL((k_pee_embed_ss<TT, NTV, true, 1, true, false, true>), dim3((unsigned)P->B), dim3(SS_THREADS), 0, st, \
-            static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, tps, \
-            reinterpret_cast<const u64*>(payload), P->payload_words, meta, reinterpret_cast<u64*>(lm), P->lm_words, \
-            static_cast<char*>(workspace) + L.sink, 0, nullptr)
         if (P->bytes == 2) {
             if (inplace) {
                 if (ss_d == 2 && nt) PES1D(uint16_t, true, true, 2);
-                else if (ss_d == 1 && nt && chain) PES1C(uint16_t, true);
                 else if (ss_d == 1 && nt) PES1D(uint16_t, true, true, 1);
                 else if (nt) PES(uint16_t, true, true); else PES(uint16_t, false, true);
             }
@@ -3512,7 +3353,6 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
 #undef PES
 #undef PES1
 #undef PES1D
-#undef PES1C
         LAUNCH_CHECK("k_pee_embed_ss");
         if ((P->H & 1) && !inplace) HIP_TRY(pee_copy_last_rows(P, cover, stego, st));
         return 0;
@@ -3755,13 +3595,8 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
 #define PXSE(IP, DD) hipLaunchKernelGGL((k_pee_extract_ss<uint16_t, true, IP, DD, true>), dim3((unsigned)P->B), dim3(SS_THREADS), 0, st, \
             static_cast<const uint16_t*>(stego), static_cast<uint16_t*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm), \
             P->lm_words, reinterpret_cast<u64*>(payload_out), P->payload_words, ctl + 1, static_cast<char*>(workspace) + L.sink)
-        // in place: the chained wave scan instead of the chunk barrier (round 5; CODEC_PEE_SSX_CHAIN)
-        const bool xchain = knob("CODEC_PEE_SSX_CHAIN", 0) != 0;
-#define PXSC() hipLaunchKernelGGL((k_pee_extract_ss<uint16_t, true, true, 1, true, true>), dim3((unsigned)P->B), dim3(SS_THREADS), 0, st, \
-            static_cast<const uint16_t*>(stego), static_cast<uint16_t*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm), \
-            P->lm_words, reinterpret_cast<u64*>(payload_out), P->payload_words, ctl + 1, static_cast<char*>(workspace) + L.sink)
         if (P->bytes == 2 && nt && xe) {
-            if (inplace) { if (xde == 1 && xchain) PXSC(); else if (xde == 1) PXSE(true, 1); else if (xde == 2) PXSE(true, 2); else PXSE(true, 4); }
+            if (inplace) { if (xde == 1) PXSE(true, 1); else if (xde == 2) PXSE(true, 2); else PXSE(true, 4); }
             else { if (xde == 1) PXSE(false, 1); else if (xde == 2) PXSE(false, 2); else PXSE(false, 4); }
         } else if (P->bytes == 2 && nt && xd != 4) {
             if (inplace) { if (xd == 2) PXSD(uint16_t, true, true, 2); else PXSD(uint16_t, true, true, 6); }
@@ -3776,7 +3611,6 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
 #undef PXS
 #undef PXSD
 #undef PXSE
-#undef PXSC
         LAUNCH_CHECK("k_pee_extract_ss");
         if ((P->H & 1) && !inplace) HIP_TRY(pee_copy_last_rows(P, stego, cover_out, st));
         return 0;

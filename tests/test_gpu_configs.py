@@ -89,12 +89,7 @@ def _pee_batch_check(covers, sample, T=2, chars=1024):
     assert payload_equal(w2, packed[0], [len(p) for p in payloads])
 
 
-@pytest.mark.parametrize("copy8", ["8", "4", "0"])
-def test_c3_lsb_256x512(copy8, monkeypatch):
-    """C3's LSB step through k_scan_decide; copy8 = the eighths of each slice's stego the scan
-    stores (CODEC_SCAN_DECIDE_COPY; the decision's idle waves and then all of its waves copy
-    the rest before the fused embed)."""
-    monkeypatch.setenv("CODEC_SCAN_DECIDE_COPY", copy8)
+def test_c3_lsb_256x512():
     B, H, W = 256, 512, 512
     covers = _batch(B, H, W, seed=1000)
     msgs = [synth.payload(1024, 5000 + i) for i in range(B)]

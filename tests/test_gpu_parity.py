@@ -31,7 +31,7 @@ def _run_case(case):
     return codec, enc
 
 
-@pytest.fixture(params=["split", "waves", "block", "fused", "fused_split"])
+@pytest.fixture(params=["split", "waves", "block", "fused"])
 def decide_path(request, monkeypatch):
     """k_decide's split decision (default for small batches: one plane workgroup per MI
     plane), its one-workgroup wave-parallel MI path (CODEC_DECIDE_SPLIT=0; the default for
@@ -41,12 +41,8 @@ def decide_path(request, monkeypatch):
     decision and embed in one launch (k_scan_decide, CODEC_FUSED_DECIDE=2 forces it on these
     one-slice batches; cases it does not take -- uint8, other block sizes, edge blocks -- run
     the separate kernels)."""
-    if request.param in ("fused", "fused_split"):
+    if request.param == "fused":
         monkeypatch.setenv("CODEC_FUSED_DECIDE", "2")
-    if request.param == "fused_split":
-        # round 5: the scan stores only the first 3/8 of the stego (rounded down to its
-        # 4096-vector step: nothing at all on small slices) and the decision copies the rest
-        monkeypatch.setenv("CODEC_SCAN_DECIDE_COPY", "3")
     if request.param == "waves":
         monkeypatch.setenv("CODEC_DECIDE_SPLIT", "0")
     if request.param == "block":

@@ -82,8 +82,6 @@ PATHS = {"auto": {}, "onepass": {"CODEC_PEE_ONEPASS": "1"}, "twopass": {"CODEC_P
          # default stages it in LDS) and with the 4-deep ring in place (default 2)
          "slice_serial_gpay": {"CODEC_PEE_SS": "1", "CODEC_PEE_SS_PAYLDS": "0"},
          "slice_serial_d4": {"CODEC_PEE_SS": "1", "CODEC_PEE_SS_D": "4"},
-         # in place: the chained wave scan instead of the chunk barrier (round 5)
-         "slice_serial_chain": {"CODEC_PEE_SS": "1", "CODEC_PEE_SS_CHAIN": "1", "CODEC_PEE_SSX_CHAIN": "1"},
          # extract ring depths other than the defaults (2 out of place, 4 in place)
          "slice_serial_xd4": {"CODEC_PEE_SS": "1", "CODEC_PEE_SSX_D": "4"},
          "slice_serial_xd6": {"CODEC_PEE_SS": "1", "CODEC_PEE_SSX_D": "6"}}

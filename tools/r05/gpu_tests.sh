@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 5 development loop: the in-place access-pattern ubench, the GPU suite (the new
-# workspace / 8-rank / chained-scan tests included), a short bench, then the chained-scan A/B.
+# workspace / 8-rank tests included) and a short bench.
 # Test failures (pytest rc 1) do not stop the later steps; a timeout, abort or crash does.
 set -o pipefail
 mkdir -p gpurun_out/r05
@@ -14,7 +14,3 @@ echo "pytest rc $rc"; grep -E "FAILED|ERROR" gpurun_out/r05/pytest_gpu.log | hea
 [ $rc -le 1 ] || stop $rc pytest
 timeout -k 10 240 python -u bench.py --steps 10 --warmup 2 --cpu-seconds 0 > gpurun_out/r05/bench_quick.json 2> gpurun_out/r05/bench_quick.err; rc=$?
 echo "bench rc $rc"; [ $rc -eq 0 ] || stop $rc bench
-timeout -k 10 300 python tools/tune_pee.py --configs '[{}, {"CODEC_PEE_SS_CHAIN": "1"}, {"CODEC_PEE_SSX_CHAIN": "1"}, {"CODEC_PEE_SS_CHAIN": "1", "CODEC_PEE_SSX_CHAIN": "1"}]' --rounds 5 --modes ip > gpurun_out/r05/chain_ab.txt 2>&1; rc=$?
-echo "chain ab rc $rc"; tail -4 gpurun_out/r05/chain_ab.txt
-timeout -k 10 300 python tools/tune.py --batch 256 --size 512 --rounds 7 --steps 20 --configs '[{"CODEC_SCAN_DECIDE_COPY": "8"}, {"CODEC_SCAN_DECIDE_COPY": "6"}, {"CODEC_SCAN_DECIDE_COPY": "5"}, {"CODEC_SCAN_DECIDE_COPY": "4"}, {"CODEC_SCAN_DECIDE_COPY": "3"}, {"CODEC_SCAN_DECIDE_COPY": "2"}, {"CODEC_SCAN_DECIDE_COPY": "0"}]' > gpurun_out/r05/c3_split_ab.txt 2>&1; rc=$?
-echo "c3 split ab rc $rc"; cat gpurun_out/r05/c3_split_ab.txt
