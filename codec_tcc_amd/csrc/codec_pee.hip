@@ -1276,8 +1276,22 @@ __device__ unsigned long long g_lb_trace[LB_TRACE_SLOTS * 12];
 __device__ __forceinline__ int pee_sc_tag(int epoch) { return epoch % 63 + 1; }
 #define PEE_SKIP 0xFFFFFFFFu
 #define PEE_STOP 0xFFFFFFFEu
+// occupancy A/B (build-time, tools/r05/ab_occupancy.sh): minimum waves per SIMD for the
+// look-back passes.  Measured: more waves per CU are slower (embed1 at 4: 0.738 -> 0.741 ms,
+// extract1 at 5: 0.712 -> 0.733), and fewer (a dynamic-LDS pad) slower or equal
+// (profiles/r05/ab_occupancy.txt, ab_ldspad.txt): the defaults stay.
+#ifdef PEE_E1_WAVES
+#define PEE_E1_LB __launch_bounds__(256, PEE_E1_WAVES)
+#else
+#define PEE_E1_LB __launch_bounds__(256)
+#endif
+#ifdef PEE_X1_WAVES
+#define PEE_X1_LB __launch_bounds__(256, PEE_X1_WAVES)
+#else
+#define PEE_X1_LB __launch_bounds__(256)
+#endif
 template <typename T, bool NT, bool INPLACE, bool SC = false>
-__global__ __launch_bounds__(256) void k_pee_embed1(const T* __restrict__ cover, T* stego, int H, int W, int T0,
+__global__ PEE_E1_LB void k_pee_embed1(const T* __restrict__ cover, T* stego, int H, int W, int T0,
                                                     int maxval, const int32_t* __restrict__ lengths,
                                                     const u64* __restrict__ payload_all, int pw, int nchunks, int B,
                                                     u64* status_all, uint32_t* ctl, codec_pee_meta* meta_all,
@@ -1663,7 +1677,7 @@ struct PeeReadAhead {
 // extract: chunks up to the one holding `end` recover bits + pixels (look-back over the
 // inner-candidate counts); later chunks are a plain copy (out of place) or skipped.
 template <typename T, bool NT, bool INPLACE, bool SC = false>
-__global__ __launch_bounds__(256) void k_pee_extract1(const T* stego, T* cover, int H, int W,
+__global__ PEE_X1_LB void k_pee_extract1(const T* stego, T* cover, int H, int W,
                                                       const codec_pee_meta* __restrict__ meta_all,
                                                       const u64* __restrict__ lm_all, int lmw, int nchunks, int B,
                                                       u64* status_all, uint32_t* ctl, u64* __restrict__ payload_all,

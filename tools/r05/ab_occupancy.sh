@@ -1,4 +1,6 @@
 #!/bin/bash
+# needs the variant libraries first:
+#   bash tools/r05/build_variant.sh tools/r05/lib_w45.so -DPEE_E1_WAVES=4 -DPEE_X1_WAVES=5  (and lib_e4 / lib_x5)
 # occupancy A/B of the headline look-back passes: the in-tree library against variants built by
 # build_variant.sh with __launch_bounds__ minimum waves per SIMD (k_pee_embed1 4: 145 -> 128
 # VGPRs; k_pee_extract1 5: 107 -> 95), alternating processes on one box (tools/tune_pee.py)
