@@ -785,7 +785,9 @@ def launch_ranks(args) -> int:
     try:
         for r in range(n):
             env = dict(env0, RANK=str(r), LOCAL_RANK=str(r), GROUP_RANK="0")
-            procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else None, text=True,
+            # rank 0's stdout is piped (its JSON line is forwarded); the other ranks' stdout goes to
+            # stderr, so library chatter (gloo prints its peer count) never reaches stdout
+            procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr, text=True,
                                           preexec_fn=lambda: _die_with_parent(me)))
         sys.stderr.write("bench.py: rank pids " + " ".join(str(p.pid) for p in procs) + "\n")
         sys.stderr.flush()
