@@ -199,8 +199,16 @@ template <> struct Vec8<uint8_t> { typedef uint2 type; };
 // stream is what lifts a 2 GiB read+write pass from ~5.1 to ~5.9 TB/s, tools/ubench_stream.hip)
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+// cache-policy A/B (build-time, tools/r05/build_variant.sh): CODEC_PLAIN_LOADS / CODEC_PLAIN_STORES
+// turn every non-temporal 16-B / 8-B vector load / store into a plain one
+#ifndef CODEC_PLAIN_LOADS
+#define CODEC_PLAIN_LOADS 0
+#endif
+#ifndef CODEC_PLAIN_STORES
+#define CODEC_PLAIN_STORES 0
+#endif
 template <bool NT> __device__ __forceinline__ uint4 ldv(const uint4* p) {
-    if constexpr (NT) {
+    if constexpr (NT && !CODEC_PLAIN_LOADS) {
         const v4u x = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
         return make_uint4(x.x, x.y, x.z, x.w);
     } else {
@@ -208,7 +216,7 @@ template <bool NT> __device__ __forceinline__ uint4 ldv(const uint4* p) {
     }
 }
 template <bool NT> __device__ __forceinline__ uint2 ldv(const uint2* p) {
-    if constexpr (NT) {
+    if constexpr (NT && !CODEC_PLAIN_LOADS) {
         const v2u x = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(p));
         return make_uint2(x.x, x.y);
     } else {
@@ -216,7 +224,7 @@ template <bool NT> __device__ __forceinline__ uint2 ldv(const uint2* p) {
     }
 }
 template <bool NT> __device__ __forceinline__ void stv(uint4* p, const uint4& v) {
-    if constexpr (NT) {
+    if constexpr (NT && !CODEC_PLAIN_STORES) {
         v4u x = {v.x, v.y, v.z, v.w};
         __builtin_nontemporal_store(x, reinterpret_cast<v4u*>(p));
     } else {
@@ -224,7 +232,7 @@ template <bool NT> __device__ __forceinline__ void stv(uint4* p, const uint4& v)
     }
 }
 template <bool NT> __device__ __forceinline__ void stv(uint2* p, const uint2& v) {
-    if constexpr (NT) {
+    if constexpr (NT && !CODEC_PLAIN_STORES) {
         v2u x = {v.x, v.y};
         __builtin_nontemporal_store(x, reinterpret_cast<v2u*>(p));
     } else {

@@ -2080,7 +2080,10 @@ __device__ __forceinline__ void ss_scan(uint32_t n, uint32_t (*wtot)[16], int pa
 // lane-private LDS counters, then takes the smallest T <= tmax whose capacity holds the
 // slice's payload (pee_select_slice's rule).  The embed that follows re-reads the slice from
 // the MALL (C3: 134 MB batch); no second launch, no global histogram, no arrival counter.
-template <typename T, bool NT, bool INPLACE, int D, bool PAY_LDS, bool AUTO = false>
+// NTS: the stores' cache policy (default: the loads'); in place plain stores -- the candidate
+// rows go back into lines the chunk has just read -- beat non-temporal ones by 11 % (embed) and
+// 15 % (extract) at 256 x 2048^2 (profiles/r05/ab_policy.txt), out of place they lose
+template <typename T, bool NT, bool INPLACE, int D, bool PAY_LDS, bool AUTO = false, bool NTS = NT>
 __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict__ cover, T* stego, int H, int W, int T0,
                                                              int maxval, const int32_t* __restrict__ lengths,
                                                              const int32_t* __restrict__ tps,
@@ -2324,10 +2327,10 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_embed_ss(const T* __restrict
               ? reinterpret_cast<uint32_t*>(lm + wix) + ((lane >> 3) & 1)
               : reinterpret_cast<uint32_t*>(sink_w)) = wm;
         if (INPLACE) {
-            stv<NT>(ok && touched ? reinterpret_cast<V*>(dst + o0 + W) : sink_v, v1);
+            stv<NTS>(ok && touched ? reinterpret_cast<V*>(dst + o0 + W) : sink_v, v1);
         } else {
-            stv<NT>(ok ? reinterpret_cast<V*>(dst + o0) : sink_v, v0);
-            stv<NT>(ok ? reinterpret_cast<V*>(dst + o0 + W) : sink_v + 1, v1);
+            stv<NTS>(ok ? reinterpret_cast<V*>(dst + o0) : sink_v, v0);
+            stv<NTS>(ok ? reinterpret_cast<V*>(dst + o0 + W) : sink_v + 1, v1);
         }
         if constexpr (!EARLY) refill(d);
         SS_STAMP(4 * k + 3);
@@ -2854,7 +2857,7 @@ __global__ __launch_bounds__(NTH) void k_pee_embed_res(const uint16_t* __restric
 
 // EARLY: the ring slot is refilled as soon as its data is taken (before the chunk's barrier
 // and compute), as the in-place embed does with D = 1 (k_pee_embed_ss)
-template <typename T, bool NT, bool INPLACE, int D, bool EARLY = false>
+template <typename T, bool NT, bool INPLACE, int D, bool EARLY = false, bool NTS = NT>   // NTS: k_pee_embed_ss
 __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restrict__ stego, T* cover, int H, int W,
                                                                const codec_pee_meta* __restrict__ meta_all,
                                                                const u64* __restrict__ lm_all, int lmw,
@@ -3012,10 +3015,10 @@ __global__ __launch_bounds__(SS_THREADS) void k_pee_extract_ss(const T* __restri
         // stores, unconditional (redirected to the sink when they must not land)
         *(wstore ? payload + wabs : sink_w) = wout;
         if (INPLACE) {
-            stv<NT>(ok && actm ? reinterpret_cast<V*>(dst + o0 + W) : sink_v, v1);
+            stv<NTS>(ok && actm ? reinterpret_cast<V*>(dst + o0 + W) : sink_v, v1);
         } else {
-            stv<NT>(ok ? reinterpret_cast<V*>(dst + o0) : sink_v, v0);
-            stv<NT>(ok ? reinterpret_cast<V*>(dst + o0 + W) : sink_v + 1, v1);
+            stv<NTS>(ok ? reinterpret_cast<V*>(dst + o0) : sink_v, v0);
+            stv<NTS>(ok ? reinterpret_cast<V*>(dst + o0 + W) : sink_v + 1, v1);
         }
         if constexpr (!EARLY) refill(d);
     };
@@ -3353,10 +3356,22 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
             static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, lengths, tps, \
             reinterpret_cast<const u64*>(payload), P->payload_words, meta, reinterpret_cast<u64*>(lm), P->lm_words, \
             static_cast<char*>(workspace) + L.sink, 0, nullptr)
+        // in place, early ring of one: the load and store cache policies (CODEC_PEE_IP_NTL /
+        // CODEC_PEE_IP_NTS; default non-temporal loads, plain stores, profiles/r05/ab_policy.txt)
+        const bool ip_ntl = knob("CODEC_PEE_IP_NTL", 1) != 0, ip_nts = knob("CODEC_PEE_IP_NTS", 0) != 0;
+#define PES1P(NTL, NTSV) hipLaunchKernelGGL((k_pee_embed_ss<uint16_t, NTL, true, 1, true, false, NTSV>), dim3((unsigned)P->B), \
+            dim3(SS_THREADS), 0, st, static_cast<const uint16_t*>(cover), static_cast<uint16_t*>(stego), P->H, P->W, P->T, \
+            P->maxval, lengths, tps, reinterpret_cast<const u64*>(payload), P->payload_words, meta, reinterpret_cast<u64*>(lm), \
+            P->lm_words, static_cast<char*>(workspace) + L.sink, 0, nullptr)
         if (P->bytes == 2) {
             if (inplace) {
                 if (ss_d == 2 && nt) PES1D(uint16_t, true, true, 2);
-                else if (ss_d == 1 && nt) PES1D(uint16_t, true, true, 1);
+                else if (ss_d == 1 && nt) {
+                    if (ip_ntl && ip_nts) PES1P(true, true);
+                    else if (ip_ntl) PES1P(true, false);
+                    else if (ip_nts) PES1P(false, true);
+                    else PES1P(false, false);
+                }
                 else if (nt) PES(uint16_t, true, true); else PES(uint16_t, false, true);
             }
             else { if (nt) PES(uint16_t, true, false); else PES(uint16_t, false, false); }
@@ -3367,6 +3382,7 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
 #undef PES
 #undef PES1
 #undef PES1D
+#undef PES1P
         LAUNCH_CHECK("k_pee_embed_ss");
         if ((P->H & 1) && !inplace) HIP_TRY(pee_copy_last_rows(P, cover, stego, st));
         return 0;
@@ -3609,8 +3625,22 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
 #define PXSE(IP, DD) hipLaunchKernelGGL((k_pee_extract_ss<uint16_t, true, IP, DD, true>), dim3((unsigned)P->B), dim3(SS_THREADS), 0, st, \
             static_cast<const uint16_t*>(stego), static_cast<uint16_t*>(cover_out), P->H, P->W, meta, reinterpret_cast<const u64*>(lm), \
             P->lm_words, reinterpret_cast<u64*>(payload_out), P->payload_words, ctl + 1, static_cast<char*>(workspace) + L.sink)
+        // in place, early ring of one: cache policies as for the in-place embed (CODEC_PEE_IP_NTL / _NTS)
+        const bool xip_ntl = knob("CODEC_PEE_IP_NTL", 1) != 0, xip_nts = knob("CODEC_PEE_IP_NTS", 0) != 0;
+#define PXSP(NTL, NTSV) hipLaunchKernelGGL((k_pee_extract_ss<uint16_t, NTL, true, 1, true, NTSV>), dim3((unsigned)P->B), \
+            dim3(SS_THREADS), 0, st, static_cast<const uint16_t*>(stego), static_cast<uint16_t*>(cover_out), P->H, P->W, meta, \
+            reinterpret_cast<const u64*>(lm), P->lm_words, reinterpret_cast<u64*>(payload_out), P->payload_words, ctl + 1, \
+            static_cast<char*>(workspace) + L.sink)
         if (P->bytes == 2 && nt && xe) {
-            if (inplace) { if (xde == 1) PXSE(true, 1); else if (xde == 2) PXSE(true, 2); else PXSE(true, 4); }
+            if (inplace) {
+                if (xde == 1) {
+                    if (xip_ntl && xip_nts) PXSP(true, true);
+                    else if (xip_ntl) PXSP(true, false);
+                    else if (xip_nts) PXSP(false, true);
+                    else PXSP(false, false);
+                }
+                else if (xde == 2) PXSE(true, 2); else PXSE(true, 4);
+            }
             else { if (xde == 1) PXSE(false, 1); else if (xde == 2) PXSE(false, 2); else PXSE(false, 4); }
         } else if (P->bytes == 2 && nt && xd != 4) {
             if (inplace) { if (xd == 2) PXSD(uint16_t, true, true, 2); else PXSD(uint16_t, true, true, 6); }
@@ -3625,6 +3655,7 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
 #undef PXS
 #undef PXSD
 #undef PXSE
+#undef PXSP
         LAUNCH_CHECK("k_pee_extract_ss");
         if ((P->H & 1) && !inplace) HIP_TRY(pee_copy_last_rows(P, stego, cover_out, st));
         return 0;
