@@ -1322,7 +1322,8 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     DTS(0);
     if (role > 0) PTS(0);
     // the scan's block key, loaded now (used by the offset argmax after the decision)
-    const bool keyed = t == 0 && role == 0 && fast_blocks && P.fixed_offset < 0 && P.mode == CODEC_MODE_HYBRID;
+    // (thread 0, and wave 13's lane 0: the paired MI round finds the offset on that idle wave)
+    const bool keyed = (t == 0 || t == 832) && role == 0 && fast_blocks && P.fixed_offset < 0 && P.mode == CODEC_MODE_HYBRID;
     const u64 key0 = keyed ? (fz ? fz->key : gkey[b]) : 0ull;
     // the slice's layout class (its layout for s is loaded once s is known)
     constexpr int kLayW = (int)(sizeof(codec_layout) / 4);
@@ -1696,6 +1697,35 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
             const int k = wv >> 1, h = wv & 1;
             double* xbuf = vals + 512 + 64 * k;                        // wave 2k+1's slot sums (k < 5)
             const int gh = (ngrp + 1) / 2;                             // groups of the first half
+            // the start offset meanwhile (it does not depend on s), on idle wave 13 with wave
+            // shuffles only -- find_offset's block barriers and cross-wave pass stay off the
+            // path after the round (C3: ~2.9 us there); thread 0 picks it up after the rounds
+            if (wv == 13 && P.fixed_offset < 0 && P.mode == CODEC_MODE_HYBRID) {
+                double ws = -1.0;
+                int wi = 0x7FFFFFFF;
+                const int cnt = exact_count(P.H, P.W, sb, exact_edge_only);
+                for (int e = lane; e < cnt; e += 64) {
+                    int by, bx;
+                    exact_block(e, P.H, P.W, sb, exact_edge_only, &by, &bx);
+                    const double sc = exact[(size_t)b * exact_cap + e];
+                    const int ix = by * nbx + bx;
+                    if (sc > ws || (sc == ws && ix < wi)) { ws = sc; wi = ix; }
+                }
+                if (lane == 0 && fast_blocks && key0) {
+                    const uint32_t score = (uint32_t)(key0 >> 32);
+                    const int ix = (int)(0xFFFFFFFFu - (uint32_t)(key0 & 0xFFFFFFFFu));
+                    const double sc = (double)score / ((double)sb * sb * (double)sb * sb);
+                    if (sc > ws || (sc == ws && ix < wi)) { ws = sc; wi = ix; }
+                }
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) {
+                    const double os = __shfl_xor(ws, o, 64);
+                    const int oi = __shfl_xor(wi, o, 64);
+                    if (os > ws || (os == ws && oi < wi)) { ws = os; wi = oi; }
+                }
+                if (lane == 0) { best_sc[0] = ws; best_ix[0] = wi; }
+            }
+            offset_done = true;   // every thread (uniform): find_offset is not called below
             // H(X) of every plane meanwhile, on an idle wave (its two table loads stay off the
             // pairs' critical path); read by thread 0's walk after the round's barrier
             if (wv == 14 && lane < nb) {
@@ -1806,6 +1836,10 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
                 __syncthreads();
                 if (ctl_sh[0]) break;
             }
+        }
+        if (pair && t == 0 && P.fixed_offset < 0 && P.mode == CODEC_MODE_HYBRID) {   // wave 13's offset
+            bsc = best_sc[0];   // (ordered by the rounds' barriers)
+            bix = best_ix[0];
         }
         for (int i0 = 0; i0 < nb && !pair; i0 += rp) {
             const int i = i0 + wv;
