@@ -62,14 +62,37 @@ struct ProfScope {   // records a start event now and the end event at scope exi
 };
 
 // ------------------------------------------------------------------ block primitives
+// inclusive scan over the wave.  CODEC_WSCAN_DPP (default): each 16-lane row scanned by four
+// DPP row_shr adds (lanes shifted in from outside the row read 0), the rows' totals then added
+// from lanes 15 / 31 / 47 via readlane (scalars) -- no LDS round trip; 0: six __shfl_up
+// (ds_bpermute) steps, the round-4 form
+#ifndef CODEC_WSCAN_DPP
+#define CODEC_WSCAN_DPP 1
+#endif
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     const int lane = threadIdx.x & 63;
+#if CODEC_WSCAN_DPP
+    int v = (int)x;
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);   // row_shr:8
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane(v, 15);
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane(v, 31);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane(v, 47);
+    const int row = lane >> 4;
+    uint32_t add = row >= 1 ? r0 : 0u;
+    add += row >= 2 ? r1 : 0u;
+    add += row >= 3 ? r2 : 0u;
+    return (uint32_t)v + add;
+#else
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(x, o, 64);
         if (lane >= o) x += y;
     }
     return x;
+#endif
 }
 
 // exclusive scan over the block (NT threads); sh needs NT/64+1 words

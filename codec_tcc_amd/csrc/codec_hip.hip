@@ -2202,7 +2202,14 @@ __global__ __launch_bounds__(1024) void k_scan_decide(const T* __restrict__ cove
     };
     __shared__ FusedSmem U;
     const int b = blockIdx.y;
+#ifdef DECIDE_TS   // diagnostic build: the workgroup's start (slot 15 of the decision's stamps)
+    long long ts_start = 0;
+    if (threadIdx.x == 0) ts_start = wall_clock64();
+#endif
     scan_rows_body<T, SB, NT, true, 0, true, 4, true>(U.s, cover, stego, P.H, P.W, bands_per_wg, ghist_all, gkey, gor);
+#ifdef DECIDE_TS
+    if (threadIdx.x == 0) reinterpret_cast<long long*>(gterms + (size_t)b * HistCfg<T>::kBins)[HistCfg<T>::kBins - 1] = ts_start;
+#endif
     // scan_rows_body ended with a barrier after its last LDS write (the block key)
     FusedScan fz;
     fz.lds = U.s.lds;

@@ -77,6 +77,15 @@ def main():
     print("slices' entry stamps: median %.2f, max %.2f us after the first; last decision done %.2f us, last embed "
           "done %.2f us after the first entry" % (np.median(t[:, 0] - t00) * 0.01, (t[:, 0].max() - t00) * 0.01,
                                                   (t[:, -1].max() - t00) * 0.01, (raw[:, 11].max() - t00) * 0.01))
+    if (raw[:, 15] > 0).all() and os.environ.get("DTS_SIZE") == "512":   # fused kernel: workgroup start stamps
+        st = raw[:, 15]
+        scan = (t[:, 0] - st) * 0.01
+        print("fused: workgroup starts spread %.2f us; scan (start -> decision entry) median %.2f, min %.2f, max %.2f us"
+              % ((st.max() - st.min()) * 0.01, np.median(scan), scan.min(), scan.max()))
+        print("  by slice % 8 (the XCD its workgroup is dealt to): " + " ".join(
+            "x%d: start %.2f scan %.2f" % (x, np.median(st[x::8] - st.min()) * 0.01, np.median(scan[x::8])) for x in range(8)))
+        order = np.argsort(t[:, 0])
+        print("  slowest 8 slices (scan us): " + " ".join("b%d=%.1f" % (i, scan[i]) for i in order[-8:]))
     print("embed (fused): load_win %.2f us, embed loop %.2f us" % (np.median(raw[:, 10] - raw[:, 5]) * 0.01,
                                                                 np.median(raw[:, 11] - raw[:, 10]) * 0.01))
 
