@@ -30,6 +30,11 @@ def main():
     for _ in range(3):
         codec.encode(covers, pl)
     torch.cuda.synchronize()
+    if os.environ.get("DTS_ISOLATED") == "1":   # the stamped call alone on an idle GPU
+        import time
+        time.sleep(0.05)
+        codec.encode(covers, pl)
+        torch.cuda.synchronize()
     R = 65536
     keys = (B * R * 4 + 255) // 256 * 256
     orv = (keys + B * 8 + 255) // 256 * 256

@@ -38,3 +38,4 @@ for name, a, b in (("start", 0, 0), ("read phase", 0, 1), ("select T", 1, 2), ("
     d = t[:, b] - t[:, a] if a != b else t[:, 0]
     print(f"{name:12s} min {d.min():7.2f}  median {np.median(d):7.2f}  max {d.max():7.2f} us")
 print("last workgroup ends at %.2f us" % t[:, 4].max())
+print("start by slice %% 8 (XCD): " + " ".join("x%d %.2f" % (x, np.median(t[x::8, 0])) for x in range(8)))
