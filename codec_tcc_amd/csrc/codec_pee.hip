@@ -1073,10 +1073,22 @@ __device__ __forceinline__ u64 wave_sum_u64(u64 v) {
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+// The finished flag of a slice: written by the chunk holding `end` as fin_val (1, or the
+// self-cleaning call's tag + 1, <= 64) in its low byte and that chunk's index + 1 above it.
+// It tells chunk c "`end` lies before you" only when the recorded chunk is LOWER than c: the
+// chunk holding `end` can finish before an earlier chunk has -- it needs only the earlier
+// chunks' aggregates, and with the pixel-count fallback not even those -- so a set flag alone
+// says nothing about chunks before it (round 5: a persistent grid that triggered the fallback
+// made earlier chunks skip their bits).
+__device__ __forceinline__ uint32_t pee_fin_word(uint32_t fin_val, int c) { return fin_val | ((uint32_t)(c + 1) << 8); }
+__device__ __forceinline__ bool pee_fin_before(uint32_t w, uint32_t fin_val, int c) {
+    return (w & 0xFFu) == fin_val && (w >> 8) != 0u && (int)((w >> 8) - 1u) < c;
+}
 // TWO: also sum the high field (the self-cleaning embed's unsafe counts); otherwise only the
 // low one, as the zeroing paths need (fewer registers in the headline kernels).
 // tag >= 0 (self-cleaning calls): only words carrying this epoch tag count as published, and
-// the finished flag `done` counts as set only when it holds done_val (tag + 1 there).
+// the finished flag `done` counts as set only when it holds done_val (tag + 1 there) and names
+// a chunk before c (pee_fin_before).
 template <bool TWO = false, typename F>
 __device__ LbSum lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, uint32_t spin_max, const F& count,
                               uint32_t* done = nullptr, uint32_t sat = 0, int tag = -1, uint32_t done_val = 1u) {
@@ -1105,7 +1117,7 @@ __device__ LbSum lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, uin
             const int first = inc ? (int)__builtin_ctzll(inc) : 64;        // nearest inclusive
             const u64 need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);  // lanes 0..first
             if (notready & need) {
-                if (done && ld_agent(done) == done_val) return LbSum{(u64)sat, 0ull};
+                if (done && pee_fin_before(ld_agent(done), done_val, c)) return LbSum{(u64)sat, 0ull};
                 if (done && (PEE_LB_PARTIAL)) {
                     // the published words already bound the prefix from below (aggregates of
                     // disjoint chunks, or an inclusive prefix): reaching `sat` (= L) places this
@@ -1350,8 +1362,8 @@ __global__ PEE_E1_LB void k_pee_embed1(const T* __restrict__ cover, T* stego, in
                 // a flag seen set was set before this chunk started, so `end` lies in an
                 // earlier chunk; a flag set meanwhile but not seen only costs this chunk the
                 // full path.  It counts only when it holds this call's value (tag + 1).
-                const bool dn = dnA == fin_val;
                 cc = (mode & PEE_MODE_NOTICKET) ? (uint32_t)j : atomicAdd(tick, 1u);
+                const bool dn = pee_fin_before(dnA, fin_val, (int)cc);
                 if (dn) {   // `end` already placed: this chunk is a plain copy
                     lb_store(status_all + par * stride + (size_t)b * nchunks + cc, LB_INC | (u64)L | tagw);
                     cc |= 0x80000000u;
@@ -1360,8 +1372,9 @@ __global__ PEE_E1_LB void k_pee_embed1(const T* __restrict__ cover, T* stego, in
                 // the two flag loads and the ticket go out together (one round trip); a ticket
                 // taken for a finished slice is published as "prefix >= L" and skipped
                 const uint32_t nd = ld_agent(ctl);
-                const uint32_t dn = ld_agent(line + PEE_LINE_FIN1);
+                const uint32_t dnw = ld_agent(line + PEE_LINE_FIN1);
                 cc = atomicAdd(tick, 1u);
+                const bool dn = pee_fin_before(dnw, 1u, (int)cc);
                 if (nd >= (uint32_t)B || dn) {
                     if (cc < (uint32_t)nchunks) lb_store(status_all + stride + (size_t)b * nchunks + cc, LB_INC | (u64)L);
                     cc = nd >= (uint32_t)B ? PEE_STOP : PEE_SKIP;
@@ -1386,8 +1399,8 @@ __global__ PEE_E1_LB void k_pee_embed1(const T* __restrict__ cover, T* stego, in
             const bool stale = b == 0 && c == dbg_stale;
             lb_store(status_all + (1 - par) * stride + (size_t)b * nchunks + c, stale ? (LB_INC | tagw) : 0ull);
             if (c == 0 || stale)
-                __hip_atomic_store(line + (par ? PEE_LINE_FIN0 : PEE_LINE_FIN1), stale ? fin_val : 0u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(line + (par ? PEE_LINE_FIN0 : PEE_LINE_FIN1), stale ? pee_fin_word(fin_val, 0) : 0u,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (INPLACE || c != j) pee_load_chunk<T, NT>(src, W, CR, items, c, a0, a1, o0);
         if (copy_only) {
@@ -1583,7 +1596,7 @@ __global__ PEE_E1_LB void k_pee_embed1(const T* __restrict__ cover, T* stego, in
         if (tid == 0) {   // `end` is in this chunk (or there is none): later chunks need no cursor
             const bool fin = (excl < L && excl + agg >= L) || (L == 0 && c == 0) || (last && excl + agg < L);
             if (fin) {
-                __hip_atomic_store(fin_flag, fin_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(fin_flag, pee_fin_word(fin_val, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (INPLACE) atomicAdd(ctl, 1u);
                 if (sc) {   // no meta atomics (nothing zeroed it): the chunk holding `end` writes them
                     M->status = (last && excl + agg < L) ? 1 : 0;

@@ -331,6 +331,43 @@ def test_gpu_lookback_fallback_out_of_place(slots, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("wgs", ["2048"])
+def test_gpu_persistent_grid_fallback_exact(wgs, monkeypatch):
+    """Round 5: an out-of-place single pass on a persistent grid larger than the resident
+    workgroups (CODEC_PEE_1P_WGS) -- chunks then wait on predecessors that have not started and
+    count them from the pixels (the fallback), so the chunk holding `end` can finish before
+    earlier chunks of its slice have.  Its finished flag used to tell those earlier chunks
+    "past end" (they copied instead of embedding: 24 of 256 slices wrong at the headline shape);
+    the flag now names the chunk that set it.  The stego must equal the default grid's bit for
+    bit and round-trip exactly."""
+    torch = pytest.importorskip("torch")
+    import bench
+    from codec_tcc_amd import synth as S
+    from codec_tcc_amd.pee import PeeCodec
+    bsz, h, w = 256, 2048, 2048          # the headline shape: the one the bug showed at
+    dev = torch.device("cuda", 0)
+    covers = bench.make_covers(torch, "ct12", bsz, h, w, dev, 0)
+    codec = PeeCodec(bsz, h, w, T=2)
+    packed = codec.pack_payloads([S.payload(1024, 7 + i) for i in range(bsz)])
+    monkeypatch.delenv("CODEC_PEE_1P_WGS", raising=False)
+    ref = codec.embed(covers, None, stego=torch.empty_like(covers), packed=packed, check=False)
+    ref_st = ref.stego.clone()
+    before = codec.diagnostics(packed[0].shape[1])["embed_fallback_chunks"]
+    monkeypatch.setenv("CODEC_PEE_1P_WGS", wgs)
+    enc = codec.embed(covers, None, stego=torch.empty_like(covers), packed=packed, check=False)
+    torch.cuda.synchronize()
+    fell_back = codec.diagnostics(packed[0].shape[1])["embed_fallback_chunks"] - before
+    bad = (enc.stego != ref_st).flatten(1).any(1).nonzero().flatten().tolist()
+    assert not bad, f"slices {bad} differ from the default grid ({fell_back} fallback chunks)"
+    assert torch.equal(enc.meta, ref.meta) and torch.equal(enc.lm, ref.lm)
+    bits, cover = codec.decode(enc)
+    assert torch.equal(cover, covers)
+    from codec_tcc_amd import framing
+    for i in range(bsz):
+        np.testing.assert_array_equal(np.asarray(bits[i]), framing.to_bits(S.payload(1024, 7 + i)))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("h,w,bsz", [(256, 256, 3), (2048, 2048, 1), (130, 2048, 5)])
 def test_gpu_selfclean_across_calls(h, w, bsz, monkeypatch):
     """Round 4: small out-of-place batches run the look-back with no zeroing launch -- two
