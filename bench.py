@@ -675,6 +675,15 @@ def _strip_private(d):
     return d
 
 
+def _device_uuid(props) -> str:
+    """The device UUID as hex ('' when the build does not expose it)."""
+    u = getattr(props, "uuid", None)
+    try:
+        return bytes(u.bytes).hex()
+    except (AttributeError, TypeError, ValueError):
+        return ""
+
+
 def rank_record(torch, dist, rank, local, dev, backend, head, c4):
     """What this rank ran on: enough for a reader of the N > 1 JSON line
     to check that N ranks ran on N distinct devices over the named backend."""
@@ -684,6 +693,7 @@ def rank_record(torch, dist, rank, local, dev, backend, head, c4):
            "host": socket.gethostname(),
            "pci": f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:"
                   f"{getattr(p, 'pci_device_id', 0):02x}",
+           "uuid": _device_uuid(p),   # tells apart partitions sharing one PCI address
            "gpu": p.name, "arch": getattr(p, "gcnArchName", ""),
            "backend": dist.get_backend(), "world_size": dist.get_world_size(),
            "ms_per_step": head.get("_rank_ms_per_step"),
@@ -695,12 +705,13 @@ def rank_record(torch, dist, rank, local, dev, backend, head, c4):
 
 def gather_rank_records(torch, dist, world, rec, backend):
     """Every rank's record, in rank order (one all_gather_object after the timed loops).
-    Over RCCL the devices must be distinct (host, PCI address): RCCL itself refuses two ranks
-    on one GPU, and a duplicate here would mean the launcher mapped ranks wrongly."""
+    Over RCCL the devices must be distinct (host, PCI address, device UUID -- the UUID tells
+    apart compute partitions of one package): RCCL itself refuses two ranks on one GPU, and a
+    duplicate here would mean the launcher mapped ranks wrongly."""
     recs = [None] * world
     dist.all_gather_object(recs, rec)
     if backend == "nccl":
-        seen = {(r["host"], r["pci"]) for r in recs}
+        seen = {(r["host"], r["pci"], r.get("uuid", "")) for r in recs}
         if len(seen) != world:
             raise RuntimeError(f"bench.py: {world} RCCL ranks on {len(seen)} distinct devices: {recs}")
     return recs
@@ -949,7 +960,7 @@ def main():
         out = _strip_private(out)
         if ranks is not None:
             out["ranks"] = ranks
-            out["distinct_devices"] = len({(r["host"], r["pci"]) for r in ranks})
+            out["distinct_devices"] = len({(r["host"], r["pci"], r.get("uuid", "")) for r in ranks})
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()   # rank 0 ran its C3 leg alone: every rank leaves the group together
