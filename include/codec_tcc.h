@@ -236,8 +236,11 @@ typedef struct codec_pee_meta {
 
 /* Zero-initialise the workspace once before its first use (the diagnostic counters live
  * in it; everything else is cleared by the calls themselves).  Small out-of-place batches
- * (B <= 7) keep call-to-call state in it (per-chunk arrival counts; status words by call
- * parity, each carrying the call's epoch tag).  Recovery rules:
+ * (B <= 7) keep call-to-call state in it (status words and finished flags by call parity,
+ * each carrying the call's epoch tag; the library counts the epochs per workspace).  A
+ * workspace serves one call at a time: calls that share it must be ordered (one stream, or
+ * synchronised); calls in flight together on different streams need separate workspaces.
+ * Recovery rules:
  *   - shape change: the library remembers per (device, workspace pointer) the shape of the
  *     last call; a call of another (B, H, W, bytes) zeroes the workspace first (one extra
  *     launch; the diagnostic counters are kept), so one workspace sized for the largest
