@@ -1082,7 +1082,8 @@ __device__ __forceinline__ u64 wave_sum_u64(u64 v) {
 // made earlier chunks skip their bits).
 __device__ __forceinline__ uint32_t pee_fin_word(uint32_t fin_val, int c) { return fin_val | ((uint32_t)(c + 1) << 8); }
 __device__ __forceinline__ bool pee_fin_before(uint32_t w, uint32_t fin_val, int c) {
-    return (w & 0xFFu) == fin_val && (w >> 8) != 0u && (int)((w >> 8) - 1u) < c;
+    // (w >> 8) in [1, c]: w - 256 wraps past every bound when the index field is 0
+    return ((w & 0xFFu) == fin_val) & ((w - 256u) < ((uint32_t)c << 8));
 }
 // TWO: also sum the high field (the self-cleaning embed's unsafe counts); otherwise only the
 // low one, as the zeroing paths need (fewer registers in the headline kernels).
