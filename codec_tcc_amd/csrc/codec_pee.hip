@@ -1047,6 +1047,13 @@ struct ExtractCount {
 #ifndef LB_WIN
 #define LB_WIN 4
 #endif
+// PEE_LB_DONE_POLL: a waiting embed chunk also polls the slice's finished flag (released as
+// "past `end`" when the chunk that set it lies before it).  Measured (round 5, headline): off,
+// the chunks past `end` wait out their predecessors' words instead -- k_pee_embed1 0.745 ->
+// 0.79-0.80 ms; it stays on
+#ifndef PEE_LB_DONE_POLL
+#define PEE_LB_DONE_POLL 1
+#endif
 #ifndef PEE_LB_PARTIAL
 #define PEE_LB_PARTIAL 1   // embed: a partial sum of the published words may end the wait (past `end`)
 #endif
@@ -1118,7 +1125,9 @@ __device__ LbSum lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, uin
             const int first = inc ? (int)__builtin_ctzll(inc) : 64;        // nearest inclusive
             const u64 need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);  // lanes 0..first
             if (notready & need) {
+#if PEE_LB_DONE_POLL
                 if (done && pee_fin_before(ld_agent(done), done_val, c)) return LbSum{(u64)sat, 0ull};
+#endif
                 if (done && (PEE_LB_PARTIAL)) {
                     // the published words already bound the prefix from below (aggregates of
                     // disjoint chunks, or an inclusive prefix): reaching `sat` (= L) places this
