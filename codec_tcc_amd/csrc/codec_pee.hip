@@ -1092,6 +1092,9 @@ __device__ __forceinline__ bool pee_fin_before(uint32_t w, uint32_t fin_val, int
     // (w >> 8) in [1, c]: w - 256 wraps past every bound when the index field is 0
     return ((w & 0xFFu) == fin_val) & ((w - 256u) < ((uint32_t)c << 8));
 }
+// untagged calls (fin_val 1, the flag zeroed before the call: it holds 0 or 1 + 256 k): one
+// compare, 0 wrapping past every bound
+__device__ __forceinline__ bool pee_fin_before1(uint32_t w, int c) { return w - 257u < ((uint32_t)c << 8); }
 // TWO: also sum the high field (the self-cleaning embed's unsafe counts); otherwise only the
 // low one, as the zeroing paths need (fewer registers in the headline kernels).
 // tag >= 0 (self-cleaning calls): only words carrying this epoch tag count as published, and
@@ -1126,7 +1129,10 @@ __device__ LbSum lb_exclusive(u64* st, int c, bool* timeout, bool* fallback, uin
             const u64 need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);  // lanes 0..first
             if (notready & need) {
 #if PEE_LB_DONE_POLL
-                if (done && pee_fin_before(ld_agent(done), done_val, c)) return LbSum{(u64)sat, 0ull};
+                if (done) {
+                    const uint32_t dw = ld_agent(done);
+                    if (tag >= 0 ? pee_fin_before(dw, done_val, c) : pee_fin_before1(dw, c)) return LbSum{(u64)sat, 0ull};
+                }
 #endif
                 if (done && (PEE_LB_PARTIAL)) {
                     // the published words already bound the prefix from below (aggregates of
@@ -1373,7 +1379,7 @@ __global__ PEE_E1_LB void k_pee_embed1(const T* __restrict__ cover, T* stego, in
                 // earlier chunk; a flag set meanwhile but not seen only costs this chunk the
                 // full path.  It counts only when it holds this call's value (tag + 1).
                 cc = (mode & PEE_MODE_NOTICKET) ? (uint32_t)j : atomicAdd(tick, 1u);
-                const bool dn = pee_fin_before(dnA, fin_val, (int)cc);
+                const bool dn = sc ? pee_fin_before(dnA, fin_val, (int)cc) : pee_fin_before1(dnA, (int)cc);
                 if (dn) {   // `end` already placed: this chunk is a plain copy
                     lb_store(status_all + par * stride + (size_t)b * nchunks + cc, LB_INC | (u64)L | tagw);
                     cc |= 0x80000000u;
@@ -1384,7 +1390,7 @@ __global__ PEE_E1_LB void k_pee_embed1(const T* __restrict__ cover, T* stego, in
                 const uint32_t nd = ld_agent(ctl);
                 const uint32_t dnw = ld_agent(line + PEE_LINE_FIN1);
                 cc = atomicAdd(tick, 1u);
-                const bool dn = pee_fin_before(dnw, 1u, (int)cc);
+                const bool dn = pee_fin_before1(dnw, (int)cc);
                 if (nd >= (uint32_t)B || dn) {
                     if (cc < (uint32_t)nchunks) lb_store(status_all + stride + (size_t)b * nchunks + cc, LB_INC | (u64)L);
                     cc = nd >= (uint32_t)B ? PEE_STOP : PEE_SKIP;
