@@ -368,6 +368,37 @@ def test_gpu_persistent_grid_fallback_exact(wgs, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("bsz", [64, 5])
+def test_gpu_lookback_fallback_stress(bsz, monkeypatch):
+    """The look-back's pixel-count fallback as the common case rather than the exception: a
+    4-poll spin bound (CODEC_DEBUG=1 CODEC_PEE_LB_SPINS=4) makes most waiting chunks count
+    their predecessors from pixels.  Embed and extract must equal the default run bit for bit
+    (64 slices: lane slots; 5: flat self-cleaning slots), three calls in a row."""
+    torch = pytest.importorskip("torch")
+    import bench
+    from codec_tcc_amd import synth as S
+    from codec_tcc_amd.pee import PeeCodec
+    h = w = 1024
+    dev = torch.device("cuda", 0)
+    covers = bench.make_covers(torch, "ct12", bsz, h, w, dev, 3)
+    codec = PeeCodec(bsz, h, w, T=2)
+    packed = codec.pack_payloads([S.payload(900, 70 + i) for i in range(bsz)])
+    pw = packed[0].shape[1]
+    ref = codec.embed(covers, None, stego=torch.empty_like(covers), packed=packed, check=False)
+    wr, cr = (t.clone() for t in codec.extract(ref.stego, ref.meta, ref.lm, payload_words=pw))
+    assert torch.equal(cr, covers)
+    monkeypatch.setenv("CODEC_DEBUG", "1")
+    monkeypatch.setenv("CODEC_PEE_LB_SPINS", "4")
+    for _ in range(3):
+        alt = codec.embed(covers, None, stego=torch.empty_like(covers), packed=packed, check=False)
+        wa, ca = codec.extract(alt.stego, alt.meta, alt.lm, payload_words=pw)
+        assert torch.equal(alt.stego, ref.stego) and torch.equal(alt.meta, ref.meta) and torch.equal(alt.lm, ref.lm)
+        assert torch.equal(wa, wr) and torch.equal(ca, covers)
+    d = codec.diagnostics(pw)
+    assert d["embed_unrecovered_chunks"] == 0 == d["extract_unrecovered_chunks"]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("h,w,bsz", [(256, 256, 3), (2048, 2048, 1), (130, 2048, 5)])
 def test_gpu_selfclean_across_calls(h, w, bsz, monkeypatch):
     """Round 4: small out-of-place batches run the look-back with no zeroing launch -- two
