@@ -1051,6 +1051,11 @@ struct ExtractCount {
 // "past `end`" when the chunk that set it lies before it).  Measured (round 5, headline): off,
 // the chunks past `end` wait out their predecessors' words instead -- k_pee_embed1 0.745 ->
 // 0.79-0.80 ms; it stays on
+// PEE_FIN_EARLY: out of place the chunk holding `end` sets the finished flag right after its
+// look-back (before its embed loop) rather than at its end
+#ifndef PEE_FIN_EARLY
+#define PEE_FIN_EARLY 1
+#endif
 #ifndef PEE_LB_DONE_POLL
 #define PEE_LB_DONE_POLL 1
 #endif
@@ -1526,6 +1531,11 @@ __global__ PEE_E1_LB void k_pee_embed1(const T* __restrict__ cover, T* stego, in
             if (fin) {
                 M->capacity = (int)(excl + agg);
                 M->flags = last ? 0 : CODEC_PEE_PARTIAL;
+                // out of place the flag goes up as soon as this chunk knows it holds `end`: the
+                // chunks past it only read the flag (nothing of this chunk's data), so they are
+                // released before this chunk's embed loop instead of after it
+                if (!INPLACE && PEE_FIN_EARLY)
+                    __hip_atomic_store(fin_flag, pee_fin_word(fin_val, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             if (last && excl + agg < L) {
                 M->end = nc - 1;
@@ -1612,7 +1622,8 @@ __global__ PEE_E1_LB void k_pee_embed1(const T* __restrict__ cover, T* stego, in
         if (tid == 0) {   // `end` is in this chunk (or there is none): later chunks need no cursor
             const bool fin = (excl < L && excl + agg >= L) || (L == 0 && c == 0) || (last && excl + agg < L);
             if (fin) {
-                __hip_atomic_store(fin_flag, pee_fin_word(fin_val, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (INPLACE || !PEE_FIN_EARLY)
+                    __hip_atomic_store(fin_flag, pee_fin_word(fin_val, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (INPLACE) atomicAdd(ctl, 1u);
                 if (sc) {   // no meta atomics (nothing zeroed it): the chunk holding `end` writes them
                     M->status = (last && excl + agg < L) ? 1 : 0;
