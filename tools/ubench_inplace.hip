@@ -28,7 +28,7 @@ __device__ __forceinline__ void lds_barrier() {
 
 // EARLY: the slot's refill is issued right after its data is taken (into temporaries), before
 // the barrier and the compute -- D loads stay in flight through the barrier
-template <int D, bool BAR, int VALU, bool EARLY = false>
+template <int D, bool BAR, int VALU, bool EARLY = false, bool PS = false>
 __global__ __launch_bounds__(NT) void inplace_stream(unsigned short* img, int nchunk, unsigned* sink) {
     __shared__ unsigned pad[21 * 1024];   // one workgroup per CU, as the embed's pad
     const size_t npx = (size_t)H * W;
@@ -67,7 +67,8 @@ __global__ __launch_bounds__(NT) void inplace_stream(unsigned short* img, int nc
             acc += x;
             b.x ^= (acc & 0u);
             if (BAR) lds_barrier();
-            __builtin_nontemporal_store(b, reinterpret_cast<v4u*>(s + so + W));
+            if (PS) *reinterpret_cast<v4u*>(s + so + W) = b;   // plain (cache-allocating) store: round 5's default
+            else __builtin_nontemporal_store(b, reinterpret_cast<v4u*>(s + so + W));
             if (!EARLY) {
                 const unsigned it = (unsigned)(k + D) * NT + threadIdx.x;
                 const unsigned kk = k + D < nchunk ? it : threadIdx.x;
@@ -218,7 +219,7 @@ int main() {
     CK(hipEventCreate(&e1));
     const double algo = (double)B * NCHUNK * NT * 48.0;   // 32 B read + 16 B written per item
     for (int pass = 0; pass < 2; ++pass) {
-        for (int variant = 0; variant < 27; ++variant) {
+        for (int variant = 0; variant < 30; ++variant) {
             const char* name = "";
             float sum = 0.f, best = 1e9f;
             const int reps = 20;
@@ -252,6 +253,9 @@ int main() {
                 case 24: name = "early ring 1 +bar2 +valu 48"; inplace_chain<1, 48, true, false, false><<<B, NT>>>(img, NCHUNK, sink); break;
                 case 25: name = "early ring 2 +chain"; inplace_chain<2, 0, true, true, false><<<B, NT>>>(img, NCHUNK, sink); break;
                 case 26: name = "early ring 4 +pair +valu 48"; inplace_chain<4, 48, true, false, true><<<B, NT>>>(img, NCHUNK, sink); break;
+                case 27: name = "early ring 1 +bar +valu 48 +ps"; inplace_stream<1, true, 48, true, true><<<B, NT>>>(img, NCHUNK, sink); break;
+                case 28: name = "early ring 2 +bar +valu 48 +ps"; inplace_stream<2, true, 48, true, true><<<B, NT>>>(img, NCHUNK, sink); break;
+                case 29: name = "ring 2 +ps (no barrier, no valu)"; inplace_stream<2, false, 0, false, true><<<B, NT>>>(img, NCHUNK, sink); break;
                 }
                 CK(hipGetLastError());
                 CK(hipEventRecord(e1, 0));
