@@ -2209,6 +2209,10 @@ __global__ __launch_bounds__(1024) void k_scan_decide(const T* __restrict__ cove
     scan_rows_body<T, SB, NT, true, 0, true, 4, true>(U.s, cover, stego, P.H, P.W, bands_per_wg, ghist_all, gkey, gor);
 #ifdef DECIDE_TS
     if (threadIdx.x == 0) reinterpret_cast<long long*>(gterms + (size_t)b * HistCfg<T>::kBins)[HistCfg<T>::kBins - 1] = ts_start;
+#ifdef DECIDE_TS_SCAN_ONLY   // diagnostic: the scan alone (decisions invalid), its start spread
+    if (threadIdx.x == 0) reinterpret_cast<long long*>(gterms + (size_t)b * HistCfg<T>::kBins)[HistCfg<T>::kBins - 16] = wall_clock64();
+    return;
+#endif
 #endif
     // scan_rows_body ended with a barrier after its last LDS write (the block key)
     FusedScan fz;
