@@ -200,3 +200,13 @@ def test_gpus_world_size_mismatch_is_refused():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_device_uuid_hex():
+    """bench._device_uuid: the UUID's bytes as hex; '' when the build exposes none."""
+    import types
+    import bench
+    u = types.SimpleNamespace(bytes=bytes(range(16)))
+    assert bench._device_uuid(types.SimpleNamespace(uuid=u)) == bytes(range(16)).hex()
+    assert bench._device_uuid(types.SimpleNamespace()) == ""
+    assert bench._device_uuid(types.SimpleNamespace(uuid="not-an-object")) == ""

@@ -248,22 +248,27 @@ def _ranks_worker(rank, world, port, same_device, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
-    rec = {"rank": rank, "host": "h", "pci": "0000:%02x:00" % (0 if same_device else rank), "ms_per_step": 1.0 + rank}
+    # "partitions": one PCI address, distinct device UUIDs (compute partitions of one package)
+    pci = "0000:%02x:00" % (rank if same_device == "distinct" else 0)
+    uuid = "%032x" % (rank if same_device == "partitions" else 7)
+    rec = {"rank": rank, "host": "h", "pci": pci, "uuid": uuid, "ms_per_step": 1.0 + rank}
     out = bench.gather_rank_records(torch, dist, world, rec, "gloo")
     ok = [r["rank"] for r in out] == list(range(world)) and out[rank] == rec
+    shared = same_device == "shared"
     try:
         bench.gather_rank_records(torch, dist, world, rec, "nccl")
-        ok &= not same_device
+        ok &= not shared
     except RuntimeError as e:
-        ok &= same_device and "distinct devices" in str(e)
+        ok &= shared and "distinct devices" in str(e)
     q.put((rank, bool(ok)))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("same_device", [False, True])
+@pytest.mark.parametrize("same_device", ["distinct", "shared", "partitions"])
 def test_rank_records_gathered_and_checked(same_device):
     """the per-rank records of the N > 1 bench line arrive in rank order,
-    and over RCCL a shared device is refused."""
+    and over RCCL a shared device is refused -- a device being (host, PCI address, UUID), so
+    compute partitions of one package (one PCI address, distinct UUIDs) are distinct."""
     world = 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
