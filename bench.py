@@ -547,6 +547,10 @@ def bench_lsb(args, torch, dist, world, rank, dev, covers, B, H, W, *, exchange=
     res = {"value": round(B * H * W * world * steps / el / 1e6, 1), "unit": "Mpixels/s",
            "ms_per_step": round(el / steps * 1e3, 4), "roundtrip_ok": cover_ok and pay_ok and status_ok,
            "cover_ok": cover_ok, "payload_ok": pay_ok, "status_ok": status_ok, "s_values": sorted({r.s for r in recs}),
+           # the guard-banded s decision: slices settled from H(X) vs those inside the 1e-9 band
+           # (decided by the numpy-order joint sums)
+           "decide": {"guarded": sum(1 for r in recs if r.flags & _lib.FLAG_INFO_FAST),
+                      "guard_fallbacks": sum(1 for r in recs if r.flags & _lib.FLAG_GUARD_FALLBACK)},
            "path": "the reference's pixel path (bit-plane LSB embed + true decode, src/codec.py:412-487, "
                    "752-793), bit-exact with it"}
     if xch is not None:   # this rank's rows of the gathered records are its own packed records

@@ -20,6 +20,8 @@ FLAG_OVERLAP = 1
 FLAG_LOSSY = 2
 FLAG_BADLUT = 4
 FLAG_DECIDE_TIMEOUT = 8   # split decision: a plane workgroup never reported (status 2)
+FLAG_INFO_FAST = 16      # s decided by the guard band: mi[] = H(X), cum_info their sum
+FLAG_GUARD_FALLBACK = 32 # a prefix within 1e-9 of the target: the exact numpy-order sums decided
 
 I16 = C.c_int32 * MAX_PLANES
 D16 = C.c_double * MAX_PLANES
@@ -74,6 +76,7 @@ _VP = C.c_void_p
 _SIGS = {
     "codec_abi_version": (C.c_int, []),
     "codec_build_digest": (C.c_char_p, []),
+    "codec_set_tuning": (C.c_int, [C.c_int32]),
     "codec_last_error": (C.c_char_p, []),
     "codec_workspace_bytes": (C.c_size_t, [C.POINTER(Params)]),
     "codec_plan": (C.c_int, [C.POINTER(Params), _VP, _VP, _VP, C.c_int64, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),

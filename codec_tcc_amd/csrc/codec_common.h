@@ -2,6 +2,8 @@
 // (error reporting, profiling hooks, wave/block scans, streaming vector loads/stores).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -290,19 +292,28 @@ __device__ __forceinline__ uint32_t lsb_count(const uint2& v) {
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
-// launch-shape knobs (defaults from measurements on MI355X; env overrides for tuning runs)
+// launch-shape knobs (the defaults are the measured best on MI355X).  An environment override
+// is honoured only while the tuning switch is on: CODEC_TUNING=1 in the
+// environment when the library is loaded (read once, at load), or codec_set_tuning(1) (A/B
+// tools, the test suite).  With the switch off -- the product default -- every knob is its
+// default and no launch reads the environment, so a stray CODEC_* variable cannot change which
+// kernels run and getenv never races a setenv in another thread.
+extern std::atomic<int> g_tuning;
+static inline bool tuning_on() { return g_tuning.load(std::memory_order_relaxed) != 0; }
 static long long knob(const char* name, long long dflt) {
+    if (!tuning_on()) return dflt;
     const char* v = getenv(name);
     return (v && *v) ? atoll(v) : dflt;
 }
 
-// fault-injection and spin-bound knobs (tests only): live only in a -DCODEC_DEBUG_KNOBS build
-// or with the master switch CODEC_DEBUG=1, so a leaked CODEC_PEE_DEBUG_SKIP cannot make a
-// production launch skip a publish
+// fault-injection and spin-bound knobs (tests only): live only under the tuning switch AND
+// either a -DCODEC_DEBUG_KNOBS build or the master switch CODEC_DEBUG=1, so a leaked
+// CODEC_PEE_DEBUG_SKIP cannot make a production launch skip a publish
 static inline bool debug_knobs_enabled() {
 #ifdef CODEC_DEBUG_KNOBS
-    return true;
+    return tuning_on();
 #else
+    if (!tuning_on()) return false;
     const char* v = getenv("CODEC_DEBUG");
     return v && v[0] == '1' && v[1] == 0;
 #endif

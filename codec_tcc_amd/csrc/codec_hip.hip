@@ -22,6 +22,12 @@
 
 thread_local char g_err[512] = "";
 ProfWin g_prof;
+// the A/B knobs' tuning switch (codec_common.h): CODEC_TUNING=1 at load, or codec_set_tuning
+static int tuning_from_env() {
+    const char* v = getenv("CODEC_TUNING");
+    return (v && v[0] == '1' && v[1] == 0) ? 1 : 0;
+}
+std::atomic<int> g_tuning{tuning_from_env()};
 
 // ------------------------------------------------------------------ numpy float emulation
 // numpy's add.reduce over a contiguous float64 array (np.sum) walks it in buffers of
@@ -1172,6 +1178,8 @@ struct ListTerm {
 // (CAS 0 -> ABANDONED); the late plane workgroup's CAS then fails and it clears the slot
 // itself, so no value of this launch can be read by the next one
 #define PLANE_ABANDONED 0x7FF8DEAD00000002ull
+// a plane workgroup whose slice the guard-banded decision settled (no joint sum needed)
+#define PLANE_FAST 0x7FF8DEAD00000003ull
 #ifdef DECIDE_TS   // diagnostic build only (tools/decide_phases.py): phase timestamps into the term scratch
 // (b, role: decide_body's slice and workgroup role -- k_decide's blockIdx.x / .y; k_scan_decide
 // runs slice blockIdx.y as role 0)
@@ -1456,6 +1464,10 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     u64* pm = reinterpret_cast<u64*>(reinterpret_cast<char*>(list) + off_pm);
     uint16_t* jl = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(list) + off_jl);
     if (wfast) terms = tl;
+    // the guard-banded decision (below) needs H(Y) only to ~1e-13: this thread's terms summed
+    // in any order
+    const bool try_fast = P.fixed_s <= 0 && !P.all_mi && lut_ok && !(P.reserved & 8);
+    double hy_part = 0.0;
     // terms of the non-zero bins in ascending value order, computed once
     if (lut_ok && !walk) {
         uint32_t r = rank0;
@@ -1476,7 +1488,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
             for (int u = 0; u < 8; ++u) tt[u] = plogp(lut, cc[u], Nd);
 #pragma unroll
             for (int u = 0; u < 8; ++u)
-                if (u < k) terms[r + u] = tt[u];
+                if (u < k) { terms[r + u] = tt[u]; hy_part += tt[u]; }
             if (wfast) {
 #pragma unroll
                 for (int u = 0; u < 8; ++u)
@@ -1485,8 +1497,81 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
             r += k;
         }
     }
+    if (try_fast && walk) {   // wide slices: no term array -- the count codes of pass 1, a wave per group
+        const int lane = t & 63, wv = t >> 6, ng = Rp / 64;
+        for (int g0 = wv; g0 < ng; g0 += 16 * 8) {
+            uint16_t cc[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int g = g0 + 16 * u;
+                cc[u] = g < ng ? list[cv_slot((g << 6) + lane)] : (uint16_t)0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                hy_part += cc[u] != kBigCode ? tcs[cc[u]] : plogp(lut, hist[((g0 + 16 * u) << 6) + lane], Nd);
+        }
+    }
+    if (t < 16) mis_sh[t] = 0.0;
     __syncthreads();
 
+    // ---- the s decision, guard-banded.  X = f(Y), so I(X;Y) = H(X) exactly: the
+    // reference's MI (codec.py:554, h_x + h_y - h_xy from two numpy-order sums) differs from
+    // H(X) only by the rounding of its sums, |d| <= ~1e-13 per plane (a pairwise sum of terms
+    // totalling <= 16 bits; measured <= 3.6e-14 on 48 slices).  So s is decided from the
+    // cumulative H(X) against beta * H(Y) with H(Y) summed in any order, unless a prefix of
+    // that walk lies within kDecideGuard of its target: then -- or when all_mi asks for every
+    // exact value, or fixed_s skips the decision -- the numpy-order joint sums below decide as
+    // before.  A slice decided here records CODEC_FLAG_INFO_FAST (mi[] = H(X) of the planes
+    // the loop evaluated, cum_info their sum); one that fell back, CODEC_FLAG_GUARD_FALLBACK.
+    constexpr double kDecideGuard = 1e-9;
+    int fs = 0;               // uniform: s of the fast decision, 0 = the exact path decides
+    bool guard_fb = false;    // uniform: the guard band sent the slice to the exact path
+    double fast_cum = 0.0;    // thread 0
+    if (try_fast) {
+        const int lane = t & 63, wv = t >> 6;
+        double hp = hy_part;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) hp += __shfl_xor(hp, o, 64);
+        if (lane == 0) hxy_sh[wv] = hp;           // scratch until the exact rounds
+        const int nb = min(P.nbits, 16);
+        if (wv == 1 && lane < nb) {   // H(X) of every plane, log2 on the device (no table round trip)
+            const uint32_t pp = pops_sh[lane];
+            const double p1 = (double)pp / Nd, p0 = (double)(npx - pp) / Nd;
+            hx_sh[lane] = (pp != 0 && (long long)pp != npx) ? -(p0 * log2(p0) + p1 * log2(p1)) : 0.0;
+        }
+        __syncthreads();
+        if (t == 0) {
+            double hyf = 0.0;
+            for (int w = 0; w < 16; ++w) hyf += hxy_sh[w];
+            const double tg = P.beta * -hyf;
+            double c = 0.0;
+            bool clear = true;    // every prefix's |cum - target| > guard (false on NaN too)
+            int sf = 1, nev = nb;
+            for (int i = 0; i < nb; ++i) {
+                c += hx_sh[i];    // 0 for a constant plane, codec.py:520-523
+                if (!(fabs(c - tg) > kDecideGuard)) clear = false;
+                if (c >= tg) { sf = i + 1; nev = i + 1; break; }
+            }
+            if (clear)
+                for (int i = 0; i < nev; ++i) mis_sh[i] = hx_sh[i];
+            fast_cum = c;
+            ctl_sh[2] = clear ? sf : 0;
+        }
+        __syncthreads();
+        fs = ctl_sh[2];
+        guard_fb = fs == 0;
+    }
+
+    if (role > 0 && fs) {   // split decision, decided without the joint sums: nothing to compute
+        if (t == 0) {
+            u64* sp = plane_slots + 16 * (size_t)b + (role - 1);
+            u64 expect = 0ull;
+            if (!__hip_atomic_compare_exchange_strong(sp, &expect, PLANE_FAST, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT) && expect == PLANE_ABANDONED)
+                __hip_atomic_store(sp, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
     if (role > 0) {
         // ---- a plane workgroup: H(X,Y) of plane i over the whole CU -- the joint order by
         // a block scan, numpy's pairwise sum by np_sum_block1024 (the same tree as the wave
@@ -1552,6 +1637,9 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
                     v = expect;
                 }
             }
+            // a plane workgroup that took the guard-banded route while this one did not (the
+            // two evaluate the same test on the same histogram, so never): an error, not a value
+            if (v == PLANE_FAST && !fs) slot_to = 1;
             slot_sh[t] = v;
         }
         __syncthreads();
@@ -1608,9 +1696,9 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     int s = 1;
     bool decided = false;
     double cum = 0.0;
-    if (t < 16) mis_sh[t] = 0.0;
+    if (fs) { s = fs; decided = true; cum = fast_cum; }   // the exact loops below stop at once
     const bool need_decision = (P.fixed_s <= 0);
-    if (wfast && nsplit > 0) {
+    if (wfast && nsplit > 0 && !fs) {
         // split decision: H(Y) here (wave 15) while the plane workgroups sum their orders,
         // then thread 0 takes the planes in order exactly like the sequential loop
         const int wv = t >> 6, lane = t & 63;
@@ -1650,6 +1738,16 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
                 }
             }
         }
+    } else if (wfast && fs) {
+        // settled by the guard band: only the record's exact H(Y) and the start offset remain.
+        // H(Y) in numpy's order by the whole workgroup (8 lanes per leaf, every leaf at once;
+        // slot sums in vals[512..], clear of the layouts), the tree re-added by wave 0
+        const double h = np_sum_block1024_w0(RankTerm{tl}, (int)m, vals + 512);
+        if (t == 0) hy_sh = -h;
+        if (t < 16 * kLayW) reinterpret_cast<int32_t*>(vals)[t] = lay_all[t];
+        find_offset();
+        __syncthreads();   // hy_sh (find_offset has no barrier without a block search)
+        Hy = hy_sh;
     } else if (wfast) {
         // H(Y) by wave 0; then rounds of `wplanes` planes, plane i0+w on wave w: its joint
         // bincount order (bit-i-clear bins ascending, then bit-i-set bins, codec.py:546-551)
@@ -1932,7 +2030,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
             for (int q = 0; q < 2; ++q) {
                 const int i = i0 + q;
                 const uint32_t pp = (i >= 0 && i < nb) ? pops_sh[i] : 0u;
-                run[q] = i < 0 || (i < nb && pp != 0 && (long long)pp != npx);   // codec.py:520-523
+                run[q] = i < 0 || (!fs && i < nb && pp != 0 && (long long)pp != npx);   // codec.py:520-523
             }
 #ifdef DECIDE_TS
             long long* wts = i0 < 0 ? reinterpret_cast<long long*>(gterms + (size_t)b * R) + R - 4 : nullptr;
@@ -2054,6 +2152,8 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     const int s = sdec;
     if ((P.mode == CODEC_MODE_MULTI && s > 1) || (P.align && s > 1) || (long long)cat > npx) flags |= CODEC_FLAG_OVERLAP;
     if (!lut_ok) flags |= CODEC_FLAG_BADLUT;
+    if (fs) flags |= CODEC_FLAG_INFO_FAST;
+    if (guard_fb) flags |= CODEC_FLAG_GUARD_FALLBACK;
     M->s = s;
     M->start_offset = (P.mode == CODEC_MODE_HYBRID) ? offset : 0;
     M->total_used = cat;
@@ -3030,6 +3130,7 @@ static WsLayout ws_layout(const codec_params* P) {
 extern "C" {
 
 int codec_abi_version(void) { return CODEC_ABI_VERSION; }
+int codec_set_tuning(int32_t on) { return g_tuning.exchange(on ? 1 : 0); }
 
 int codec_profile_begin(int32_t capacity) {
     if (g_prof.ev) return set_err(CODEC_EINVAL, "profile window already open");
@@ -3196,6 +3297,15 @@ static int launch_scan_generic(const codec_params* P, const void* cover, void* s
     return 0;
 }
 
+// codec_params.reserved bits of the decision's A/B knobs: 1 block-sequential path
+// (CODEC_DECIDE_WAVES=0), 2 no walk path (CODEC_DECIDE_WALK=0), 4 one wave per plane
+// (CODEC_DECIDE_PAIRS=0), 8 no guard-banded decision: the numpy-order sums always decide
+// (CODEC_DECIDE_EXACT=1)
+static int decide_reserved() {
+    return (knob("CODEC_DECIDE_WAVES", 1) ? 0 : 1) | (knob("CODEC_DECIDE_WALK", 1) ? 0 : 2) |
+           (knob("CODEC_DECIDE_PAIRS", 1) ? 0 : 4) | (knob("CODEC_DECIDE_EXACT", 0) ? 8 : 0);
+}
+
 // codec_plan's body; E != nullptr: codec_encode's fused path (k_decide embeds the payload)
 static int plan_impl(const codec_params* P, const void* cover, void* stego, const double* log2_lut, int64_t lut_len,
                      const codec_layout* table, const int32_t* slice_class, codec_slice_meta* meta, void* workspace,
@@ -3239,8 +3349,7 @@ static int plan_impl(const codec_params* P, const void* cover, void* stego, cons
                               (!need_blocks0 || host_exact_count(P, true) == 0);
         if (fk != 0 && shape_ok && (fk == 2 || (long long)P->B >= device_cu_count())) {
             codec_params Pv = *P;
-            Pv.reserved = (knob("CODEC_DECIDE_WAVES", 1) ? 0 : 1) | (knob("CODEC_DECIDE_WALK", 1) ? 0 : 2) |
-                          (knob("CODEC_DECIDE_PAIRS", 1) ? 0 : 4);
+            Pv.reserved = decide_reserved();
             ProfScope prof(st, CODEC_K_SCAN_DECIDE);
             const bool nt = knob("CODEC_NT", 1) != 0;
 #define SD(NTV) hipLaunchKernelGGL((k_scan_decide<uint16_t, 16, NTV>), dim3(1, P->B), dim3(1024), 0, st, \
@@ -3284,13 +3393,17 @@ static int plan_impl(const codec_params* P, const void* cover, void* stego, cons
     }
     codec_params Pv = *P;
     // bit 0: force the block-sequential decision; bit 1: no walk path for wide slices
-    Pv.reserved = (knob("CODEC_DECIDE_WAVES", 1) ? 0 : 1) | (knob("CODEC_DECIDE_WALK", 1) ? 0 : 2) |
-                          (knob("CODEC_DECIDE_PAIRS", 1) ? 0 : 4);
-    // small batches: the per-plane joint entropies go to plane workgroups on otherwise idle
-    // CUs (1 + nb workgroups per slice, all co-resident: at most 240 of them, one per CU)
+    Pv.reserved = decide_reserved();
+    // small batches asking for every plane's exact MI (all_mi): the per-plane joint entropies
+    // go to plane workgroups on otherwise idle CUs (1 + nb workgroups per slice, all
+    // co-resident: at most 240 of them, one per CU).  Without all_mi the guard-banded decision
+    // settles nearly every slice without the joint sums, and the rare slice inside the guard
+    // band runs them on its own workgroup's waves; CODEC_DECIDE_SPLIT=2 splits anyway (tests),
+    // 0 never.
     const int nbp = P->nbits < 16 ? P->nbits : 16;
-    const bool need_mi = P->fixed_s <= 0 || P->all_mi;
-    const int nsplit = (knob("CODEC_DECIDE_SPLIT", 1) && need_mi && (long long)P->B * (1 + nbp) <= 240) ? nbp : 0;
+    const long long split_knob = knob("CODEC_DECIDE_SPLIT", 1);
+    const bool want_split = split_knob == 2 ? (P->fixed_s <= 0 || P->all_mi) : (split_knob != 0 && P->all_mi);
+    const int nsplit = (want_split && (long long)P->B * (1 + nbp) <= 240) ? nbp : 0;
     u64* slots = reinterpret_cast<u64*>(ws + L.slots);
     // bound of the main workgroup's wait for each plane slot (polls of ~0.1 us); the plane
     // workgroups are co-resident by construction, so it only trips on a broken launch --

@@ -41,6 +41,17 @@ extern "C" {
 #define CODEC_FLAG_LOSSY 2u     /* segments do not tile the payload (T < s, clamp) */
 #define CODEC_FLAG_BADLUT 4u    /* log2 table shorter than H*W (status error)      */
 #define CODEC_FLAG_DECIDE_TIMEOUT 8u /* split decision: a plane workgroup never reported (status 2) */
+/* The s decision is guard-banded.  Since every bit plane X is a function of the
+ * image Y, I(X;Y) = H(X) exactly, and the reference's MI (codec.py:554) differs from H(X) only
+ * by the rounding of its numpy-order sums (~1e-13 at most).  Unless all_mi is set, s is
+ * decided from the cumulative H(X) against beta * H(Y) when every prefix of that walk lies
+ * more than 1e-9 from its target -- the same s as the reference's loop -- and the slice
+ * records CODEC_FLAG_INFO_FAST: mi[] holds H(X) of the planes the loop evaluated and cum_info
+ * their sum (entropy and target stay numpy-exact).  A slice with a prefix inside the band is
+ * decided by the exact numpy-order sums (mi[], cum_info exact) and records
+ * CODEC_FLAG_GUARD_FALLBACK.  all_mi = 1 always takes the exact sums. */
+#define CODEC_FLAG_INFO_FAST 16u
+#define CODEC_FLAG_GUARD_FALLBACK 32u
 
 /* Call parameters (one batch: all slices share shape and dtype). */
 typedef struct codec_params {
@@ -97,6 +108,13 @@ typedef struct codec_slice_meta {
 
 int codec_abi_version(void);
 const char* codec_last_error(void);
+/* Tuning switch of the A/B knobs.  Every launch-shape choice (scan sweep, ring depths, store
+ * policy, decision path, ...) has a measured default.  The CODEC_* environment variables that
+ * override them are honoured only while this switch is on: CODEC_TUNING=1 in the
+ * environment when the library is loaded (read once), or codec_set_tuning(1).  With it off --
+ * the default -- no call reads the environment.  The fault-injection knobs additionally need
+ * CODEC_DEBUG=1.  Returns the previous setting.  No reference counterpart. */
+int codec_set_tuning(int32_t on);
 /* SHA-256 (hex) of the sources, headers and compiler flags this library was built from
  * (codec_tcc_amd/build.py); the Python loader refuses an in-tree library whose digest differs
  * from the tree's.  No reference counterpart (build integrity only). */

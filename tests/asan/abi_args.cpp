@@ -108,6 +108,11 @@ int main() {
 
     if (codec_abi_version() != 1) { fprintf(stderr, "FAIL abi version\n"); return 2; }
     if (!codec_last_error()) { fprintf(stderr, "FAIL last_error NULL\n"); return 2; }
+    {   // the knobs' tuning switch returns the previous setting (the bad-argument checks below
+        // run with it on, so every knob-reading branch is driven too)
+        const int was = codec_set_tuning(1);
+        if (codec_set_tuning(1) != 1 || (was != 0 && was != 1)) { fprintf(stderr, "FAIL tuning switch\n"); return 2; }
+    }
 
     // ---------------------------------------------------------------- LSB path
     EXPECT_ZERO(codec_workspace_bytes(nullptr));

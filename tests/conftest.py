@@ -6,6 +6,10 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
+# the suite drives the A/B and fault-injection knobs through the environment: turn the
+# library's tuning switch on before it is loaded (it is read once, at load; the product
+# default is off -- tests/test_gpu_api.py::test_knobs_ignored_without_tuning checks that)
+os.environ.setdefault("CODEC_TUNING", "1")
 
 
 def pytest_configure(config):

@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 import golden_io
-from codec_tcc_amd import Codec, framing, synth
+from codec_tcc_amd import Codec, _lib, framing, synth
 from codec_tcc_amd import codec as K
 from oracle import ref_cpu as R
 
@@ -17,13 +17,14 @@ torch = pytest.importorskip("torch")
 CASES = [c for c in golden_io.cases() if str(c["embedder"]) in ("hybrid", "multi")]
 
 
-def _run_case(case):
+def _run_case(case, all_mi=True, beta=None):
     cover = case["cover"]
     h, w = cover.shape
     nb = int(case["nbits"])
     nbits = None if nb < 0 else nb
-    codec = Codec(1, h, w, dtype=str(cover.dtype), beta=float(case["beta"]), block=int(case["sb"]),
-                  align=bool(case["align"]), mode=str(case["embedder"]), nbits=nbits, all_mi=True)
+    beta = float(case["beta"]) if beta is None else beta
+    codec = Codec(1, h, w, dtype=str(cover.dtype), beta=beta, block=int(case["sb"]),
+                  align=bool(case["align"]), mode=str(case["embedder"]), nbits=nbits, all_mi=all_mi)
     bitstr = str(case["bits"])
     bits = (np.frombuffer(bitstr.encode(), np.uint8) - 48) if bitstr else np.zeros(0, np.uint8)
     enc = codec.encode(torch.from_numpy(cover[None].copy()).cuda(), [bits])
@@ -43,6 +44,8 @@ def decide_path(request, monkeypatch):
     the separate kernels)."""
     if request.param == "fused":
         monkeypatch.setenv("CODEC_FUSED_DECIDE", "2")
+    if request.param == "split":   # plane workgroups also without all_mi (default: all_mi only)
+        monkeypatch.setenv("CODEC_DECIDE_SPLIT", "2")
     if request.param == "waves":
         monkeypatch.setenv("CODEC_DECIDE_SPLIT", "0")
     if request.param == "block":
@@ -51,9 +54,35 @@ def decide_path(request, monkeypatch):
     return request.param
 
 
+def _ref_loop(mis, entropy, beta):
+    """The reference's decision loop (codec.py:580-593) run on the reference's own float64
+    MI values and entropy (the golden tables): s and cumulative_info."""
+    tg = beta * entropy
+    c = 0.0
+    for i, mi in enumerate(mis):
+        c += mi
+        if c >= tg:
+            return i + 1, c
+    return 1, c
+
+
+def _ref_evaluated(mis, entropy, beta):
+    """How many planes the reference's loop evaluates (all of them when it never breaks)."""
+    tg = beta * entropy
+    c = 0.0
+    for i, mi in enumerate(mis):
+        c += mi
+        if c >= tg:
+            return i + 1
+    return len(mis)
+
+
+@pytest.mark.parametrize("all_mi", [True, False], ids=["exact_mi", "guarded"])
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
-def test_golden_case(case, decide_path):
-    codec, enc = _run_case(case)
+def test_golden_case(case, decide_path, all_mi):
+    """all_mi: every plane's MI by the numpy-order sums (bit-exact); guarded: the default
+    guard-banded decision -- same s and outputs, mi[] = H(X) of the evaluated planes."""
+    codec, enc = _run_case(case, all_mi=all_mi)
     m = enc.records()[0]
     s = int(case["s"])
     assert m.status == 0
@@ -64,7 +93,18 @@ def test_golden_case(case, decide_path):
     # bit-exact float64 information values (calculate_entropy / calculate_mutual_information)
     assert m.entropy == float(case["entropy"])
     nb = len(case["mi"])
-    assert [m.mi[i] for i in range(nb)] == list(case["mi"])
+    if all_mi or int(case.get("fixed_s", 0)) > 0:
+        assert [m.mi[i] for i in range(nb)] == list(case["mi"])
+        assert not (m.flags & (_lib.FLAG_INFO_FAST | _lib.FLAG_GUARD_FALLBACK))
+    elif m.flags & _lib.FLAG_INFO_FAST:
+        assert not (m.flags & _lib.FLAG_GUARD_FALLBACK)
+        ev = _ref_evaluated(list(case["mi"]), float(case["entropy"]), float(case["beta"]))
+        for i in range(nb):   # H(X) vs the reference's h_x + h_y - h_xy: rounding only
+            assert abs(m.mi[i] - float(case["mi"][i])) <= 1e-12 if i < ev else m.mi[i] == 0.0, i
+    else:   # inside the guard band: the exact sums decided
+        assert m.flags & _lib.FLAG_GUARD_FALLBACK
+        ev = _ref_evaluated(list(case["mi"]), float(case["entropy"]), float(case["beta"]))
+        assert [m.mi[i] for i in range(ev)] == list(case["mi"])[:ev]
     # stego pixels
     exp = golden_io.stego(case)
     got = enc.stego.cpu().numpy()[0]
@@ -449,3 +489,46 @@ def test_maps_fully_defined(fused, monkeypatch):
     a = codec.encode(covers, pl, maps=torch.full((B, pl.map_words), -1, dtype=torch.int64, device=covers.device))
     z = codec.encode(covers, pl, maps=torch.zeros((B, pl.map_words), dtype=torch.int64, device=covers.device))
     assert torch.equal(a.maps, z.maps) and torch.equal(a.stego.view(torch.int16), z.stego.view(torch.int16))
+
+
+GUARD_CASES = [c for c in CASES if str(c["embedder"]) == "hybrid" and int(c["nbits"]) < 0 and float(c["beta"]) > 0
+               and not bool(c["align"])]
+GUARD_CASES = list({str(c["image_key"]) + str(c["cover"].shape): c for c in GUARD_CASES}.values())[:6]
+
+
+@pytest.mark.parametrize("case", GUARD_CASES, ids=[c["name"] for c in GUARD_CASES])
+def test_guard_band_ties_fall_back_to_reference_s(case, decide_path):
+    """beta set so that beta * H(Y) lands on (and one ulp either side of)
+    a prefix sum of the reference's own MI values -- inside the guard band, so the exact
+    numpy-order sums must decide, and s must be the reference loop's on its own floats
+    (codec.py:580-593 over the golden MI table).  Far from a tie the fast route decides."""
+    mis = [float(x) for x in case["mi"]]
+    H = float(case["entropy"])
+    cover = case["cover"]
+    ncheck = 0
+    c = 0.0
+    for k in range(min(len(mis), 6)):
+        c += mis[k]
+        if c <= 0.0:
+            continue
+        b0 = c / H
+        for beta in (b0, float(np.nextafter(b0, 0.0)), float(np.nextafter(b0, 2.0))):
+            _, enc = _run_case(case, all_mi=False, beta=beta)
+            m = enc.records()[0]
+            s_ref, cum_ref = _ref_loop(mis, H, beta)
+            assert m.status == 0
+            assert m.s == s_ref, (k, beta)
+            assert m.flags & _lib.FLAG_GUARD_FALLBACK, (k, beta)
+            assert not (m.flags & _lib.FLAG_INFO_FAST)
+            assert m.cum_info == cum_ref, (k, beta)
+            ev = _ref_evaluated(mis, H, beta)
+            assert [m.mi[i] for i in range(ev)] == mis[:ev]
+            ncheck += 1
+    assert ncheck >= 3
+    # midway between two prefix sums: far from any tie, decided without the joint sums
+    c0, c1 = mis[0], mis[0] + mis[1]
+    if c1 - c0 > 1e-6:
+        beta = (c0 + c1) / 2 / H
+        _, enc = _run_case(case, all_mi=False, beta=beta)
+        m = enc.records()[0]
+        assert m.flags & _lib.FLAG_INFO_FAST and m.s == _ref_loop(mis, H, beta)[0] == 2

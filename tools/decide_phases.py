@@ -4,6 +4,7 @@
 its term scratch) and prints median per-phase microseconds over the batch.
     hipcc ... -DDECIDE_TS ... -o tools/bin/libcodec_hip_dts.so && python tools/decide_phases.py"""
 import os
+os.environ.setdefault("CODEC_TUNING", "1")   # the library honours CODEC_* knobs only under this switch
 import sys
 
 import numpy as np

@@ -8,6 +8,7 @@ three paths give identical stego / location maps / payload / restored cover.
 import argparse
 import json
 import os
+os.environ.setdefault("CODEC_TUNING", "1")   # the library honours CODEC_* knobs only under this switch
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -1,4 +1,5 @@
 #!/bin/bash
+export CODEC_TUNING=1   # CODEC_* knobs are honoured only under the tuning switch
 # cache-policy A/B: the in-tree library (non-temporal vector loads and stores where the kernels
 # ask for them) against builds with plain stores / plain loads, alternating processes on one box
 #   bash tools/r05/build_variant.sh tools/r05/lib_pst.so -DCODEC_PLAIN_STORES=1

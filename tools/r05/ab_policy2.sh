@@ -1,4 +1,5 @@
 #!/bin/bash
+export CODEC_TUNING=1   # CODEC_* knobs are honoured only under the tuning switch
 # per-kernel cache policies (in-tree library, runtime knobs): the in-place slice-serial PEE
 # passes' loads/stores (CODEC_PEE_IP_NTL / CODEC_PEE_IP_NTS) and C3's k_restore_il stores
 # (CODEC_RIL_NTS), interleaved in one process; then the PEE and config GPU tests

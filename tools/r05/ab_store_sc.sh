@@ -1,4 +1,5 @@
 #!/bin/bash
+export CODEC_TUNING=1   # CODEC_* knobs are honoured only under the tuning switch
 # write-through (sc1 / sc0 sc1) instead of non-temporal 16-B stores, alternating processes:
 #   bash tools/r05/build_variant.sh tools/r05/lib_sc1.so -DCODEC_ST_SC=1
 #   bash tools/r05/build_variant.sh tools/r05/lib_sc01.so -DCODEC_ST_SC=3

@@ -1,4 +1,5 @@
 #!/bin/bash
+export CODEC_TUNING=1   # CODEC_* knobs are honoured only under the tuning switch
 # wave scan by DPP (in-tree) vs ds_bpermute shuffles (lib_old.so: -DCODEC_WSCAN_DPP=0):
 # MED-PEE headline and C3 (tune_pee.py), LSB at C3 / C2 / headline (tune.py)
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 9

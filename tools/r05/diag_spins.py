@@ -2,6 +2,7 @@
 CODEC_DEBUG=1 CODEC_PEE_LB_SPINS=<n> (tiny spin bound: most waits fall back) for the embed and
 the extract, compared bit for bit with the default run."""
 import os
+os.environ.setdefault("CODEC_TUNING", "1")   # the library honours CODEC_* knobs only under this switch
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))

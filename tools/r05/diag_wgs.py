@@ -2,6 +2,7 @@
 bench_pee's round trip at the headline shape, with the fields that decide roundtrip_ok."""
 import json
 import os
+os.environ.setdefault("CODEC_TUNING", "1")   # the library honours CODEC_* knobs only under this switch
 import sys
 import types
 

@@ -1,6 +1,7 @@
 """Which pass goes wrong under a persistent grid (CODEC_PEE_1P_WGS) at the headline shape:
 embed with the knob vs the default embed (stego / meta / map, per slice), then each extract."""
 import os
+os.environ.setdefault("CODEC_TUNING", "1")   # the library honours CODEC_* knobs only under this switch
 import sys
 
 import numpy as np

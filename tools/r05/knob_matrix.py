@@ -4,6 +4,7 @@ after the persistent-grid bug): each configuration's embed (stego, meta, map) an
 place.  DIAG_B slices of 2048^2 ct12, T = 2, 1 KB payloads."""
 import json
 import os
+os.environ.setdefault("CODEC_TUNING", "1")   # the library honours CODEC_* knobs only under this switch
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))

@@ -4,6 +4,7 @@ the default run's bit for bit, at the headline slice size (DIAG_B x 2048^2) and 
 ct12 slices, 1 KB payloads."""
 import json
 import os
+os.environ.setdefault("CODEC_TUNING", "1")   # the library honours CODEC_* knobs only under this switch
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))

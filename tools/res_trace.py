@@ -6,6 +6,7 @@ CODEC_PEE_RES_TRACE=1 run.
     CODEC_PEE_RES_TRACE=1 python3 tools/res_trace.py"""
 import ctypes as C
 import os
+os.environ.setdefault("CODEC_TUNING", "1")   # the library honours CODEC_* knobs only under this switch
 import sys
 
 import numpy as np

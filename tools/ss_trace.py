@@ -8,6 +8,7 @@ pixels have arrived), t2 after the scan barrier, t3 after the stores + refill ar
 Prints cycles (s_memtime) per phase."""
 import ctypes as C
 import os
+os.environ.setdefault("CODEC_TUNING", "1")   # the library honours CODEC_* knobs only under this switch
 import subprocess
 import sys
 

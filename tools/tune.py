@@ -7,6 +7,7 @@ import argparse
 import ctypes as C
 import json
 import os
+os.environ.setdefault("CODEC_TUNING", "1")   # the library honours CODEC_* knobs only under this switch
 import sys
 
 import numpy as np

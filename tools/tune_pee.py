@@ -7,6 +7,7 @@ Prints, per configuration and mode, the median per-kernel HIP-event times over r
 import argparse
 import json
 import os
+os.environ.setdefault("CODEC_TUNING", "1")   # the library honours CODEC_* knobs only under this switch
 import sys
 import types
 
