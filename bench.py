@@ -180,6 +180,25 @@ def _timed_loop(fn, budget_s):
     return px, n, t_work
 
 
+def _cgroup_cpu_quota():
+    """CPU quota of this process's cgroup in cores (cgroup v2 cpu.max / v1 cfs files), or None
+    when unlimited or unreadable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = float(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = float(f.read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
 def _affinity():
     """Host cores this process may run on (sorted)."""
     try:
@@ -248,14 +267,19 @@ def _pool_job(job):
 
 
 def cpu_baseline_pool(args, which: str, per_worker: int = 0):
-    """The same oracle work over a process pool (one worker per host core of
-    this GPU's share), each worker pinned to its own core.  The pool has
-    min(len(sched_getaffinity), --cpu-pool) workers: the affinity set on the GPU box can be
-    the whole machine while this GPU's share is 16 cores (--cpu-pool).  Forked BEFORE the GPU
-    is initialised in this process; the covers are generated in the parent first, so the
-    wall clock holds the fork and the oracle work."""
+    """The same oracle work over a process pool (one worker per host core),
+    each worker pinned to its own core.  The pool has min(len(sched_getaffinity), cgroup CPU
+    quota, --cpu-pool) workers: on the GPU box the affinity set is the whole machine (256
+    cores) while the pool's rules give one GPU's job a 16-core share (--cpu-pool 16), so a
+    whole-machine pool would time-slice 256 workers on that share.  The whole-host figure is
+    therefore reported beside it as an extrapolation (`host_extrapolated`: the pool's per-core
+    rate x the cores in the affinity set), labelled as such.  Forked BEFORE the GPU is
+    initialised in this process; the covers are generated in the parent first, so the wall
+    clock holds the fork and the oracle work."""
     cores = _affinity()
-    workers = max(1, min(len(cores), int(args.cpu_pool)))
+    quota = _cgroup_cpu_quota()
+    usable = len(cores) if quota is None else max(1, min(len(cores), int(quota)))
+    workers = max(1, min(usable, int(args.cpu_pool)))
     per_worker = per_worker or (40 if which == "pee" else 4)   # ~2 s of oracle work per worker
     for i in range(CPU_DISTINCT):
         _cpu_img(args.size, args.kind, i)
@@ -265,12 +289,18 @@ def cpu_baseline_pool(args, which: str, per_worker: int = 0):
         res = pool.map(_pool_job, jobs, chunksize=1)
     wall = time.perf_counter() - t0
     px = sum(r[0] for r in res)
-    return {"value": round(px / wall / 1e6, 3), "unit": "Mpixels/s", "cores": workers, "kind": "port",
+    rate = px / wall / 1e6
+    return {"value": round(rate, 3), "unit": "Mpixels/s", "cores": workers, "kind": "port",
             "sample": f"{len(jobs)} x {args.size}x{args.size} {args.kind} slices ({which} oracle) over a "
                       f"{workers}-process pool, one core per worker (fork; {CPU_DISTINCT} distinct covers "
                       f"generated beforehand), wall clock",
             "seconds": round(wall, 2), "cpu_model": _cpu_model(), "cores_available": len(cores),
-            "pinned_cores": cores[:workers]}
+            "cgroup_cpu_quota": quota, "per_gpu_share_cores": int(args.cpu_pool),
+            "pinned_cores": cores[:workers],
+            # NOT a measurement: the pool's per-core rate scaled to every core of the affinity
+            # set (the oracle slices are independent, one per core: linear up to memory bandwidth)
+            "host_extrapolated": {"value": round(rate / workers * len(cores), 1), "cores": len(cores),
+                                  "basis": "pool per-core rate x cores_available (extrapolated, not run)"}}
 
 
 # ------------------------------------------------------------------ helpers
@@ -480,6 +510,7 @@ def bench_pee(args, torch, dist, world, rank, dev, covers, B, H, W, *, inplace=F
         res["value"] = round(prefix_px * world * steps / el / 1e6, 1)
         res["value_basis"] = ("pixels read up to each slice's `end` (items of 8 px x 2 rows); nominal_mpx_s "
                               "counts every pixel of the batch")
+        res["touched_fraction"] = round(prefix_px / (B * H * W), 4)
         res["prefix_pixels_per_step"] = int(prefix_px)
         if emb in ("k_pee_embed_res", "k_pee_embed_ss_auto", "k_pee_embed_ss", "k_pee_embed1") and kern[emb] > 0:
             res["roofline"] = _roof(emb, by, kern[emb], traffic(emb))
@@ -597,8 +628,13 @@ def bench_lsb_inplace(args, torch, dist, world, dev, covers, B, H, W):
     cover_ok = bool(torch.equal(work.view(torch.int16), covers.view(torch.int16)))
     pay_ok = payload_equal(pay, pl.words, [r.total_used for r in recs])
     status_ok = all(r.status == 0 for r in recs)
+    written = sum(r.total_used for r in recs)
     res = {"value": round(B * H * W * world * args.steps / el / 1e6, 1), "unit": "Mpixels/s",
            "ms_per_step": round(el / args.steps * 1e3, 4), "roundtrip_ok": cover_ok and pay_ok and status_ok,
+           # every pixel is READ (the decision's histogram/block scan, k_scan_read); only the
+           # payload windows are written (embed) and rewritten (restore)
+           "value_basis": "pixels read (the whole cover: the scan); written pixels are the windows only",
+           "touched_fraction": 1.0, "written_fraction": round(2 * written / (B * H * W), 6),
            "kernels_ms": {k: round(v, 4) for k, v in kern.items()}}
     rk = next((k for k in ("k_scan_rows_read", "k_scan_read") if k in kern), None)
     if rk:   # read-only pass over the cover

@@ -249,57 +249,66 @@ __device__ double np_sum_block1024(const F& f, int m, double* vals /*[1024]*/) {
     return np_tree_combine1024(m, vals);
 }
 
+// np_sum_block1024's leaves alone (no barrier): slot sums into vals[chunk * 128 + slot]
+template <class F>
+__device__ __forceinline__ void np_leaves_block1024(const F& f, int m, double* vals, int wrot = 0) {
+    const int t = threadIdx.x;
+    const int lane = t & 63, wv = ((t >> 6) + wrot) & 15, q = lane & 7;   // wave w takes slots of (w + wrot) % 16
+    const int nchunks_ = (m + NP_CHUNK - 1) / NP_CHUNK;
+    for (int rnd = 0; rnd < nchunks_; ++rnd) {
+        const int slot = rnd * 128 + wv * 8 + (lane >> 3);
+        const int cs = rnd * NP_CHUNK;
+        const int rr = min(NP_CHUNK, max(0, m - cs));
+        int a = 0, n = 0;
+        if (rr > 0) n = np_node_size(rr, 7, slot & 127, &a);
+        a += cs;
+        const int lim = n - (n % 8);
+        double tv[NP_LEAF / 8];
+#pragma unroll
+        for (int u = 0; u < NP_LEAF / 8; ++u) tv[u] = (8 * u < lim) ? f(a + 8 * u + q) : 0.0;
+        double acc = 0.0;
+        if (n >= 8) {
+            acc = tv[0];
+#pragma unroll
+            for (int u = 1; u < NP_LEAF / 8; ++u)
+                if (8 * u < lim) acc += tv[u];
+        }
+        const double s2 = acc + __shfl_xor(acc, 1, 64);
+        const double s4 = s2 + __shfl_xor(s2, 2, 64);
+        const double s8 = s4 + __shfl_xor(s4, 4, 64);
+        if (q == 0) {
+            double res;
+            if (n >= 8) {
+                res = s8;
+                for (int i = lim; i < n; ++i) res += f(a + i);
+            } else {
+                res = -0.0;
+                for (int i = 0; i < n; ++i) res += f(a + i);
+            }
+            vals[slot] = n > 0 ? res : 0.0;
+        }
+    }
+}
+
+// the chunk trees over np_leaves_block1024's slot sums, re-added by ONE wave with shuffles
+// (after a barrier that orders the slot stores); the sum, valid in that wave
+__device__ __forceinline__ double np_combine_slots_wave(int m, const double* vals) {
+    const int lane = threadIdx.x & 63;
+    double res = -0.0;
+    for (int cs = 0; cs < m; cs += NP_CHUNK) {
+        const int c = cs / NP_CHUNK;
+        res += np_combine_wave(vals[c * 128 + lane], vals[c * 128 + 64 + lane], min(NP_CHUNK, m - cs));
+    }
+    return res;
+}
+
 // np_sum_block1024's leaves, then wave 0 alone re-adds the chunk trees with shuffles (no
 // block barriers: 14 fewer than np_tree_combine1024).  The sum is valid in wave 0 only.
 template <class F>
 __device__ double np_sum_block1024_w0(const F& f, int m, double* vals /*[1024]*/) {
-    const int t = threadIdx.x;
-    {
-        const int lane = t & 63, wv = t >> 6, q = lane & 7;
-        const int nchunks_ = (m + NP_CHUNK - 1) / NP_CHUNK;
-        for (int rnd = 0; rnd < nchunks_; ++rnd) {
-            const int slot = rnd * 128 + wv * 8 + (lane >> 3);
-            const int cs = rnd * NP_CHUNK;
-            const int rr = min(NP_CHUNK, max(0, m - cs));
-            int a = 0, n = 0;
-            if (rr > 0) n = np_node_size(rr, 7, slot & 127, &a);
-            a += cs;
-            const int lim = n - (n % 8);
-            double tv[NP_LEAF / 8];
-#pragma unroll
-            for (int u = 0; u < NP_LEAF / 8; ++u) tv[u] = (8 * u < lim) ? f(a + 8 * u + q) : 0.0;
-            double acc = 0.0;
-            if (n >= 8) {
-                acc = tv[0];
-#pragma unroll
-                for (int u = 1; u < NP_LEAF / 8; ++u)
-                    if (8 * u < lim) acc += tv[u];
-            }
-            const double s2 = acc + __shfl_xor(acc, 1, 64);
-            const double s4 = s2 + __shfl_xor(s2, 2, 64);
-            const double s8 = s4 + __shfl_xor(s4, 4, 64);
-            if (q == 0) {
-                double res;
-                if (n >= 8) {
-                    res = s8;
-                    for (int i = lim; i < n; ++i) res += f(a + i);
-                } else {
-                    res = -0.0;
-                    for (int i = 0; i < n; ++i) res += f(a + i);
-                }
-                vals[slot] = n > 0 ? res : 0.0;
-            }
-        }
-    }
+    np_leaves_block1024(f, m, vals);
     __syncthreads();
-    double res = -0.0;
-    if (t < 64) {
-        for (int cs = 0; cs < m; cs += NP_CHUNK) {
-            const int c = cs / NP_CHUNK;
-            res += np_combine_wave(vals[c * 128 + t], vals[c * 128 + 64 + t], min(NP_CHUNK, m - cs));
-        }
-    }
-    return res;
+    return threadIdx.x < 64 ? np_combine_slots_wave(m, vals) : -0.0;
 }
 
 // ---- wide slices (k_decide's walk path): the non-zero bins of a slice are kept as 64-bin
@@ -1286,9 +1295,18 @@ struct FusedScan {
     uint32_t orv;
     u64 key;
     bool lds_ok;
+    // the decision's global inputs, loaded before the scan (their latency hides under it):
+    // the slice's layout class, this thread's int of the class's 16 layouts, its payload word
+    int cls;
+    int32_t lay_v;
+    u64 pay_v;
 };
 
-template <typename T, bool EMBED>
+// FUSEDK (k_scan_decide): the wave-parallel exact MI rounds are compiled out -- a slice the
+// guard band sends to the exact sums (or all_mi / fixed_s there) runs the block-sequential
+// sums over the LDS terms instead -- so the fused kernel carries the register pressure of the
+// scan and the fast decision only
+template <typename T, bool EMBED, bool FUSEDK = false>
 __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const FusedScan* fz, const int b, const int role,
                                             codec_params P,
                                             uint32_t* __restrict__ ghist_all, uint32_t* __restrict__ gor,
@@ -1330,21 +1348,24 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     DTS(0);
     if (role > 0) PTS(0);
     // the scan's block key, loaded now (used by the offset argmax after the decision)
-    // (thread 0, and wave 13's lane 0: the paired MI round finds the offset on that idle wave)
-    const bool keyed = (t == 0 || t == 832) && role == 0 && fast_blocks && P.fixed_offset < 0 && P.mode == CODEC_MODE_HYBRID;
+    // (thread 0, and lane 0 of waves 2 and 13: the fast decision / the paired MI round find the
+    // offset on those idle waves)
+    const bool keyed = (t == 0 || t == 128 || t == 832) && role == 0 && fast_blocks && P.fixed_offset < 0 && P.mode == CODEC_MODE_HYBRID;
     const u64 key0 = keyed ? (fz ? fz->key : gkey[b]) : 0ull;
     // the slice's layout class (its layout for s is loaded once s is known)
     constexpr int kLayW = (int)(sizeof(codec_layout) / 4);
     static_assert(16 * kLayW <= 1024, "one int of the class's layouts per thread");
-    const int cls = role == 0 ? slice_class[b] : 0;
+    const int cls = fz ? fz->cls : role == 0 ? slice_class[b] : 0;
     const int32_t* lay_all = reinterpret_cast<const int32_t*>(table + (size_t)cls * 16);
     // fused embed: the slice's payload words (<= 2 KiB) go to LDS now, read by the embed
     // loop after the decision instead of one dependent global load per bit
     constexpr int kPaySh = EMBED ? 256 : 1;
     auto& pay_sh = S.pay_sh;
     const bool pay_in_lds = EMBED && E.pw <= kPaySh;
-    if (EMBED && pay_in_lds && role == 0)
-        for (int w = t; w < E.pw; w += 1024) pay_sh[w] = E.payload[(size_t)b * E.pw + w];
+    static_assert(kPaySh <= 1024, "one payload word per thread");
+    // requested now, parked in LDS just before the windows: a store here would hold the
+    // workgroup until the load returns (one global round trip ahead of pass 1)
+    const u64 pay_v = fz ? fz->pay_v : (EMBED && pay_in_lds && role == 0 && t < E.pw) ? E.payload[(size_t)b * E.pw + t] : 0ull;
     // ---- bins that can be non-zero: [0, Rp), Rp = next power of two above OR(pixels)
     const uint32_t orv = fz ? fz->orv : gor[b];
     int Rp = orv ? (1 << (32 - __clz((int)orv))) : 1;
@@ -1404,12 +1425,27 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     // free until the sums) for the terms pass, instead of a second histogram round trip
     uint32_t* cnt_sh = reinterpret_cast<uint32_t*>(vals);
     const bool cnt_lds = !wide && Rp <= (int)(sizeof(vals) / 4);
+    // <= 8 bins per thread (Rp <= 8192: every 12-bit slice): the counts stay in registers and
+    // their log2 table entries are requested at once, so that the table round trip runs under
+    // the rank scan instead of after it
+    const bool lut_pre = !wide && bpt <= 8 && lut_len >= npx;
+    uint32_t c8[8];
+    double l8[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { c8[u] = 0u; l8[u] = 0.0; }
     for (int k0 = 0; k0 < bpt && !wide; k0 += 16) {
         uint32_t cc[16];
 #pragma unroll
         for (int u = 0; u < 16; ++u) {            // 16 loads in flight, then the adds
             const int v = v0 + k0 + u;
             cc[u] = (k0 + u < bpt && v < Rp) ? (flds ? (flds[v >> 1] >> (16 * (v & 1))) & 0xFFFFu : hist[v]) : 0u;
+        }
+        if (lut_pre) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                c8[u] = cc[u];
+                if (cc[u]) l8[u] = lut[cc[u] - 1];
+            }
         }
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
@@ -1425,7 +1461,9 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     DTS(12);
     // the entry prefetches are consumed here, with pass 1's loads (issued before them, so
     // no extra wait): left to themselves they sink to their first use after the decision
-    asm volatile("" ::"v"((uint32_t)key0), "v"((uint32_t)(key0 >> 32)), "s"(cls));
+    if (!fz) asm volatile("" ::"v"((uint32_t)key0), "v"((uint32_t)(key0 >> 32)), "s"(cls));
+    // the class's 16 layouts (one int per thread), requested now, stored into LDS after the terms
+    const int32_t lay_v = fz ? fz->lay_v : (role == 0 && t < 16 * kLayW) ? lay_all[t] : 0;
     if (t < 16) pops_sh[t] = 0;
     uint32_t m;
     const uint32_t rank0 = block_excl_scan<1024>((uint32_t)__popcll(nzmask), sh, &m);
@@ -1458,7 +1496,9 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     const size_t off_jl = off_pm + (size_t)ngrp * 128;
     const int wplanes = (m > 1 && off_jl + 2 * (size_t)m <= arena) ? (int)min((size_t)16, (arena - off_jl) / (2 * (size_t)m)) : 0;
     const bool wfast = lut_ok && wplanes >= 1 && knob_dev_decide_fast(P);
-    const bool walk = wide && lut_ok && !wfast && m > 1;
+    // (compiled out of the fused kernel: a wide slice there sums its terms from global memory
+    // on the block path -- with the guard band that is H(Y) alone for nearly every slice)
+    const bool walk = !FUSEDK && wide && lut_ok && !wfast && m > 1;
     double* tl = reinterpret_cast<double*>(list);
     uint16_t* rv = reinterpret_cast<uint16_t*>(tl + (wfast ? m : 0));
     u64* pm = reinterpret_cast<u64*>(reinterpret_cast<char*>(list) + off_pm);
@@ -1469,7 +1509,18 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     const bool try_fast = P.fixed_s <= 0 && !P.all_mi && lut_ok && !(P.reserved & 8);
     double hy_part = 0.0;
     // terms of the non-zero bins in ascending value order, computed once
-    if (lut_ok && !walk) {
+    if (lut_ok && !walk && lut_pre) {   // from pass 1's registers: bin v0 + u has rank rank0 + (set bits below u)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if ((nzmask >> u) & 1ull) {
+                const uint32_t r = rank0 + (uint32_t)__popcll(nzmask & ((1ull << u) - 1ull));
+                const double tt = ((double)c8[u] / Nd) * l8[u];      // plogp: p * log2(p)
+                terms[r] = tt;
+                hy_part += tt;
+                if (wfast) rv[r] = (uint16_t)(v0 + u);
+            }
+        }
+    } else if (lut_ok && !walk) {
         uint32_t r = rank0;
         u64 msk = nzmask;
         while (msk) {
@@ -1497,6 +1548,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
             r += k;
         }
     }
+    if (try_fast) DTS(8);
     if (try_fast && walk) {   // wide slices: no term array -- the count codes of pass 1, a wave per group
         const int lane = t & 63, wv = t >> 6, ng = Rp / 64;
         for (int g0 = wv; g0 < ng; g0 += 16 * 8) {
@@ -1527,39 +1579,99 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     int fs = 0;               // uniform: s of the fast decision, 0 = the exact path decides
     bool guard_fb = false;    // uniform: the guard band sent the slice to the exact path
     double fast_cum = 0.0;    // thread 0
+    // the start offset (codec.py:441-453; independent of s): find_offset below, or one wave's
+    // shuffles (wave_offset) where a wave is idle meanwhile
+    const int sb = P.block;
+    const int nbx = (P.W + sb - 1) / sb;
+    double bsc = -1.0;
+    int bix = 0x7FFFFFFF;
+    bool offset_done = false;
+    const bool need_offset = P.fixed_offset < 0 && P.mode == CODEC_MODE_HYBRID;
+    // first maximal float(np.var) block in raster order: the exact scores of the partial /
+    // non-power-of-two blocks and the scan's packed key (lane 0 holds it), reduced by the calling
+    // wave alone (score desc, raster index asc) into best_sc[0] / best_ix[0]
+    auto wave_offset = [&]() {
+        const int lane = t & 63;
+        double ws = -1.0;
+        int wi = 0x7FFFFFFF;
+        const int cnt = exact_count(P.H, P.W, sb, exact_edge_only);
+        for (int e = lane; e < cnt; e += 64) {
+            int by, bx;
+            exact_block(e, P.H, P.W, sb, exact_edge_only, &by, &bx);
+            const double sc = exact[(size_t)b * exact_cap + e];
+            const int ix = by * nbx + bx;
+            if (sc > ws || (sc == ws && ix < wi)) { ws = sc; wi = ix; }
+        }
+        if (lane == 0 && fast_blocks && key0) {
+            const uint32_t score = (uint32_t)(key0 >> 32);
+            const int ix = (int)(0xFFFFFFFFu - (uint32_t)(key0 & 0xFFFFFFFFu));
+            const double sc = (double)score / ((double)sb * sb * (double)sb * sb);
+            if (sc > ws || (sc == ws && ix < wi)) { ws = sc; wi = ix; }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const double os = __shfl_xor(ws, o, 64);
+            const int oi = __shfl_xor(wi, o, 64);
+            if (os > ws || (os == ws && oi < wi)) { ws = os; wi = oi; }
+        }
+        if (lane == 0) { best_sc[0] = ws; best_ix[0] = wi; }
+    };
+    // the record's exact H(Y) (numpy's order, 8 lanes per leaf over the whole workgroup, slot
+    // sums in vals[512..], clear of the layouts) and the offset ride along with the fast
+    // decision on the wave path, so a settled slice goes straight to its windows
+    const bool pre = try_fast && wfast && role == 0;
     if (try_fast) {
         const int lane = t & 63, wv = t >> 6;
+        if (pre) {
+            if (t < 16 * kLayW) reinterpret_cast<int32_t*>(vals)[t] = lay_v;   // the class's 16 layouts (one per s)
+            np_leaves_block1024(RankTerm{tl}, (int)m, vals + 512, 8);   // waves 8.. (clear of waves 0-2)
+        }
         double hp = hy_part;
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) hp += __shfl_xor(hp, o, 64);
         if (lane == 0) hxy_sh[wv] = hp;           // scratch until the exact rounds
         const int nb = min(P.nbits, 16);
-        if (wv == 1 && lane < nb) {   // H(X) of every plane, log2 on the device (no table round trip)
+        double hx = 0.0;                          // wave 1, lane i: H(X) of plane i
+        if (wv == 1 && lane < nb) {   // codec.py:530-532; log2 on the device (no table round trip)
             const uint32_t pp = pops_sh[lane];
             const double p1 = (double)pp / Nd, p0 = (double)(npx - pp) / Nd;
-            hx_sh[lane] = (pp != 0 && (long long)pp != npx) ? -(p0 * log2(p0) + p1 * log2(p1)) : 0.0;
+            hx = (pp != 0 && (long long)pp != npx) ? -(p0 * log2(p0) + p1 * log2(p1)) : 0.0;
         }
+        DTS(6);
         __syncthreads();
-        if (t == 0) {
-            double hyf = 0.0;
-            for (int w = 0; w < 16; ++w) hyf += hxy_sh[w];
-            const double tg = P.beta * -hyf;
-            double c = 0.0;
-            bool clear = true;    // every prefix's |cum - target| > guard (false on NaN too)
-            int sf = 1, nev = nb;
-            for (int i = 0; i < nb; ++i) {
-                c += hx_sh[i];    // 0 for a constant plane, codec.py:520-523
-                if (!(fabs(c - tg) > kDecideGuard)) clear = false;
-                if (c >= tg) { sf = i + 1; nev = i + 1; break; }
+        DTS(7);
+        if (wv == 1) {   // the walk, lane-parallel: prefix sums of H(X) against beta * H(Y)
+            double hyf = lane < 16 ? hxy_sh[lane] : 0.0;
+#pragma unroll
+            for (int o = 8; o >= 1; o >>= 1) hyf += __shfl_xor(hyf, o, 64);
+            const double tg = P.beta * -__shfl(hyf, 0, 64);
+            double c = hx;                        // 0 for a constant plane, codec.py:520-523
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+                const double y = __shfl_up(c, o, 64);
+                if (lane >= o) c += y;
             }
-            if (clear)
-                for (int i = 0; i < nev; ++i) mis_sh[i] = hx_sh[i];
-            fast_cum = c;
-            ctl_sh[2] = clear ? sf : 0;
+            const u64 reach = __ballot(lane < nb && c >= tg);
+            const int sf = reach ? __ffsll((long long)reach) : 1;   // codec.py:591-593; s = 1 if never
+            const int nev = reach ? sf : nb;                         // planes the loop evaluates
+            // every evaluated prefix more than the guard from its target (a NaN fails it too)
+            const bool clear = __ballot(lane < nev && !(fabs(c - tg) > kDecideGuard)) == 0ull;
+            const double cum = __shfl(c, nev - 1, 64);
+            if (clear && lane < nev) mis_sh[lane] = hx;
+            if (lane == 0) { ctl_sh[2] = clear ? sf : 0; hxy_sh[0] = cum; }   // after the wave's reads
+            WVTS(1);
         }
+        if (pre && wv == 8) {
+            const double h = np_combine_slots_wave((int)m, vals + 512);
+            if (lane == 0) hy_sh = -h;
+            WVTS(0);
+        }
+        if (pre && wv == 2 && need_offset) { wave_offset(); WVTS(2); }
         __syncthreads();
+        DTS(9);
         fs = ctl_sh[2];
         guard_fb = fs == 0;
+        if (t == 0) fast_cum = hxy_sh[0];
     }
 
     if (role > 0 && fs) {   // split decision, decided without the joint sums: nothing to compute
@@ -1648,11 +1760,6 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
 
     // ---- start offset: first maximal float(np.var) block in raster order (codec.py:441-453);
     // independent of s, so the split decision finds it while its plane workgroups work
-    const int sb = P.block;
-    const int nbx = (P.W + sb - 1) / sb;
-    double bsc = -1.0;
-    int bix = 0x7FFFFFFF;
-    bool offset_done = false;
     auto find_offset = [&]() {
         offset_done = true;
         if (!(P.fixed_offset < 0 && P.mode == CODEC_MODE_HYBRID)) return;
@@ -1698,7 +1805,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     double cum = 0.0;
     if (fs) { s = fs; decided = true; cum = fast_cum; }   // the exact loops below stop at once
     const bool need_decision = (P.fixed_s <= 0);
-    if (wfast && nsplit > 0 && !fs) {
+    if (!FUSEDK && wfast && nsplit > 0 && !fs) {
         // split decision: H(Y) here (wave 15) while the plane workgroups sum their orders,
         // then thread 0 takes the planes in order exactly like the sequential loop
         const int wv = t >> 6, lane = t & 63;
@@ -1712,7 +1819,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
             hx_sh[lane] = (pp != 0 && (long long)pp != npx) ? -(plogp(lut, (uint32_t)(npx - pp), Nd) + plogp(lut, pp, Nd)) : 0.0;
         }
         // the class's 16 layouts (one per s) into LDS meanwhile (`vals` is free here)
-        if (t < 16 * kLayW) reinterpret_cast<int32_t*>(vals)[t] = lay_all[t];
+        if (t < 16 * kLayW) reinterpret_cast<int32_t*>(vals)[t] = lay_v;
         find_offset();   // meanwhile (its barrier also orders hx_sh / hy_sh)
         DTS(8);
         collect();
@@ -1739,16 +1846,12 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
             }
         }
     } else if (wfast && fs) {
-        // settled by the guard band: only the record's exact H(Y) and the start offset remain.
-        // H(Y) in numpy's order by the whole workgroup (8 lanes per leaf, every leaf at once;
-        // slot sums in vals[512..], clear of the layouts), the tree re-added by wave 0
-        const double h = np_sum_block1024_w0(RankTerm{tl}, (int)m, vals + 512);
-        if (t == 0) hy_sh = -h;
-        if (t < 16 * kLayW) reinterpret_cast<int32_t*>(vals)[t] = lay_all[t];
-        find_offset();
-        __syncthreads();   // hy_sh (find_offset has no barrier without a block search)
+        // settled by the guard band: the record's exact H(Y), the start offset and the layouts
+        // came with it
         Hy = hy_sh;
-    } else if (wfast) {
+        if (t == 0 && need_offset) { bsc = best_sc[0]; bix = best_ix[0]; }
+        offset_done = true;
+    } else if (!FUSEDK && wfast) {
         // H(Y) by wave 0; then rounds of `wplanes` planes, plane i0+w on wave w: its joint
         // bincount order (bit-i-clear bins ascending, then bit-i-set bins, codec.py:546-551)
         // is written to its own list and summed with np_sum_wave.  Thread 0 then walks the
@@ -1756,7 +1859,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
         const int wv = t >> 6, lane = t & 63;
         // the class's 16 layouts (one per s) into LDS now (`vals` is free until the windows):
         // loaded after the decision they were one dependent global round trip (~2 us)
-        if (t < 16 * kLayW) reinterpret_cast<int32_t*>(vals)[t] = lay_all[t];
+        if (t < 16 * kLayW) reinterpret_cast<int32_t*>(vals)[t] = lay_v;
         // paired planes (one buffer of m <= 8192 ranks): each plane's list build and leaf sums
         // go to two waves (2k, 2k + 1: different SIMDs), DECIDE_RP2 planes per round -- the round
         // is VALU-issue bound, and two planes on one SIMD were its critical path.
@@ -1798,31 +1901,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
             // the start offset meanwhile (it does not depend on s), on idle wave 13 with wave
             // shuffles only -- find_offset's block barriers and cross-wave pass stay off the
             // path after the round (C3: ~2.9 us there); thread 0 picks it up after the rounds
-            if (wv == 13 && P.fixed_offset < 0 && P.mode == CODEC_MODE_HYBRID) {
-                double ws = -1.0;
-                int wi = 0x7FFFFFFF;
-                const int cnt = exact_count(P.H, P.W, sb, exact_edge_only);
-                for (int e = lane; e < cnt; e += 64) {
-                    int by, bx;
-                    exact_block(e, P.H, P.W, sb, exact_edge_only, &by, &bx);
-                    const double sc = exact[(size_t)b * exact_cap + e];
-                    const int ix = by * nbx + bx;
-                    if (sc > ws || (sc == ws && ix < wi)) { ws = sc; wi = ix; }
-                }
-                if (lane == 0 && fast_blocks && key0) {
-                    const uint32_t score = (uint32_t)(key0 >> 32);
-                    const int ix = (int)(0xFFFFFFFFu - (uint32_t)(key0 & 0xFFFFFFFFu));
-                    const double sc = (double)score / ((double)sb * sb * (double)sb * sb);
-                    if (sc > ws || (sc == ws && ix < wi)) { ws = sc; wi = ix; }
-                }
-#pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) {
-                    const double os = __shfl_xor(ws, o, 64);
-                    const int oi = __shfl_xor(wi, o, 64);
-                    if (os > ws || (os == ws && oi < wi)) { ws = os; wi = oi; }
-                }
-                if (lane == 0) { best_sc[0] = ws; best_ix[0] = wi; }
-            }
+            if (wv == 13 && need_offset) wave_offset();
             offset_done = true;   // every thread (uniform): find_offset is not called below
             // H(X) of every plane meanwhile, on an idle wave (its two table loads stay off the
             // pairs' critical path); read by thread 0's walk after the round's barrier
@@ -2060,18 +2139,25 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
             if (i0 < 0) DTS(7);
         }
     }
-    if (lut_ok && !wfast && !walk) Hy = -np_sum_block1024(RankTerm{terms}, (int)m, vals);
+    // the block-sequential path: slices off the wave path, and the fused kernel's exact sums
+    // (its terms stay in LDS: joint orders at jl, tree slots at vals[512..], the layouts kept)
+    const bool blockp = lut_ok && !walk && (!wfast || (FUSEDK && !fs));
+    const double* bt = wfast ? tl : terms;
+    uint16_t* bl = wfast ? jl : list;
+    double* bv = wfast ? vals + 512 : vals;
+    if (blockp && wfast && t < 16 * kLayW) reinterpret_cast<int32_t*>(vals)[t] = lay_v;
+    if (blockp) Hy = pre ? hy_sh : -np_sum_block1024(RankTerm{bt}, (int)m, bv);
     const double target = P.beta * Hy;
 
     // ---- the s decision (codec.py:580-593)
-    for (int i = 0; i < P.nbits && i < 16 && lut_ok && !wfast && !walk; ++i) {
+    for (int i = 0; i < P.nbits && i < 16 && blockp; ++i) {
         if (!(need_decision && !decided) && !P.all_mi) break;
         const uint32_t pp = pops_sh[i];
         double mi = 0.0;
         if (m > 1 && pp != 0 && (long long)pp != npx) {          // codec.py:520-523
-            build_joint_order(nzmask, v0, rank0, i, list, sh);
+            build_joint_order(nzmask, v0, rank0, i, bl, sh);
             if (i == 0) DTS(6);
-            const double hxy = -np_sum_block1024(ListTerm{terms, list}, (int)m, vals);
+            const double hxy = -np_sum_block1024(ListTerm{bt, bl}, (int)m, bv);
             if (i == 0) DTS(7);
             const double hx = -(plogp(lut, (uint32_t)(npx - pp), Nd) + plogp(lut, pp, Nd));
             mi = (hx + Hy) - hxy;                                // codec.py:554
@@ -2106,6 +2192,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     auto& seg_p = S.seg_p;
     auto& seg_q0 = S.seg_q0;
     auto& seg_s0 = S.seg_s0;
+    if (EMBED && pay_in_lds && role == 0 && t < E.pw) pay_sh[t] = pay_v;   // read by the embed loop
     __syncthreads();   // lay_sh
     DTS(4);
     if (t < 64) {   // ---- windows and the slice record (wave 0: lane j = segment j in perm order)
@@ -2306,6 +2393,11 @@ __global__ __launch_bounds__(1024) void k_scan_decide(const T* __restrict__ cove
     long long ts_start = 0;
     if (threadIdx.x == 0) ts_start = wall_clock64();
 #endif
+    // the decision's global inputs first: their latency hides under the scan
+    const int cls = slice_class[b];
+    constexpr int kLayW = (int)(sizeof(codec_layout) / 4);
+    const int32_t lay_v = threadIdx.x < 16 * kLayW ? reinterpret_cast<const int32_t*>(table + (size_t)cls * 16)[threadIdx.x] : 0;
+    const u64 pay_v = ((int)threadIdx.x < E.pw && E.pw <= 256) ? E.payload[(size_t)b * E.pw + threadIdx.x] : 0ull;
     scan_rows_body<T, SB, NT, true, 0, true, 4, true>(U.s, cover, stego, P.H, P.W, bands_per_wg, ghist_all, gkey, gor);
 #ifdef DECIDE_TS
     if (threadIdx.x == 0) reinterpret_cast<long long*>(gterms + (size_t)b * HistCfg<T>::kBins)[HistCfg<T>::kBins - 1] = ts_start;
@@ -2321,12 +2413,15 @@ __global__ __launch_bounds__(1024) void k_scan_decide(const T* __restrict__ cove
     fz.key = U.s.wkey;
     const int Rp = fz.orv ? (1 << (32 - __clz((int)fz.orv))) : 1;
     fz.lds_ok = sizeof(T) == 2 && U.s.wrap == 0u && Rp <= 4096;
+    fz.cls = cls;
+    fz.lay_v = lay_v;
+    fz.pay_v = pay_v;
     if (!fz.lds_ok) {   // uniform: the global histogram path (wrap fix-ups are already there)
         hist_flush<T>(U.s.lds, ghist_all + (size_t)b * HistCfg<T>::kBins);
         __threadfence();
     }
     __syncthreads();   // every read of the scan's LDS words above precedes the decision's writes
-    decide_body<T, true>(U.d, &fz, b, 0, P, ghist_all, gor, gterms, gkey, exact, exact_cap, exact_edge_only, 1, lut,
+    decide_body<T, true, true>(U.d, &fz, b, 0, P, ghist_all, gor, gterms, gkey, exact, exact_cap, exact_edge_only, 1, lut,
                          lut_len, table, slice_class, meta_all, E, nullptr, 0, 0u, -1);
 }
 

@@ -237,3 +237,68 @@ def test_pee_file_pipeline_gpu(name, codec, T, tmp_path):
     np.testing.assert_array_equal(cover, img)
     if name == "pe":
         assert info["lm_count"] > 0 or side["lm"].sum() == 0
+
+
+_FAKE_CJXL = '''import sys
+a = sys.argv[1:]
+# the reference's command line: cjxl <in.png> <out.jxl> -d 0 -e 3 (codec.py:121)
+assert len(a) == 6 and a[2:] == ["-d", "0", "-e", "3"] and a[0].endswith(".png") and a[1].endswith(".jxl"), a
+data = open(a[0], "rb").read()
+assert data[:8] == b"\\x89PNG\\r\\n\\x1a\\n"
+open(a[1], "wb").write(b"FAKEJXL1" + data)
+open(__file__ + ".log", "a").write(" ".join(["cjxl"] + a[2:]) + "\\n")
+'''
+_FAKE_DJXL = '''import sys
+a = sys.argv[1:]
+# djxl <in.jxl> <out.png> (codec.py:175)
+assert len(a) == 2 and a[0].endswith(".jxl") and a[1].endswith(".png"), a
+d = open(a[0], "rb").read()
+assert d[:8] == b"FAKEJXL1"
+open(a[1], "wb").write(d[8:])
+open(__file__ + ".log", "a").write("djxl\\n")
+'''
+
+
+@pytest.mark.parametrize("name", ["pe_b0.4_1k", "torax_b0.4_1k"])
+def test_jxl_plumbing_with_stand_in_binaries(name, tmp_path, monkeypatch):
+    """C5's JPEG-XL leg (pipeline.py _compress/_decompress, codec.py:111-129 / 169-182) run end
+    to end with stand-in cjxl/djxl on PATH (the real binaries are absent: .MISSING_LARGE_BLOBS).
+    The stand-ins assert the reference's argument vectors and pass the 16-bit PNG through, so
+    what is checked is this build's side: the PNG it writes (the reference's
+    Image.fromarray(stego.astype(uint16))), the file layout, and the PNG it reads back --
+    bit-exact, a uint8 stego coming back as uint16 exactly as in the reference.  decode_bin then
+    runs on the .bin with its two GPU calls (extract_local_planes, decode_message) replaced by
+    the oracle's, and returns the reference's own decoded message (golden)."""
+    import sys
+    from codec_tcc_amd import api, pipeline
+    from oracle import ref_cpu as R
+    pytest.importorskip("PIL")
+    bind = tmp_path / "bin"
+    bind.mkdir()
+    for exe, body in (("cjxl", _FAKE_CJXL), ("djxl", _FAKE_DJXL)):
+        p = bind / exe
+        p.write_text(f"#!{sys.executable}\n" + body)
+        p.chmod(0o755)
+    monkeypatch.setenv("PATH", str(bind) + os.pathsep + os.environ.get("PATH", ""))
+    case = CASES[name]
+    stego = golden_io.stego(case)
+    h, w = stego.shape
+    data = pipeline._compress(stego, "jxl")
+    assert data[:8] == b"FAKEJXL1"
+    back = pipeline._decompress(data, "jxl", h, w)
+    assert back.dtype == np.uint16 and back.shape == (h, w)
+    np.testing.assert_array_equal(back, stego.astype(np.uint16))
+    # the whole file: header + jxl stego + zlib bitmaps -> decode_bin (GPU calls -> oracle)
+    s = int(case["s"])
+    blob = container.bitmaps_blob(golden_io.dense_bitmaps(case).astype(np.uint8))
+    hdr = container.create_header("jxl", s, [int(x) for x in case["sizes"]], [int(x) for x in case["perm"]],
+                                  len(blob), w, h, 0, False)
+    out = str(tmp_path / "saida.bin")
+    container.create_binary_file(out, hdr, data, blob)
+    monkeypatch.setattr(api, "extract_local_planes", R.extract_local_planes)
+    monkeypatch.setattr(api, "decode_message", R.decode_message)
+    message, st = pipeline.decode_bin(out)
+    np.testing.assert_array_equal(st, stego.astype(np.uint16))
+    assert message == golden_io.decoded(case)
+    log = (bind / "cjxl.log").read_text().split("\n") + (bind / "djxl.log").read_text().split("\n")
+    assert "cjxl -d 0 -e 3" in log and log.count("djxl") == 2

@@ -13,3 +13,15 @@ cat gpurun_out/r06/phases_c3.txt gpurun_out/r06/phases_c2.txt gpurun_out/r06/pha
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_api.py -m gpu -q \
     --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r06/pytest_lsb.log 2>&1; rc=$?
 echo "pytest rc $rc"; grep -E "^FAILED|^ERROR" gpurun_out/r06/pytest_lsb.log | head -20; tail -2 gpurun_out/r06/pytest_lsb.log
+[ $rc -le 1 ] || stop $rc pytest
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --cpu-seconds 0 --cpu-ref-seconds 0 \
+    > gpurun_out/r06/bench_quick.json 2> gpurun_out/r06/bench_quick.err; rc=$?
+echo "bench rc $rc"; [ $rc -eq 0 ] || stop $rc bench
+python3 - <<'PY'
+import json
+d = json.loads(open("gpurun_out/r06/bench_quick.json").read().strip().splitlines()[-1])
+l = d.get("lsb", {}); c3 = d.get("c3", {}).get("lsb", {}); c2 = d.get("c2", {}).get("lsb", {})
+print("headline", d["value"], d["ms_per_step"])
+for n, x in (("lsb", l), ("c3.lsb", c3), ("c2.lsb", c2)):
+    print(n, x.get("ms_per_step"), x.get("roundtrip_ok"), x.get("decide"), x.get("kernels_ms"))
+PY
