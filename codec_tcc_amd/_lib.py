@@ -121,6 +121,9 @@ EXPORTS = tuple(_SIGS)
 
 _lib = None
 _load_error = None
+# -D flags of diagnostic builds (tools/): never the product library
+_DIAG_DEFINES = {"-DDECIDE_TS", "-DDECIDE_TS_SCAN_ONLY", "-DCODEC_ST_SC", "-DPEE_LB_TRACE", "-DPEE_SS_TRACE",
+                 "-DCODEC_DEBUG_KNOBS", "-DRES_TRACE", "-DPEE_X_COPYONLY"}
 
 
 def load(path: str = LIB_PATH):
@@ -167,6 +170,15 @@ def _check_digest(path: str):
     # CODEC_OFFLOAD_ARCH / CODEC_BUILD_DEFS loads without that environment, and a mismatch
     # names the sources as the cause only when they are
     flags = build.library_flags(path)
+    # a diagnostic build matches its own digest but is not the product: phase
+    # stamps, a scan that returns before deciding (DECIDE_TS_SCAN_ONLY), trace buffers ...
+    diag = sorted({f for f in (flags or []) if f.split("=")[0] in _DIAG_DEFINES})
+    if diag and os.environ.get("CODEC_ALLOW_DIAG_LIB") != "1":
+        raise RuntimeError(f"{path} is a diagnostic build ({' '.join(diag)}); rebuild the product library with "
+                           "`python -c 'import __graft_entry__ as g; g.build()'` (CODEC_ALLOW_DIAG_LIB=1 loads it anyway)")
+    if flags is not None and flags != build.FLAGS and not diag:
+        import warnings
+        warnings.warn(f"{path} was built with non-default flags {' '.join(flags)}", RuntimeWarning, stacklevel=3)
     have, want = build.library_digest(path), build.source_digest(flags)
     if have != want:
         extra = "" if flags is None or flags == build.FLAGS else \

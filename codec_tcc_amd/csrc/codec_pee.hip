@@ -3184,9 +3184,20 @@ struct PeeWsShape {
     int B, H, W, bytes;
     uint32_t epoch;   // self-cleaning calls issued on this workspace (their status-word epoch)
     bool sc_clean;    // the self-cleaning state region is known clean (zeroed here, or kept by SC calls)
+    size_t diag;      // offset of the diagnostic counters in this shape's layout
+    // a call on this workspace was captured into a graph: replays run without the
+    // host, so they can rewrite the captured shape's state at any time.  Self-cleaning calls of
+    // any OTHER shape then take the zeroing path (their finished flags could sit on the replay's
+    // words); the captured shape itself stays exact through its epoch tags
+    bool captured;
+    int cB, cH, cW, cbytes;
 };
 static std::mutex g_pee_ws_mu;
 static std::map<std::pair<int, uintptr_t>, PeeWsShape> g_pee_ws;
+// the registry only remembers pointers: an unknown pointer is treated as a fresh workspace
+// (its self-cleaning state zeroed on first use), so forgetting entries is always safe --
+// bounded here so that a process allocating many workspaces does not grow it without end
+constexpr size_t kPeeWsMax = 4096;
 static std::pair<int, uintptr_t> pee_ws_key(const void* ws) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) dev = -1;
@@ -3197,29 +3208,52 @@ static hipError_t pee_ws_zero(void* ws, const PeeWs& L, hipStream_t st) {
     char* w = static_cast<char*>(ws);
     return pee_zero(st, w, L.diag, w + L.hist, L.total - L.hist);
 }
+static bool pee_capturing(hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
+}
 // every workspace-taking PEE call, after its argument checks
 static hipError_t pee_ws_enter(void* ws, const codec_pee_params* P, const PeeWs& L, hipStream_t st) {
-    bool changed = false;
+    bool changed = false, moved_diag = false;
     {
         std::lock_guard<std::mutex> g(g_pee_ws_mu);
         auto k = pee_ws_key(ws);
         auto it = g_pee_ws.find(k);
-        const PeeWsShape now{P->B, P->H, P->W, P->bytes, 0u, it != g_pee_ws.end()};   // zeroed below if seen
+        if (it == g_pee_ws.end() && g_pee_ws.size() >= kPeeWsMax) g_pee_ws.clear();
+        PeeWsShape now{P->B, P->H, P->W, P->bytes, 0u, it != g_pee_ws.end(), L.diag, false, 0, 0, 0, 0};
         if (it == g_pee_ws.end()) {
-            g_pee_ws.emplace(k, now);
+            it = g_pee_ws.emplace(k, now).first;
         } else if (it->second.B != now.B || it->second.H != now.H || it->second.W != now.W ||
                    it->second.bytes != now.bytes) {
+            // a shape change: zeroed below -- including the diagnostic counters when this
+            // layout puts them elsewhere (they would start from the old shape's words)
+            moved_diag = it->second.diag != L.diag;
+            now.captured = it->second.captured;
+            now.cB = it->second.cB; now.cH = it->second.cH; now.cW = it->second.cW; now.cbytes = it->second.cbytes;
             it->second = now;
             changed = true;
         }
+        if (pee_capturing(st)) {
+            it->second.captured = true;
+            it->second.cB = P->B; it->second.cH = P->H; it->second.cW = P->W; it->second.cbytes = P->bytes;
+        }
     }
-    return changed ? pee_ws_zero(ws, L, st) : hipSuccess;
+    if (!changed) return hipSuccess;
+    return moved_diag ? pee_zero(st, ws, L.total) : pee_ws_zero(ws, L, st);
 }
 // the self-cleaning words' unsafe-count field holds < 2^24 (LB_HI): bigger slices zero
-// instead; so does a call being captured into a graph (a replay would repeat one epoch)
-static bool pee_sc_fits(const codec_pee_params* P, hipStream_t st) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+// instead; so does a call being captured into a graph (a replay would repeat one epoch), and
+// a call of another shape than a graph captured on this workspace (its replays may have
+// written that shape's state over this one's)
+static bool pee_sc_fits(const codec_pee_params* P, hipStream_t st, const void* ws) {
+    if (pee_capturing(st)) return false;
+    {
+        std::lock_guard<std::mutex> g(g_pee_ws_mu);
+        auto it = g_pee_ws.find(pee_ws_key(ws));
+        if (it != g_pee_ws.end() && it->second.captured &&
+            (it->second.cB != P->B || it->second.cH != P->H || it->second.cW != P->W || it->second.cbytes != P->bytes))
+            return false;
+    }
     return (long long)(P->H / 2) * (P->W / 2) <= PEE_SC_MAX_NC;
 }
 // this self-cleaning call's epoch (mod 126: parity and tag epoch % 63 + 1 both cycle in it);
@@ -3321,7 +3355,11 @@ int codec_pee_reset(const codec_pee_params* P, void* workspace, size_t workspace
     hipStream_t st = as_stream(stream);
     HIP_TRY(pee_zero(st, workspace, L.total));   // diagnostics included: a fresh workspace
     std::lock_guard<std::mutex> g(g_pee_ws_mu);
-    g_pee_ws[pee_ws_key(workspace)] = PeeWsShape{P->B, P->H, P->W, P->bytes, 0u, true};
+    // (a graph captured on this workspace stays remembered: its replays may still run)
+    auto& e = g_pee_ws[pee_ws_key(workspace)];
+    const PeeWsShape prev = e;
+    e = PeeWsShape{P->B, P->H, P->W, P->bytes, 0u, true, pee_ws(P).diag, prev.captured, prev.cB, prev.cH, prev.cW,
+                   prev.cbytes};
     return 0;
 }
 
@@ -3437,7 +3475,7 @@ int codec_pee_embed_ts(const codec_pee_params* P, const void* cover, void* stego
         // small out-of-place batches (flat slots, no ticket) clean up after themselves: no
         // zeroing launch (C2: one launch of ~2 us fewer per call); meta is written without
         // atomics out of place, so only in place (and the ticket modes) zero it
-        if (flat && (mode & PEE_MODE_NOTICKET) && knob("CODEC_PEE_SELFCLEAN", 1) && pee_sc_fits(P, st)) mode |= PEE_MODE_SC;
+        if (flat && (mode & PEE_MODE_NOTICKET) && knob("CODEC_PEE_SELFCLEAN", 1) && pee_sc_fits(P, st, workspace)) mode |= PEE_MODE_SC;
         if (!(mode & PEE_MODE_SC))
             HIP_TRY(pee_zero(st, stw, L.ctl - L.st + PEE_CTL_WORDS(P->B, L.nchunks) * 4, meta, (size_t)P->B * sizeof(codec_pee_meta),
                              inplace ? lm : nullptr, inplace ? (size_t)P->B * P->lm_words * 8 : 0));
@@ -3708,7 +3746,7 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
                         : (knob("CODEC_PEE_X_CHUNK_MAJOR", knob("CODEC_PEE_1P_CHUNK_MAJOR", 1)) ? PEE_MODE_CMAJOR : 0) |
                               (knob("CODEC_PEE_X_NOTICKET", 1) ? PEE_MODE_NOTICKET : 0) |
                               ((int)(knob("CODEC_PEE_X_GROUP", 32) / 8) << 8);
-        if (flat && (mode & PEE_MODE_NOTICKET) && knob("CODEC_PEE_SELFCLEAN", 1) && pee_sc_fits(P, st)) mode |= PEE_MODE_SC;
+        if (flat && (mode & PEE_MODE_NOTICKET) && knob("CODEC_PEE_SELFCLEAN", 1) && pee_sc_fits(P, st, workspace)) mode |= PEE_MODE_SC;
         if (!(mode & PEE_MODE_SC))
             HIP_TRY(pee_zero(st, payload_out, (size_t)P->B * P->payload_words * 8, stw, L.ctl - L.st + PEE_CTL_WORDS(P->B, L.nchunks) * 4));
         bool sc_fresh = false;

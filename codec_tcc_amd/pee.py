@@ -64,9 +64,13 @@ class PeeCodec:
         ws = _lib.load().codec_pee_workspace_bytes(C.byref(P))
         if ws == 0:
             _lib.check(-1, "codec_pee_workspace_bytes")
-        # zeroed once: the cumulative look-back diagnostics live in it (codec_pee_diag_offset)
-        self.workspace = torch.zeros(int(ws), dtype=torch.uint8, device=self.device)
+        # zeroed by the reset below (codec_pee_reset: the whole workspace, the cumulative
+        # look-back diagnostics included -- codec_pee_diag_offset)
+        self.workspace = torch.empty(int(ws), dtype=torch.uint8, device=self.device)
         self.t_slices = torch.empty(self.B, dtype=torch.int32, device=self.device) if self.auto else None
+        # register the fresh workspace with the library: an allocation at an address
+        # an earlier workspace used would otherwise inherit that one's call-to-call state record
+        self.reset()
 
     def reset(self):
         """Re-zero the workspace (codec_pee_reset, on the current stream): the state small

@@ -261,13 +261,23 @@ typedef struct codec_pee_meta {
  * Recovery rules:
  *   - shape change: the library remembers per (device, workspace pointer) the shape of the
  *     last call; a call of another (B, H, W, bytes) zeroes the workspace first (one extra
- *     launch; the diagnostic counters are kept), so one workspace sized for the largest
- *     batch may serve smaller batches in turn;
- *   - desynchronised counters (a call that never completed, a graph replayed against a
- *     workspace another shape has used): a chunk reads only status words carrying its own
- *     epoch tag, so a stale word counts as "not published", the bounded wait ends in the
- *     pixel-count fallback and the results stay exact (slower; codec_pee_diag_offset counts
- *     the fallbacks).  codec_pee_reset restores the fast path;
+ *     launch; the diagnostic counters are kept, or zeroed too when the new shape places
+ *     them elsewhere), so one workspace sized for the largest batch may serve smaller
+ *     batches in turn;
+ *   - graphs: a call made under stream capture takes the zeroing path, and the library
+ *     remembers that shape as captured on the workspace.  Replays run without the host, so
+ *     from then on self-cleaning calls of any OTHER shape on that workspace take the zeroing
+ *     path as well (a replay may have written the captured shape's words where their finished
+ *     flags lie); calls of the captured shape keep the fast path.  A fresh workspace per
+ *     captured graph avoids the extra launch;
+ *   - desynchronised counters (a call that never completed): a chunk reads only status words
+ *     carrying its own epoch tag, so a stale word counts as "not published", the bounded
+ *     wait ends in the pixel-count fallback and the results stay exact (slower;
+ *     codec_pee_diag_offset counts the fallbacks).  codec_pee_reset restores the fast path;
+ *   - the library keys this state by (device, pointer) and treats an unknown pointer as a
+ *     fresh workspace (zeroed on its first self-cleaning call); a workspace allocated at an
+ *     address an earlier one used inherits that entry, so zero-initialise it or call
+ *     codec_pee_reset once (PeeCodec does so at construction);
  *   - after any failed call (non-zero return, ELOOKBACK status, a raised exception in the
  *     host layer) call codec_pee_reset before reusing the workspace: PeeCodec does so. */
 size_t codec_pee_workspace_bytes(const codec_pee_params* P);

@@ -114,6 +114,7 @@ def test_library_digest_ties_binary_to_sources(monkeypatch, tmp_path):
     assert _lib.load().codec_build_digest().decode() == build.source_digest()
 
 
+@pytest.mark.filterwarnings("ignore:.*non-default flags:RuntimeWarning")   # this test fakes another environment
 def test_library_digest_uses_the_flags_it_was_built_with(monkeypatch):
     """the build flags travel inside the library, so a process whose environment
     would build with other flags (CODEC_OFFLOAD_ARCH / CODEC_BUILD_DEFS) still loads it; a
@@ -217,3 +218,14 @@ def test_numpy_log2_is_elementwise():
     for k in (1, 2, 3, 7, 8, 9, 15, 16, 17):
         for i in range(0, 300):
             assert np.log2(x[i:i + k])[0] == full[i]
+
+
+def test_loader_refuses_diagnostic_builds(tmp_path, monkeypatch):
+    """a diagnostic build (phase stamps, a scan that returns before deciding) carries
+    a digest that matches its own flags; the loader still refuses it at the in-tree path unless
+    CODEC_ALLOW_DIAG_LIB=1."""
+    from codec_tcc_amd import build
+    monkeypatch.setattr(build, "library_flags", lambda path=None: build.FLAGS + ["-DDECIDE_TS", "-DDECIDE_TS_SCAN_ONLY"])
+    monkeypatch.delenv("CODEC_ALLOW_DIAG_LIB", raising=False)
+    with pytest.raises(RuntimeError, match="diagnostic build"):
+        _lib._check_digest(_lib.LIB_PATH)

@@ -567,6 +567,74 @@ def test_gpu_workspace_reused_across_batch_sizes(monkeypatch):
 
 
 @pytest.mark.gpu
+def test_gpu_graph_replay_then_other_shape_on_one_workspace(monkeypatch):
+    """a step of shape S1 captured into a graph and replayed, with eager
+    calls of shape S2 on the SAME workspace in between.  Replays bypass the host registry,
+    so they can leave S1's words where S2's finished flags lie; the library therefore sends
+    S2's self-cleaning calls down the zeroing path once S1 was captured there.  Every replay
+    and every eager call equals the oracle, interleaved in both orders."""
+    import ctypes as C
+
+    import torch
+    from codec_tcc_amd import _lib, framing, graphs
+    from codec_tcc_amd.codec import _stream
+    from codec_tcc_amd.pee import PeeCodec
+    monkeypatch.setenv("CODEC_PEE_ONEPASS", "1")
+    h, w, T = 256, 512, 2
+    big = PeeCodec(3, h, w, T=T)
+    ws = big.workspace
+    lib = _lib.load()
+
+    def buffers(bsz, seed):
+        covers = np.stack([synth.ct12(h, w, seed + i) for i in range(bsz)])
+        pays = [_bits(P.capacity(c, T) - 13 * i - 5, seed + 50 + i) for i, c in enumerate(covers)]
+        packed, lengths = framing.pack_bits([np.asarray(p) for p in pays])
+        prm = _lib.PeeParams(B=bsz, H=h, W=w, bytes=2, T=T, maxval=65535, payload_words=int(packed.shape[1]),
+                             lm_words=big.lm_words)
+        b = {"prm": prm, "covers": covers, "pays": pays, "packed": packed,
+             "cov": torch.from_numpy(covers).cuda(), "words": torch.from_numpy(packed).cuda(),
+             "lens": torch.tensor(lengths, dtype=torch.int32, device="cuda")}
+        b["stego"] = torch.empty_like(b["cov"])
+        b["rest"] = torch.empty_like(b["cov"])
+        b["lm"] = torch.empty((bsz, big.lm_words), dtype=torch.int64, device="cuda")
+        b["meta"] = torch.empty((bsz, _lib.PEE_META_BYTES), dtype=torch.uint8, device="cuda")
+        b["out"] = torch.empty((bsz, int(packed.shape[1])), dtype=torch.int64, device="cuda")
+        return b
+
+    def step(b):
+        prm = b["prm"]
+        _lib.check(lib.codec_pee_embed_ts(C.byref(prm), b["cov"].data_ptr(), b["stego"].data_ptr(),
+                                          b["words"].data_ptr(), b["lens"].data_ptr(), None, b["meta"].data_ptr(),
+                                          b["lm"].data_ptr(), ws.data_ptr(), ws.numel(), _stream()), "embed")
+        _lib.check(lib.codec_pee_extract(C.byref(prm), b["stego"].data_ptr(), b["meta"].data_ptr(),
+                                         b["lm"].data_ptr(), b["rest"].data_ptr(), b["out"].data_ptr(),
+                                         ws.data_ptr(), ws.numel(), _stream()), "extract")
+
+    def check(b, what):
+        torch.cuda.synchronize()
+        st_h = b["stego"].cpu().numpy()
+        for i in range(len(b["covers"])):
+            st, _side = P.pee_embed(b["covers"][i], b["pays"][i], T, truncate=True)
+            np.testing.assert_array_equal(st_h[i], st, err_msg=f"{what} slice {i}")
+        np.testing.assert_array_equal(b["out"].cpu().numpy().view(np.uint64), b["packed"].view(np.uint64))
+        np.testing.assert_array_equal(b["rest"].cpu().numpy(), b["covers"])
+
+    s1 = buffers(3, 900)
+    g = graphs.capture(lambda: step(s1))            # S1 = (3, 256, 512), captured: zeroing variant
+    s2 = buffers(2, 1000)
+    for k in range(3):
+        for key in ("stego", "rest", "out", "meta"):   # the replay must write every output again
+            s1[key].zero_()
+        g.replay()
+        check(s1, f"replay {k}")
+        for j in range(2):                          # S2 eagerly on the same workspace, twice
+            for key in ("stego", "rest", "out"):
+                s2[key].zero_()
+            step(s2)
+            check(s2, f"eager S2 {k}.{j}")
+
+
+@pytest.mark.gpu
 def test_gpu_reset_after_failed_call(monkeypatch):
     """A call that fails (here: an in-place look-back made to time out, status ELOOKBACK)
     re-zeroes the workspace before the exception leaves PeeCodec.embed: the cumulative
