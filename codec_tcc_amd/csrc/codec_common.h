@@ -153,6 +153,22 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("" ::: "memory");
 }
 
+// block_excl_scan with LDS-only barriers (see lds_barrier): global loads in flight (prefetches)
+// stay in flight through it
+template <int NT>
+__device__ uint32_t block_excl_scan_lds(uint32_t x, uint32_t* sh, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan(x);
+    if (lane == 63) sh[wv] = inc;
+    lds_barrier();
+    const uint32_t wt = lane < NT / 64 ? sh[lane] : 0u;
+    const uint32_t wi = wave_incl_scan(wt);
+    const uint32_t pre = wv ? (uint32_t)__shfl(wi, wv - 1, 64) : 0u;
+    *total = (uint32_t)__shfl(wi, NT / 64 - 1, 64);
+    lds_barrier();   // sh reusable
+    return pre + inc - x;
+}
+
 // block_excl_scan64 / block_sum_u32 with LDS-only barriers (see lds_barrier)
 template <int NT>
 __device__ u64 block_excl_scan64_lds(u64 x, u64* sh, u64* total) {

@@ -987,7 +987,9 @@ __device__ __forceinline__ void scan_rows_body(ScanRowsSmem<T>& SS, const T* __r
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) vor |= __shfl_xor(vor, o, 64);
     if (lane == 0 && vor) atomicOr(&SS.wor, vor);   // the workgroup's OR (bounds the flush)
-    __syncthreads();
+    // fused (k_scan_decide): LDS-only -- the copy's last stores drain during the decision
+    // instead (the fused embed, which rewrites window pixels, waits for them with a full barrier)
+    if constexpr (FUSED) lds_barrier(); else __syncthreads();
     // block keys: score c(n-c) (exact variance numerator of a full pow2 block), first
     // maximal block in raster order wins (~index in the low word)
     u64 best = 0;
@@ -1006,7 +1008,7 @@ __device__ __forceinline__ void scan_rows_body(ScanRowsSmem<T>& SS, const T* __r
     }
     if (lane == 0 && best) atomicMax(&wkey, best);
     if (DIAG == 0 && !FUSED) hist_flush<T>(lds, ghist, SS.wor);
-    __syncthreads();
+    if constexpr (FUSED) lds_barrier(); else __syncthreads();
     if (!FUSED && threadIdx.x == 0 && wkey) atomicMax(&gkey[b], wkey);
     if (!FUSED && threadIdx.x == 0 && SS.wor) atomicOr(&gor[b], SS.wor);
 }
@@ -1466,7 +1468,10 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     const int32_t lay_v = fz ? fz->lay_v : (role == 0 && t < 16 * kLayW) ? lay_all[t] : 0;
     if (t < 16) pops_sh[t] = 0;
     uint32_t m;
-    const uint32_t rank0 = block_excl_scan<1024>((uint32_t)__popcll(nzmask), sh, &m);
+    // LDS-only barriers from here to the embed (lds_barrier): a __syncthreads would also wait
+    // for every global access in flight -- the log2-table prefetch above, the meta stores of
+    // the windows phase -- where only LDS needs ordering
+    const uint32_t rank0 = block_excl_scan_lds<1024>((uint32_t)__popcll(nzmask), sh, &m);
     DTS(13);
     {   // the 16 per-plane sums of the wave as one reduce-scatter: 8 + 4 + 2 + 1 shuffles leave
         // lane l with plane l >> 2 summed over 16 lanes, two more finish it (17 instead of 96)
@@ -1564,7 +1569,8 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
         }
     }
     if (t < 16) mis_sh[t] = 0.0;
-    __syncthreads();
+    if (wfast) lds_barrier();   // the terms are in LDS (uniform)
+    else __syncthreads();       // the terms went to global memory
 
     // ---- the s decision, guard-banded.  X = f(Y), so I(X;Y) = H(X) exactly: the
     // reference's MI (codec.py:554, h_x + h_y - h_xy from two numpy-order sums) differs from
@@ -1638,7 +1644,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
             hx = (pp != 0 && (long long)pp != npx) ? -(p0 * log2(p0) + p1 * log2(p1)) : 0.0;
         }
         DTS(6);
-        __syncthreads();
+        lds_barrier();
         DTS(7);
         if (wv == 1) {   // the walk, lane-parallel: prefix sums of H(X) against beta * H(Y)
             double hyf = lane < 16 ? hxy_sh[lane] : 0.0;
@@ -1667,7 +1673,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
             WVTS(0);
         }
         if (pre && wv == 2 && need_offset) { wave_offset(); WVTS(2); }
-        __syncthreads();
+        lds_barrier();
         DTS(9);
         fs = ctl_sh[2];
         guard_fb = fs == 0;
@@ -2174,10 +2180,13 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     // the slice's segment layout for its s (64 ints), loaded by one wave in one round trip
     // while the offset is found, instead of thread 0's dependent loads in the windows loop
     auto& lay_sh = S.lay_sh;
+    // lay_sh and everything the windows read are written and read by wave 0 (thread 0's s, the
+    // offset, the layouts), so no barrier follows the fill; s itself crosses waves only on the
+    // exact paths (thread 0 decided there) -- the guard band's s is every thread's
     if (t == 0) ctl_sh[1] = s;
-    __syncthreads();
+    if (!fs) lds_barrier();
     {
-        const int sl = min(max(ctl_sh[1], 1), 16);
+        const int sl = fs ? fs : min(max(ctl_sh[1], 1), 16);
         if (t < kLayW) lay_sh[t] = wfast ? reinterpret_cast<const int32_t*>(vals)[(sl - 1) * kLayW + t]
                                          : lay_all[(sl - 1) * kLayW + t];
     }
@@ -2192,8 +2201,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     auto& seg_p = S.seg_p;
     auto& seg_q0 = S.seg_q0;
     auto& seg_s0 = S.seg_s0;
-    if (EMBED && pay_in_lds && role == 0 && t < E.pw) pay_sh[t] = pay_v;   // read by the embed loop
-    __syncthreads();   // lay_sh
+    if (EMBED && pay_in_lds && role == 0 && t < E.pw) pay_sh[t] = pay_v;   // read by the embed loop (after its barrier)
     DTS(4);
     if (t < 64) {   // ---- windows and the slice record (wave 0: lane j = segment j in perm order)
     const int lane = t;
@@ -2265,7 +2273,9 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     }
     if constexpr (EMBED) {
         const SliceWin& W = Wsh;
-        __syncthreads();
+        // Wsh, seg_* (the meta stores need not land first).  Fused: a full barrier -- the scan's
+        // stego copy stores (left in flight) must land before the window pixels are rewritten
+        if constexpr (FUSEDK) __syncthreads(); else lds_barrier();
         DTS(10);
         const T* cv = static_cast<const T*>(E.cover) + (size_t)b * npx;
         T* sv = static_cast<T*>(E.stego) + (size_t)b * npx;
@@ -2419,8 +2429,10 @@ __global__ __launch_bounds__(1024) void k_scan_decide(const T* __restrict__ cove
     if (!fz.lds_ok) {   // uniform: the global histogram path (wrap fix-ups are already there)
         hist_flush<T>(U.s.lds, ghist_all + (size_t)b * HistCfg<T>::kBins);
         __threadfence();
+        __syncthreads();   // the flush lands before pass 1 reads it back
+    } else {
+        lds_barrier();     // every read of the scan's LDS words above precedes the decision's writes
     }
-    __syncthreads();   // every read of the scan's LDS words above precedes the decision's writes
     decide_body<T, true, true>(U.d, &fz, b, 0, P, ghist_all, gor, gterms, gkey, exact, exact_cap, exact_edge_only, 1, lut,
                          lut_len, table, slice_class, meta_all, E, nullptr, 0, 0u, -1);
 }
