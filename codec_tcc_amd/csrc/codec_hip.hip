@@ -1304,11 +1304,12 @@ struct FusedScan {
     u64 pay_v;
 };
 
-// FUSEDK (k_scan_decide): the wave-parallel exact MI rounds are compiled out -- a slice the
-// guard band sends to the exact sums (or all_mi / fixed_s there) runs the block-sequential
-// sums over the LDS terms instead -- so the fused kernel carries the register pressure of the
-// scan and the fast decision only
-template <typename T, bool EMBED, bool FUSEDK = false>
+// FUSEDK: the fused scan + decision kernel (k_scan_decide).  LEAN (the fused kernel, and
+// k_decide wherever the guard-banded decision applies: no all_mi, no forced split): the
+// wave-parallel exact MI rounds and the walk path are compiled out -- a slice the guard band
+// sends to the exact sums runs the block-sequential sums instead (over the LDS terms on the
+// wave path) -- so the kernel carries the register pressure of the fast decision only
+template <typename T, bool EMBED, bool FUSEDK = false, bool LEAN = FUSEDK>
 __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const FusedScan* fz, const int b, const int role,
                                             codec_params P,
                                             uint32_t* __restrict__ ghist_all, uint32_t* __restrict__ gor,
@@ -1368,14 +1369,23 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     // requested now, parked in LDS just before the windows: a store here would hold the
     // workgroup until the load returns (one global round trip ahead of pass 1)
     const u64 pay_v = fz ? fz->pay_v : (EMBED && pay_in_lds && role == 0 && t < E.pw) ? E.payload[(size_t)b * E.pw + t] : 0ull;
+    // 16-bit slices whose values stay below 4096 (12-bit CT): each thread's 4 bins [4t, 4t + 4)
+    // of the global histogram are requested together with the OR word instead of one round
+    // trip after it (bins at or above the range read as zero: the workspace is kept clean)
+    constexpr bool kSpec = sizeof(T) == 2;
+    uint4 spec = make_uint4(0u, 0u, 0u, 0u);
+    if (kSpec && !fz) spec = reinterpret_cast<const uint4*>(hist)[t];
     // ---- bins that can be non-zero: [0, Rp), Rp = next power of two above OR(pixels)
     const uint32_t orv = fz ? fz->orv : gor[b];
     int Rp = orv ? (1 << (32 - __clz((int)orv))) : 1;
     // fused (k_scan_decide): pass 1 reads the counts from the scan's LDS histogram
     const uint32_t* flds = (fz && fz->lds_ok) ? fz->lds : nullptr;
     if (Rp > R) Rp = R;
-    const int bpt = Rp > 1024 ? Rp / 1024 : 1;     // <= 64 bins per thread
+    // <= 64 bins per thread; 16-bit slices below 4096 take 4 per thread (threads past the range
+    // hold none), the speculative load's layout
+    const int bpt = Rp > 4096 ? Rp / 1024 : kSpec ? 4 : Rp > 1024 ? Rp / 1024 : 1;
     const int v0 = t * bpt;
+    const bool use_spec = kSpec && !fz && bpt == 4;
 
     // ---- pass 1: non-zero bins (bitmask), per-plane popcounts (the planes of codec.py:571)
     u64 nzmask = 0;
@@ -1440,7 +1450,10 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
 #pragma unroll
         for (int u = 0; u < 16; ++u) {            // 16 loads in flight, then the adds
             const int v = v0 + k0 + u;
-            cc[u] = (k0 + u < bpt && v < Rp) ? (flds ? (flds[v >> 1] >> (16 * (v & 1))) & 0xFFFFu : hist[v]) : 0u;
+            if (use_spec && u < 4)
+                cc[u] = v < Rp ? (u == 0 ? spec.x : u == 1 ? spec.y : u == 2 ? spec.z : spec.w) : 0u;
+            else
+                cc[u] = (k0 + u < bpt && v < Rp) ? (flds ? (flds[v >> 1] >> (16 * (v & 1))) & 0xFFFFu : hist[v]) : 0u;
         }
         if (lut_pre) {
 #pragma unroll
@@ -1503,7 +1516,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     const bool wfast = lut_ok && wplanes >= 1 && knob_dev_decide_fast(P);
     // (compiled out of the fused kernel: a wide slice there sums its terms from global memory
     // on the block path -- with the guard band that is H(Y) alone for nearly every slice)
-    const bool walk = !FUSEDK && wide && lut_ok && !wfast && m > 1;
+    const bool walk = !LEAN && wide && lut_ok && !wfast && m > 1;
     double* tl = reinterpret_cast<double*>(list);
     uint16_t* rv = reinterpret_cast<uint16_t*>(tl + (wfast ? m : 0));
     u64* pm = reinterpret_cast<u64*>(reinterpret_cast<char*>(list) + off_pm);
@@ -1811,7 +1824,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     double cum = 0.0;
     if (fs) { s = fs; decided = true; cum = fast_cum; }   // the exact loops below stop at once
     const bool need_decision = (P.fixed_s <= 0);
-    if (!FUSEDK && wfast && nsplit > 0 && !fs) {
+    if (!LEAN && wfast && nsplit > 0 && !fs) {
         // split decision: H(Y) here (wave 15) while the plane workgroups sum their orders,
         // then thread 0 takes the planes in order exactly like the sequential loop
         const int wv = t >> 6, lane = t & 63;
@@ -1857,7 +1870,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
         Hy = hy_sh;
         if (t == 0 && need_offset) { bsc = best_sc[0]; bix = best_ix[0]; }
         offset_done = true;
-    } else if (!FUSEDK && wfast) {
+    } else if (!LEAN && wfast) {
         // H(Y) by wave 0; then rounds of `wplanes` planes, plane i0+w on wave w: its joint
         // bincount order (bit-i-clear bins ascending, then bit-i-set bins, codec.py:546-551)
         // is written to its own list and summed with np_sum_wave.  Thread 0 then walks the
@@ -2147,7 +2160,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     }
     // the block-sequential path: slices off the wave path, and the fused kernel's exact sums
     // (its terms stay in LDS: joint orders at jl, tree slots at vals[512..], the layouts kept)
-    const bool blockp = lut_ok && !walk && (!wfast || (FUSEDK && !fs));
+    const bool blockp = lut_ok && !walk && (!wfast || (LEAN && !fs));
     const double* bt = wfast ? tl : terms;
     uint16_t* bl = wfast ? jl : list;
     double* bv = wfast ? vals + 512 : vals;
@@ -2359,7 +2372,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     if (t == 0) { gkey[b] = 0ull; gor[b] = 0u; }
 }
 
-template <typename T, bool EMBED = false>
+template <typename T, bool EMBED = false, bool LEAN = false>
 __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __restrict__ ghist_all,
                                                  uint32_t* __restrict__ gor, double* __restrict__ gterms,
                                                  u64* __restrict__ gkey, const double* __restrict__ exact,
@@ -2371,7 +2384,7 @@ __global__ __launch_bounds__(1024) void k_decide(codec_params P, uint32_t* __res
                                                  u64* __restrict__ plane_slots, int nsplit, uint32_t spin_max,
                                                  int dbg_late) {
     __shared__ DecideSmem<T, EMBED> S;
-    decide_body<T, EMBED>(S, nullptr, (int)blockIdx.x, (int)blockIdx.y, P, ghist_all, gor, gterms, gkey, exact, exact_cap, exact_edge_only, fast_blocks,
+    decide_body<T, EMBED, false, LEAN>(S, nullptr, (int)blockIdx.x, (int)blockIdx.y, P, ghist_all, gor, gterms, gkey, exact, exact_cap, exact_edge_only, fast_blocks,
                           lut, lut_len, table, slice_class, meta_all, E, plane_slots, nsplit, spin_max, dbg_late);
 }
 
@@ -3520,11 +3533,19 @@ static int plan_impl(const codec_params* P, const void* cover, void* stego, cons
     const int dbg_late = (int)debug_knob("CODEC_DECIDE_DEBUG_LATE", 0) - 1;
     ProfScope prof(st, E ? CODEC_K_DECIDE_EMBED : CODEC_K_DECIDE);
     const EmbedArgs Ev = E ? *E : EmbedArgs{nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
-#define DEC(TT, EM) hipLaunchKernelGGL((k_decide<TT, EM>), dim3(P->B, 1 + nsplit), dim3(1024), 0, st, Pv, hist, orv, terms, keys, exact, \
-                                       L.exact_cap, edge_only, fast ? 1 : 0, log2_lut, (long long)lut_len, table, slice_class, meta, Ev, \
-                                       slots, nsplit, spin_max, dbg_late)
-    if (P->in_bytes == 2) { if (E) DEC(uint16_t, true); else DEC(uint16_t, false); }
-    else { if (E) DEC(uint8_t, true); else DEC(uint8_t, false); }
+    // lean instantiation (no wave-parallel exact rounds, no walk path: fewer registers, no
+    // spills) where the guard band decides -- every call without all_mi / fixed_s / a split
+    const bool lean = nsplit == 0 && P->fixed_s <= 0 && !P->all_mi && !(Pv.reserved & 8) && knob("CODEC_DECIDE_LEAN", 1);
+#define DEC(TT, EM, LN) hipLaunchKernelGGL((k_decide<TT, EM, LN>), dim3(P->B, 1 + nsplit), dim3(1024), 0, st, Pv, hist, orv, terms, keys, \
+                                       exact, L.exact_cap, edge_only, fast ? 1 : 0, log2_lut, (long long)lut_len, table, slice_class, \
+                                       meta, Ev, slots, nsplit, spin_max, dbg_late)
+    if (P->in_bytes == 2) {
+        if (lean) { if (E) DEC(uint16_t, true, true); else DEC(uint16_t, false, true); }
+        else { if (E) DEC(uint16_t, true, false); else DEC(uint16_t, false, false); }
+    } else {
+        if (lean) { if (E) DEC(uint8_t, true, true); else DEC(uint8_t, false, true); }
+        else { if (E) DEC(uint8_t, true, false); else DEC(uint8_t, false, false); }
+    }
 #undef DEC
     const hipError_t e2 = hipGetLastError();
     if (e2 != hipSuccess) return reclear(set_err(-(int)e2, "launch k_decide: %s", hipGetErrorString(e2)));

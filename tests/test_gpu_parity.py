@@ -32,7 +32,7 @@ def _run_case(case, all_mi=True, beta=None):
     return codec, enc
 
 
-@pytest.fixture(params=["split", "waves", "block", "fused"])
+@pytest.fixture(params=["split", "waves", "waves_full", "block", "fused"])
 def decide_path(request, monkeypatch):
     """k_decide's split decision (default for small batches: one plane workgroup per MI
     plane), its one-workgroup wave-parallel MI path (CODEC_DECIDE_SPLIT=0; the default for
@@ -41,13 +41,17 @@ def decide_path(request, monkeypatch):
     codec_encode unfused (codec_plan then the separate k_embed launch).  "fused": the scan,
     decision and embed in one launch (k_scan_decide, CODEC_FUSED_DECIDE=2 forces it on these
     one-slice batches; cases it does not take -- uint8, other block sizes, edge blocks -- run
-    the separate kernels)."""
+    the separate kernels).  "waves" runs the lean k_decide (guard-band fallbacks on the block
+    path) unless all_mi asks for every exact value; "waves_full" keeps the wave-parallel exact
+    rounds for the fallbacks as well (CODEC_DECIDE_LEAN=0)."""
     if request.param == "fused":
         monkeypatch.setenv("CODEC_FUSED_DECIDE", "2")
     if request.param == "split":   # plane workgroups also without all_mi (default: all_mi only)
         monkeypatch.setenv("CODEC_DECIDE_SPLIT", "2")
-    if request.param == "waves":
+    if request.param in ("waves", "waves_full"):
         monkeypatch.setenv("CODEC_DECIDE_SPLIT", "0")
+    if request.param == "waves_full":   # the k_decide instantiation with the wave-parallel exact
+        monkeypatch.setenv("CODEC_DECIDE_LEAN", "0")   # rounds also without all_mi (guard fallbacks)
     if request.param == "block":
         monkeypatch.setenv("CODEC_DECIDE_WAVES", "0")
         monkeypatch.setenv("CODEC_FUSED_EMBED", "0")
