@@ -93,7 +93,7 @@ def test_committed_pmc_summaries_resolve_every_bench_instance():
         assert bench.pmc_traffic(tag, 1, 2048, 2048, "ct12", ta) is not None, tag
     # every source is this round's
     for tag, shape in (("k_pee_embed1", (256, 2048, 2048)), ("k_scan_decide", (256, 512, 512)), ("k_scan_fast", (1, 2048, 2048))):
-        assert "profiles/r05/" in bench.pmc_traffic(tag, *shape, "ct12", {2: "false"} if tag == "k_pee_embed1" else {})["source"]
+        assert "profiles/r06/" in bench.pmc_traffic(tag, *shape, "ct12", {2: "false"} if tag == "k_pee_embed1" else {})["source"]
 
 
 def _launcher(env_extra):
