@@ -536,3 +536,52 @@ def test_guard_band_ties_fall_back_to_reference_s(case, decide_path):
         _, enc = _run_case(case, all_mi=False, beta=beta)
         m = enc.records()[0]
         assert m.flags & _lib.FLAG_INFO_FAST and m.s == _ref_loop(mis, H, beta)[0] == 2
+
+
+def _mixed_covers(kind, n, h, w, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        k = kind[i % len(kind)]
+        if k == "smooth":     # few values, large counts (a low-entropy slice: small H(Y))
+            y, x = np.mgrid[:h, :w]
+            out.append((((x // 7 + y // 5) % 9) * 3 + rng.integers(0, 2, (h, w))).astype(np.uint16))
+        elif k == "sparse":   # ~200 distinct 16-bit values
+            vals = np.sort(rng.choice(65536, 200, replace=False)).astype(np.uint16)
+            out.append(vals[rng.integers(0, vals.size, (h, w))])
+        else:
+            out.append(synth.GENERATORS[k](h, w, seed + i))
+    return np.stack(out)
+
+
+@pytest.mark.parametrize("dtype", ["uint16", "uint8"])
+def test_guard_band_random_betas_batch(dtype, decide_path):
+    """The guard-banded decision over a mixed batch and a sweep of beta, including betas one
+    part in 1e12 from a slice's prefix tie (inside the band: that slice falls back to the exact
+    sums while the others of the same launch take the fast route): s equals the reference
+    loop's on the oracle's float64 MI values (oracle/ref_cpu.py, pinned to the reference)."""
+    kinds = ["ct12", "u16", "smooth", "sparse"] if dtype == "uint16" else ["u8"]
+    B, h, w = 12, 96, 128
+    covers = _mixed_covers(kinds, B, h, w, 77) if dtype == "uint16" else \
+        np.stack([synth.u8(h, w, 70 + i) for i in range(B)])
+    nb = 8 * covers.dtype.itemsize
+    tabs = []
+    for i in range(B):
+        mis = [R.mutual_information((covers[i] >> p) & 1, covers[i]) for p in range(nb)]
+        tabs.append((mis, R.entropy(covers[i])))
+    betas = [0.0, 0.05, 0.2, 0.35, 0.5, 0.65, 0.8, 0.95, 1.0, 1.2]
+    for i in (1, 2, 5):   # near-ties of slice i's prefix 2
+        c = sum(tabs[i][0][:2])
+        if c > 0:
+            b0 = c / tabs[i][1]
+            betas += [b0 * (1 + 1e-12), b0 * (1 - 1e-12)]
+    msgs = [synth.payload(20 + 3 * i, 500 + i) for i in range(B)]
+    fallbacks = 0
+    for beta in betas:
+        codec = Codec(B, h, w, dtype=dtype, beta=beta, block=16)
+        enc = codec.encode(torch.from_numpy(covers).cuda(), msgs)
+        for i, m in enumerate(enc.records()):
+            assert m.s == _ref_loop(tabs[i][0], tabs[i][1], beta)[0], (beta, i)
+            assert m.entropy == tabs[i][1]
+            fallbacks += bool(m.flags & _lib.FLAG_GUARD_FALLBACK)
+    assert fallbacks >= 1        # the near-tie betas reached the exact sums
