@@ -97,6 +97,50 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
 #endif
 }
 
+// ---- float64 across a wave without the LDS crossbar (DPP and gfx950's permlane swaps): a
+// butterfly, so the order of additions is NOT numpy's -- for approximate sums only (the
+// guard-banded decision's H(Y) and walk)
+template <int CTRL, bool BC>
+__device__ __forceinline__ double dpp_f64(double x) {
+    const long long v = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, BC);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(v >> 32), CTRL, 0xF, 0xF, BC);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(uint32_t)lo);
+}
+// x + (x of lane ^ 32) / (lane ^ 16), every lane (v_permlane32/16_swap of a register with itself)
+__device__ __forceinline__ double xor32_sum_f64(double x) {
+    const long long v = __double_as_longlong(x);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(v >> 32), (unsigned)(v >> 32), false, false);
+    return __longlong_as_double(((long long)hi[0] << 32) | (long long)lo[0]) +
+           __longlong_as_double(((long long)hi[1] << 32) | (long long)lo[1]);
+}
+__device__ __forceinline__ double xor16_sum_f64(double x) {
+    const long long v = __double_as_longlong(x);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(v >> 32), (unsigned)(v >> 32), false, false);
+    return __longlong_as_double(((long long)hi[0] << 32) | (long long)lo[0]) +
+           __longlong_as_double(((long long)hi[1] << 32) | (long long)lo[1]);
+}
+// the wave's sum in every lane
+__device__ __forceinline__ double wave_sum_f64(double x) {
+    x = xor32_sum_f64(x);
+    x = xor16_sum_f64(x);
+    x += dpp_f64<0x128, false>(x);   // row_ror:8
+    x += dpp_f64<0x124, false>(x);   // row_ror:4
+    x += dpp_f64<0x4E, false>(x);    // quad_perm [2,3,0,1]
+    x += dpp_f64<0xB1, false>(x);    // quad_perm [1,0,3,2]
+    return x;
+}
+// inclusive scan inside each 16-lane row (row_shr with zero fill)
+__device__ __forceinline__ double row_incl_scan_f64(double x) {
+    x += dpp_f64<0x111, true>(x);
+    x += dpp_f64<0x112, true>(x);
+    x += dpp_f64<0x114, true>(x);
+    x += dpp_f64<0x118, true>(x);
+    return x;
+}
+
 // exclusive scan over the block (NT threads); sh needs NT/64+1 words
 template <int NT>
 __device__ uint32_t block_excl_scan(uint32_t x, uint32_t* sh, uint32_t* total) {
@@ -163,8 +207,10 @@ __device__ uint32_t block_excl_scan_lds(uint32_t x, uint32_t* sh, uint32_t* tota
     lds_barrier();
     const uint32_t wt = lane < NT / 64 ? sh[lane] : 0u;
     const uint32_t wi = wave_incl_scan(wt);
-    const uint32_t pre = wv ? (uint32_t)__shfl(wi, wv - 1, 64) : 0u;
-    *total = (uint32_t)__shfl(wi, NT / 64 - 1, 64);
+    // the wave index is uniform: readlane instead of a bpermute round trip through the LDS crossbar
+    const int wvs = __builtin_amdgcn_readfirstlane(wv);
+    const uint32_t pre = wvs ? (uint32_t)__builtin_amdgcn_readlane((int)wi, wvs - 1) : 0u;
+    *total = (uint32_t)__builtin_amdgcn_readlane((int)wi, NT / 64 - 1);
     lds_barrier();   // sh reusable
     return pre + inc - x;
 }

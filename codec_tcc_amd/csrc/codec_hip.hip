@@ -1199,10 +1199,13 @@ struct ListTerm {
 #define PTS(k) do { if (threadIdx.x == 0) reinterpret_cast<long long*>(gterms + (size_t)b * HistCfg<T>::kBins)[HistCfg<T>::kBins - 80 + 4 * (role - 1) + (k)] = wall_clock64(); } while (0)
 // wave path: lane 0 of wave k stamps the end of its first round's work (slot R - 80 + k)
 #define WVTS(k) do { if ((threadIdx.x & 63) == 0 && role == 0) reinterpret_cast<long long*>(gterms + (size_t)b * HistCfg<T>::kBins)[HistCfg<T>::kBins - 80 + (k)] = wall_clock64(); } while (0)
+// every wave's lane 0 stamps phase boundary `ph` (0: pass 1 done, 1: terms done) into its own slot
+#define WPH(ph) do { if ((threadIdx.x & 63) == 0 && role == 0) reinterpret_cast<long long*>(gterms + (size_t)b * HistCfg<T>::kBins)[HistCfg<T>::kBins - 112 + 16 * (ph) + (threadIdx.x >> 6)] = wall_clock64(); } while (0)
 #else
 #define DTS(k) do { } while (0)
 #define PTS(k) do { } while (0)
 #define WVTS(k) do { } while (0)
+#define WPH(ph) do { } while (0)
 #endif
 // CODEC_DECIDE_WAVES=0 (host env, passed in codec_params.reserved bit 0) forces the
 // block-sequential decision path (A/B and tests)
@@ -1474,6 +1477,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
         }
     }
     DTS(12);
+    WPH(0);
     // the entry prefetches are consumed here, with pass 1's loads (issued before them, so
     // no extra wait): left to themselves they sink to their first use after the decision
     if (!fz) asm volatile("" ::"v"((uint32_t)key0), "v"((uint32_t)(key0 >> 32)), "s"(cls));
@@ -1567,6 +1571,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
         }
     }
     if (try_fast) DTS(8);
+    WPH(1);
     if (try_fast && walk) {   // wide slices: no term array -- the count codes of pass 1, a wave per group
         const int lane = t & 63, wv = t >> 6, ng = Rp / 64;
         for (int g0 = wv; g0 < ng; g0 += 16 * 8) {
@@ -1645,9 +1650,7 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
             if (t < 16 * kLayW) reinterpret_cast<int32_t*>(vals)[t] = lay_v;   // the class's 16 layouts (one per s)
             np_leaves_block1024(RankTerm{tl}, (int)m, vals + 512, 8);   // waves 8.. (clear of waves 0-2)
         }
-        double hp = hy_part;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) hp += __shfl_xor(hp, o, 64);
+        const double hp = wave_sum_f64(hy_part);  // any order: the fast H(Y)
         if (lane == 0) hxy_sh[wv] = hp;           // scratch until the exact rounds
         const int nb = min(P.nbits, 16);
         double hx = 0.0;                          // wave 1, lane i: H(X) of plane i
@@ -1660,22 +1663,16 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
         lds_barrier();
         DTS(7);
         if (wv == 1) {   // the walk, lane-parallel: prefix sums of H(X) against beta * H(Y)
-            double hyf = lane < 16 ? hxy_sh[lane] : 0.0;
-#pragma unroll
-            for (int o = 8; o >= 1; o >>= 1) hyf += __shfl_xor(hyf, o, 64);
-            const double tg = P.beta * -__shfl(hyf, 0, 64);
-            double c = hx;                        // 0 for a constant plane, codec.py:520-523
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) {
-                const double y = __shfl_up(c, o, 64);
-                if (lane >= o) c += y;
-            }
+            const double tg = P.beta * -wave_sum_f64(lane < 16 ? hxy_sh[lane] : 0.0);
+            const double c = row_incl_scan_f64(hx);   // lanes 0..15; 0 for a constant plane (codec.py:520-523)
             const u64 reach = __ballot(lane < nb && c >= tg);
             const int sf = reach ? __ffsll((long long)reach) : 1;   // codec.py:591-593; s = 1 if never
             const int nev = reach ? sf : nb;                         // planes the loop evaluates
             // every evaluated prefix more than the guard from its target (a NaN fails it too)
             const bool clear = __ballot(lane < nev && !(fabs(c - tg) > kDecideGuard)) == 0ull;
-            const double cum = __shfl(c, nev - 1, 64);
+            const double cum = __longlong_as_double(
+                ((long long)__builtin_amdgcn_readlane((int)(__double_as_longlong(c) >> 32), nev - 1) << 32) |
+                (long long)(uint32_t)__builtin_amdgcn_readlane((int)__double_as_longlong(c), nev - 1));
             if (clear && lane < nev) mis_sh[lane] = hx;
             if (lane == 0) { ctl_sh[2] = clear ? sf : 0; hxy_sh[0] = cum; }   // after the wave's reads
             WVTS(1);

@@ -48,6 +48,12 @@ def main():
           f"wave1 walk {np.median(wv[:, 1] - raw[:, 7]) * 0.01:.2f}, wave2 offset {np.median(wv[:, 2] - raw[:, 7]) * 0.01:.2f}), "
           f"to DTS2 {d(9, 2):.2f}, H(Y)/offset {d(2, 3):.2f}, ->4 {d(3, 4):.2f}, windows {d(4, 5):.2f}, "
           f"embed {d(5, 11):.2f}; decision total {d(0, 5):.2f} us")
+    ph = allr[:, R - 112:R - 80].reshape(B, 2, 16)
+    if (ph > 0).all():   # per-wave ends of pass 1 and of the terms, relative to the entry stamp
+        rel = (ph - raw[:, 0:1, None]) * 0.01
+        print("  per wave, median over slices (us after entry): pass 1 end " +
+              " ".join(f"{np.median(rel[:, 0, w]):.2f}" for w in range(16)) +
+              "; terms end " + " ".join(f"{np.median(rel[:, 1, w]):.2f}" for w in range(16)))
 
 
 if __name__ == "__main__":
