@@ -1471,9 +1471,18 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
             if (cc[u]) {
                 if (cnt_lds) cnt_sh[v] = cc[u];
                 nzmask |= 1ull << (k0 + u);
+                if (bpt != 4) {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) pop[i] += ((v >> i) & 1) ? cc[u] : 0u;
+                    for (int i = 0; i < 16; ++i) pop[i] += ((v >> i) & 1) ? cc[u] : 0u;
+                }
             }
+        }
+        if (bpt == 4) {   // bins 4t .. 4t + 3: planes 0 and 1 differ inside, planes >= 2 are bits of t
+            const uint32_t tot = cc[0] + cc[1] + cc[2] + cc[3];
+            pop[0] = cc[1] + cc[3];
+            pop[1] = cc[2] + cc[3];
+#pragma unroll
+            for (int i = 2; i < 16; ++i) pop[i] = ((t >> (i - 2)) & 1) ? tot : 0u;
         }
     }
     DTS(12);
@@ -1492,18 +1501,29 @@ __device__ __forceinline__ void decide_body(DecideSmem<T, EMBED>& S, const Fused
     DTS(13);
     {   // the 16 per-plane sums of the wave as one reduce-scatter: 8 + 4 + 2 + 1 shuffles leave
         // lane l with plane l >> 2 summed over 16 lanes, two more finish it (17 instead of 96)
+        // (lane ^ 32 and ^ 16 by gfx950's permlane swaps, ^ 8 by a DPP row rotation, ^ 4 by a
+        // swizzle, ^ 2 and ^ 1 by quad permutes: no bpermute round trip through the LDS crossbar)
         const int lane = t & 63;
         uint32_t a[8], b4[4], c2[2];
-        const bool h5 = (lane >> 5) & 1, h4 = (lane >> 4) & 1, h3 = (lane >> 3) & 1, h2 = (lane >> 2) & 1;
+        const bool h3 = (lane >> 3) & 1, h2 = (lane >> 2) & 1;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = (h5 ? pop[8 + j] : pop[j]) + __shfl_xor(h5 ? pop[j] : pop[8 + j], 32, 64);
+        for (int j = 0; j < 8; ++j) {   // lanes < 32 keep plane j, lanes >= 32 plane 8 + j
+            const auto sw = __builtin_amdgcn_permlane32_swap(pop[j], pop[8 + j], false, false);
+            a[j] = sw[0] + sw[1];
+        }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) b4[j] = (h4 ? a[4 + j] : a[j]) + __shfl_xor(h4 ? a[j] : a[4 + j], 16, 64);
+        for (int j = 0; j < 4; ++j) {   // lanes with bit 4 clear keep a[j], the others a[4 + j]
+            const auto sw = __builtin_amdgcn_permlane16_swap(a[j], a[4 + j], false, false);
+            b4[j] = sw[0] + sw[1];
+        }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) c2[j] = (h3 ? b4[2 + j] : b4[j]) + __shfl_xor(h3 ? b4[j] : b4[2 + j], 8, 64);
-        uint32_t x = (h2 ? c2[1] : c2[0]) + __shfl_xor(h2 ? c2[0] : c2[1], 4, 64);
-        x += __shfl_xor(x, 2, 64);
-        x += __shfl_xor(x, 1, 64);
+        for (int j = 0; j < 2; ++j)     // row_ror:8 inside a 16-lane row is lane ^ 8
+            c2[j] = (h3 ? b4[2 + j] : b4[j]) +
+                    (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(h3 ? b4[j] : b4[2 + j]), 0x128, 0xF, 0xF, false);
+        uint32_t x = (h2 ? c2[1] : c2[0]) +
+                     (uint32_t)__builtin_amdgcn_ds_swizzle((int)(h2 ? c2[0] : c2[1]), 0x101F);   // lane ^ 4
+        x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+        x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
         if ((lane & 3) == 0 && x) atomicAdd(&pops_sh[lane >> 2], x);
     }
     DTS(1);
