@@ -59,8 +59,12 @@ def main():
         codec.decode(stego, maps, meta, payload_words=pl.payload_words, map_words=pl.map_words, cover=cov2,
                      payload=pay)
 
+    def enc():
+        codec.encode(covers, pl, stego=stego, maps=maps, meta=meta, check=False)
+
     if a.inplace:
         work = covers.clone()
+        enc = None   # an in-place encode alone would leave the buffer embedded
 
         def step():   # noqa: F811
             codec.encode(work, pl, stego=work, maps=maps, meta=meta, check=False)
@@ -90,12 +94,24 @@ def main():
                 per.setdefault(_lib.KERNEL_TAGS[tags[k]], []).append(ms[k])
             for k, v in per.items():
                 res[i].setdefault(k, []).append(float(np.mean(v)))
+            # wall time of the step and of its encode half (no profile window: launch gaps included)
+            for name, fn in (("step_ms", step), ("encode_ms", enc)):
+                if fn is None:
+                    continue
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.steps):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                res[i].setdefault(name, []).append(e0.elapsed_time(e1) / a.steps)
     if not torch.equal(cov2.view(torch.int16), covers.view(torch.int16)):   # diagnostic configs (CODEC_DIAG_*)
         print("WARNING: round trip not exact under the last configuration", flush=True)
     for i, cfg in enumerate(configs):
         row = {k: round(float(np.median(v)), 4) for k, v in res[i].items()}
+        wall = {k: row.pop(k) for k in ("step_ms", "encode_ms") if k in row}
         tot = round(sum(row.values()), 4)
-        print(json.dumps({"cfg": cfg, "kernels_ms": row, "sum_ms": tot}))
+        print(json.dumps({"cfg": cfg, "kernels_ms": row, "sum_ms": tot, **wall}))
 
 
 if __name__ == "__main__":
