@@ -29,6 +29,23 @@ Scheme (integer only):
               expandable one" -- is the definition the GPU kernels implement.
   decoding    e' = x' - pred; LM -> unchanged; -2T <= e' < 2T -> bit = e' & 1,
               x = pred + (e' >> 1); e' >= 2T -> x = x' - T; else x = x' + T.
+
+Scheme 2, four sublattice passes (the version-16 container's scheme byte 1):
+  lattices    pass 0 (odd, odd) -- scheme 1's candidates; pass 1 (even, even); pass 2 (odd, even);
+              pass 3 (even, odd), as (row, column) parities, with y >= 1 and x >= 1 (so every
+              candidate has its W / N / NW neighbours).  Each lattice's three MED neighbours lie on
+              the other three lattices, so one pass never reads a pixel it writes.
+              Lattice (ry, rx): y = 2i + y0, x = 2j + x0, y0 = 1 if ry else 2, x0 = 1 if rx else
+              2, i < hc = (H - y0 + 1) // 2, j < wc = (W - x0 + 1) // 2, index k = i * wc + j.
+  embed       pass p runs scheme 1 on lattice p of the RUNNING stego (passes 0..p-1 applied),
+              truncating to its capacity: it takes the next min(remaining, capacity_p) payload
+              bits (all candidates processed when it fills up, as scheme 1's truncation).
+              Side information per pass (T, L_p, end_p, LM_p); status 1 when bits remain after
+              pass 3.
+  decoding    passes 3..0 in reverse, each on the image the later passes' decoding restored:
+              pass p's neighbours then hold exactly the values they had when pass p embedded
+              (lattices < p still carry their stego values, lattices > p are restored).  The
+              payload is the concatenation of the passes' bits in pass order.
 """
 from __future__ import annotations
 
@@ -37,13 +54,26 @@ from typing import Dict, Tuple
 import numpy as np
 
 
-def _grids(img: np.ndarray):
+# (row parity, column parity) of pass p's candidates (scheme 2); lattice 0 is scheme 1's
+LATTICES = ((1, 1), (0, 0), (1, 0), (0, 1))
+
+
+def lattice_origin(lattice: int, H: int, W: int):
+    """(y0, x0, hc, wc): lattice candidate (i, j) is pixel (y0 + 2i, x0 + 2j), i < hc, j < wc."""
+    ry, rx = LATTICES[lattice]
+    y0, x0 = (1 if ry else 2), (1 if rx else 2)
+    return y0, x0, max(0, (H - y0 + 1) // 2), max(0, (W - x0 + 1) // 2)
+
+
+def _grids(img: np.ndarray, lattice: int = 0):
     H, W = img.shape
-    hc, wc = H // 2, W // 2
-    x = img[1:2 * hc:2, 1:2 * wc:2].astype(np.int64)
-    a = img[1:2 * hc:2, 0:2 * wc:2].astype(np.int64)
-    b = img[0:2 * hc:2, 1:2 * wc:2].astype(np.int64)
-    c = img[0:2 * hc:2, 0:2 * wc:2].astype(np.int64)
+    y0, x0, hc, wc = lattice_origin(lattice, H, W)
+    ys, xs = slice(y0, y0 + 2 * hc, 2), slice(x0, x0 + 2 * wc, 2)
+    ys1, xs1 = slice(y0 - 1, y0 - 1 + 2 * hc, 2), slice(x0 - 1, x0 - 1 + 2 * wc, 2)
+    x = img[ys, xs].astype(np.int64)
+    a = img[ys, xs1].astype(np.int64)
+    b = img[ys1, xs].astype(np.int64)
+    c = img[ys1, xs1].astype(np.int64)
     return x, a, b, c
 
 
@@ -63,7 +93,7 @@ def classify(x, p, T: int, maxval: int):
 
 
 def pee_embed(cover: np.ndarray, bits: np.ndarray, T: int = 2, maxval: int | None = None,
-              truncate: bool = False) -> Tuple[np.ndarray, Dict]:
+              truncate: bool = False, lattice: int = 0) -> Tuple[np.ndarray, Dict]:
     if cover.dtype not in (np.uint8, np.uint16) or cover.ndim != 2:
         raise ValueError("cover must be a 2-D uint8/uint16 image")
     if T < 1:
@@ -71,7 +101,7 @@ def pee_embed(cover: np.ndarray, bits: np.ndarray, T: int = 2, maxval: int | Non
     maxval = int(np.iinfo(cover.dtype).max) if maxval is None else int(maxval)
     bits = np.asarray(bits, dtype=np.uint8).ravel()
     L = bits.size
-    x, a, b, c = _grids(cover)
+    x, a, b, c = _grids(cover, lattice)
     p = med(a, b, c)
     e, expand, right, safe = classify(x, p, T, maxval)
     es = (expand & safe).ravel()
@@ -94,15 +124,17 @@ def pee_embed(cover: np.ndarray, bits: np.ndarray, T: int = 2, maxval: int | Non
     new = np.where(es, pf + 2 * ef + bit, np.where(rf, xf + T, xf - T))
     out = np.where(proc, new, xf)
     stego = cover.copy()
-    hc, wc = x.shape
-    stego[1:2 * hc:2, 1:2 * wc:2] = out.reshape(hc, wc).astype(cover.dtype)
+    y0, x0, hc, wc = lattice_origin(lattice, *cover.shape)
+    stego[y0:y0 + 2 * hc:2, x0:x0 + 2 * wc:2] = out.reshape(hc, wc).astype(cover.dtype)
     lm = ~safe.ravel()[: end + 1]
-    return stego, {"T": T, "L": L, "end": end, "maxval": maxval, "lm": lm, "capacity": capacity, "status": status}
+    return stego, {"T": T, "L": L, "end": end, "maxval": maxval, "lm": lm, "capacity": capacity, "status": status,
+                   "lattice": lattice}
 
 
 def pee_extract(stego: np.ndarray, side: Dict) -> Tuple[np.ndarray, np.ndarray]:
     T, end, L = side["T"], side["end"], side["L"]
-    x, a, b, c = _grids(stego)
+    lattice = side.get("lattice", 0)
+    x, a, b, c = _grids(stego, lattice)
     p = med(a, b, c).ravel()
     xf = x.ravel()
     e2 = xf - p
@@ -114,9 +146,35 @@ def pee_extract(stego: np.ndarray, side: Dict) -> Tuple[np.ndarray, np.ndarray]:
     bits = (e2[inner] & 1).astype(np.uint8)[:L]
     rec = np.where(inner, p + (e2 >> 1), np.where(act & (e2 >= 2 * T), xf - T, np.where(act, xf + T, xf)))
     cover = stego.copy()
-    hc, wc = x.shape
-    cover[1:2 * hc:2, 1:2 * wc:2] = rec.reshape(hc, wc).astype(stego.dtype)
+    y0, x0, hc, wc = lattice_origin(lattice, *stego.shape)
+    cover[y0:y0 + 2 * hc:2, x0:x0 + 2 * wc:2] = rec.reshape(hc, wc).astype(stego.dtype)
     return bits, cover
+
+
+def pee_embed_multi(cover: np.ndarray, bits: np.ndarray, T: int = 2, maxval: int | None = None,
+                    passes: int = 4) -> Tuple[np.ndarray, Dict]:
+    """Scheme 2: passes 0..passes-1 on lattices 0..passes-1 of the running stego, each taking
+    the next min(remaining, capacity) bits.  Side: T, L (bits embedded), status (1: bits left
+    over), and the per-pass side dicts."""
+    if not 1 <= passes <= 4:
+        raise ValueError("passes must be in 1..4")
+    bits = np.asarray(bits, dtype=np.uint8).ravel()
+    stego, sides, pos = cover.copy(), [], 0
+    for p in range(passes):
+        stego, side = pee_embed(stego, bits[pos:], T, maxval, truncate=True, lattice=p)
+        pos += side["L"]
+        sides.append(side)
+    return stego, {"T": T, "L": pos, "status": 1 if pos < bits.size else 0, "passes": sides,
+                   "maxval": sides[0]["maxval"]}
+
+
+def pee_extract_multi(stego: np.ndarray, side: Dict) -> Tuple[np.ndarray, np.ndarray]:
+    """Inverse of pee_embed_multi: passes in reverse, bits concatenated in pass order."""
+    img, got = stego, []
+    for ps in reversed(side["passes"]):
+        b, img = pee_extract(img, ps)
+        got.append(b)
+    return (np.concatenate(got[::-1]) if got else np.zeros(0, np.uint8)), img
 
 
 def capacity_curve(cover: np.ndarray, tmax: int, maxval: int | None = None) -> np.ndarray:
@@ -139,8 +197,8 @@ def select_T(cover: np.ndarray, L: int, tmax: int = 16, maxval: int | None = Non
     return int(hit[0]) + 1 if hit.size else tmax
 
 
-def capacity(cover: np.ndarray, T: int = 2, maxval: int | None = None) -> int:
+def capacity(cover: np.ndarray, T: int = 2, maxval: int | None = None, lattice: int = 0) -> int:
     maxval = int(np.iinfo(cover.dtype).max) if maxval is None else int(maxval)
-    x, a, b, c = _grids(cover)
+    x, a, b, c = _grids(cover, lattice)
     _e, expand, _r, safe = classify(x, med(a, b, c), T, maxval)
     return int((expand & safe).sum())

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Known-answer vectors of the MED-PEE scheme -> tests/golden/pee_kat.json.
+"""Known-answer vectors of the MED-PEE scheme -> tests/golden/pee_kat.json (scheme 1, one
+pass) and tests/golden/pee_multi_kat.json (scheme 2, four sublattice passes).
 
 Computed by the scalar restatement tests/pee_scalar.py (not by the vectorised oracle they
 then check).  Covers: seeded ct12 / u8 / u16 images (and ct12 x 16 as smooth 16-bit data), even and odd sizes, T = 1..5, a
@@ -66,6 +67,54 @@ def case_inputs(c):
     return img, payload_bits(n, seed), T, mv
 
 
+# scheme 2 (four sublattice passes): (kind, h, w, seed, T, maxval, clip, payload rule); rules
+# against the scheme's total capacity C (bits a payload longer than every pass can take
+# embeds): "pass0" = lattice 0's capacity on the cover (one pass), "two" = that + 3 (spills
+# into pass 1), "all" = C (every pass filled), "over" = C + 40 (status 1), "zero"
+MULTI_CASES = [
+    ("ct12", 32, 48, 11, 2, 4095, False, "two"),
+    ("ct12", 33, 41, 12, 1, 4095, False, "all"),
+    ("ct12", 24, 31, 13, 3, 4095, True, "over"),
+    ("u8", 30, 32, 14, 2, None, True, "two"),
+    ("u8", 27, 20, 15, 1, None, False, "pass0"),
+    ("ct16", 16, 34, 16, 4, None, False, "all"),
+    ("u16", 17, 24, 17, 2, None, True, "over"),
+    ("ct12", 20, 24, 18, 2, 4095, False, "zero"),
+]
+
+
+def multi_case_inputs(c):
+    kind, h, w, seed, T, maxval, clip, rule = c
+    img = make_image(kind, h, w, seed, maxval, clip)
+    mv = int(np.iinfo(img.dtype).max) if maxval is None else int(maxval)
+    _st, side0 = S.embed(img.tolist(), [], T, mv)
+    _st, sides = S.embed_multi(img.tolist(), [1] * (4 * h * w), T, mv)   # every pass filled
+    total = sum(sd["L"] for sd in sides)
+    n = {"pass0": side0["capacity"], "two": side0["capacity"] + 3, "all": total, "over": total + 40,
+         "zero": 0}[rule]
+    return img, payload_bits(n, 500 + seed), T, mv
+
+
+def multi_main():
+    out = []
+    for c in MULTI_CASES:
+        img, bits, T, mv = multi_case_inputs(c)
+        st, sides = S.embed_multi(img.tolist(), [int(b) for b in bits], T, mv)
+        stego = np.array(st, dtype=img.dtype)
+        got, back = S.extract_multi(st, sides)
+        L = sum(sd["L"] for sd in sides)
+        assert got == [int(b) for b in bits[:L]] and back == img.tolist()
+        out.append({"kind": c[0], "h": c[1], "w": c[2], "seed": c[3], "T": T, "maxval": c[5], "clip": c[6],
+                    "rule": c[7], "L_in": int(bits.size), "L": L, "status": 1 if L < bits.size else 0,
+                    "passes": [{"L": sd["L"], "end": sd["end"], "capacity": sd["capacity"], "status": sd["status"],
+                                "lm_hex": np.packbits(np.array(sd["lm"], bool), bitorder="little").tobytes().hex()}
+                               for sd in sides],
+                    "stego_sha256": hashlib.sha256(stego.tobytes()).hexdigest()})
+    with open(os.path.join(HERE, "pee_multi_kat.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(f"{len(out)} cases -> pee_multi_kat.json")
+
+
 def main():
     out = []
     for c in CASES:
@@ -87,3 +136,4 @@ def main():
 
 if __name__ == "__main__":
     main()
+    multi_main()

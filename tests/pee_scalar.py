@@ -16,21 +16,30 @@ def _med(a: int, b: int, c: int) -> int:
     return a + b - c
 
 
-def _cands(img):
-    """(k, y, x, value, prediction) of every candidate in index order: y, x odd."""
+# scheme 2's sublattices as (row parity, column parity); 0 is scheme 1's (odd, odd)
+LATTICES = ((1, 1), (0, 0), (1, 0), (0, 1))
+
+
+def _cands(img, lattice=0):
+    """(k, y, x, value, prediction) of every candidate in index order: pixels whose row and
+    column parities are the lattice's, with y >= 1 and x >= 1, row by row."""
     H, W = len(img), len(img[0])
+    ry, rx = LATTICES[lattice]
     out = []
-    for i in range(H // 2):
-        for j in range(W // 2):
-            y, x = 2 * i + 1, 2 * j + 1
+    for y in range(1, H):
+        if y % 2 != ry:
+            continue
+        for x in range(1, W):
+            if x % 2 != rx:
+                continue
             p = _med(img[y][x - 1], img[y - 1][x], img[y - 1][x - 1])
-            out.append((i * (W // 2) + j, y, x, img[y][x], p))
+            out.append((len(out), y, x, img[y][x], p))
     return out
 
 
-def embed(img, bits, T: int, maxval: int, truncate: bool = True):
+def embed(img, bits, T: int, maxval: int, truncate: bool = True, lattice: int = 0):
     """img: list of lists of ints -> (stego rows, side dict) as pee_cpu.pee_embed."""
-    cands = _cands(img)
+    cands = _cands(img, lattice)
     kinds = []
     for _k, _y, _x, v, p in cands:
         e = v - p
@@ -71,14 +80,14 @@ def embed(img, bits, T: int, maxval: int, truncate: bool = True):
             out[y][x] = v + T
         else:
             out[y][x] = v - T
-    return out, {"T": T, "L": L, "end": end, "lm": lm, "capacity": capacity, "status": status}
+    return out, {"T": T, "L": L, "end": end, "lm": lm, "capacity": capacity, "status": status, "lattice": lattice}
 
 
 def extract(stego, side):
     T, end, L = side["T"], side["end"], side["L"]
     out = [list(r) for r in stego]
     bits = []
-    for idx, (_k, y, x, v, p) in enumerate(_cands(stego)):
+    for idx, (_k, y, x, v, p) in enumerate(_cands(stego, side.get("lattice", 0))):
         if idx > end:
             break
         if side["lm"][idx]:
@@ -92,3 +101,23 @@ def extract(stego, side):
         else:
             out[y][x] = v + T
     return bits[:L], out
+
+
+def embed_multi(img, bits, T: int, maxval: int, passes: int = 4):
+    """Scheme 2: pass p embeds the next bits on lattice p of the running stego (truncating to
+    its capacity); returns (stego rows, [per-pass side dicts])."""
+    out, sides, pos = [list(r) for r in img], [], 0
+    for p in range(passes):
+        out, side = embed(out, bits[pos:], T, maxval, truncate=True, lattice=p)
+        pos += side["L"]
+        sides.append(side)
+    return out, sides
+
+
+def extract_multi(stego, sides):
+    """Passes in reverse; the bits in pass order."""
+    out, parts = [list(r) for r in stego], []
+    for side in reversed(sides):
+        b, out = extract(out, side)
+        parts.append(b)
+    return [b for part in reversed(parts) for b in part], out

@@ -933,6 +933,80 @@ def test_oracle_matches_scheme_kats(k):
     assert np.array_equal(np.array(st2, dtype=img.dtype), st) and side2["end"] == k["end"]
 
 
+# ---- scheme 2: four sublattice passes (tests/golden/pee_multi_kat.json, same generator)
+def _multi_kats():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "pee_multi_kat.json")) as f:
+        return json.load(f)
+
+
+def _multi_kat_inputs(k):
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "make_pee_golden", os.path.join(os.path.dirname(__file__), "golden", "make_pee_golden.py"))
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    img = g.make_image(k["kind"], k["h"], k["w"], k["seed"], k["maxval"], k["clip"])
+    mv = int(np.iinfo(img.dtype).max) if k["maxval"] is None else int(k["maxval"])
+    return img, g.payload_bits(k["L_in"], 500 + k["seed"]), mv
+
+
+@pytest.mark.parametrize("k", _multi_kats(), ids=_kat_id)
+def test_oracle_matches_multipass_kats(k):
+    """Scheme 2: the vectorised oracle's four passes reproduce the scalar restatement's known
+    answers (stego digest; per pass L, end, capacity on the running stego, status, location
+    map) and the reverse passes restore payload and cover."""
+    import hashlib
+    img, bits, mv = _multi_kat_inputs(k)
+    st, side = P.pee_embed_multi(img, bits, k["T"], maxval=mv)
+    assert hashlib.sha256(st.tobytes()).hexdigest() == k["stego_sha256"]
+    assert (side["L"], side["status"]) == (k["L"], k["status"])
+    for ps, kp in zip(side["passes"], k["passes"]):
+        assert (ps["L"], ps["end"], ps["capacity"], ps["status"]) == (kp["L"], kp["end"], kp["capacity"], kp["status"])
+        assert np.packbits(ps["lm"], bitorder="little").tobytes().hex() == kp["lm_hex"]
+    got, back = P.pee_extract_multi(st, side)
+    np.testing.assert_array_equal(got, bits[: k["L"]])
+    np.testing.assert_array_equal(back, img)
+
+
+@pytest.mark.parametrize("h,w", [(32, 48), (33, 41), (2, 9), (9, 2), (1, 7), (6, 1)])
+def test_lattice_geometry(h, w):
+    """Every pixel with y >= 1 and x >= 1 is a candidate of exactly one lattice; lattice 0 is
+    scheme 1's (odd, odd) set in scheme 1's index order, so pass 0 of scheme 2 IS scheme 1."""
+    seen = np.zeros((h, w), int)
+    for lat in range(4):
+        y0, x0, hc, wc = P.lattice_origin(lat, h, w)
+        assert hc >= 0 and wc >= 0
+        seen[y0:y0 + 2 * hc:2, x0:x0 + 2 * wc:2] += 1
+    assert (seen[1:, 1:] == 1).all() and seen[0].sum() == 0 and seen[:, 0].sum() == 0
+    assert P.lattice_origin(0, h, w)[2:] == (h // 2, w // 2)
+    img = synth.ct12(max(h, 2), max(w, 2), 4)[:h, :w]
+    bits = np.ones(3, np.uint8)
+    a, sa = P.pee_embed(img, bits, 2, 4095, truncate=True)
+    b, sb = P.pee_embed(img, bits, 2, 4095, truncate=True, lattice=0)
+    np.testing.assert_array_equal(a, b)
+
+
+def test_multipass_capacity_gain():
+    """The point of scheme 2: a 512^2 ct12 slice's 1 KB payload (8 192
+    bits) needs T = 4 on one lattice but fits at T = 2 over the sublattice passes, at a lower
+    distortion (squared error: more pixels move, by about 2 instead of 4)."""
+    img = synth.ct12(512, 512, 3)
+    bits = np.random.default_rng(5).integers(0, 2, 8192).astype(np.uint8)
+    assert P.capacity(img, 2, 4095) < 8192 <= P.capacity(img, 4, 4095)
+    st, side = P.pee_embed_multi(img, bits, 2, maxval=4095)
+    assert side["status"] == 0 and side["L"] == 8192
+    st1, side1 = P.pee_embed(img, bits, 4, 4095)
+    def sse(a):
+        return int(((a.astype(np.int64) - img.astype(np.int64)) ** 2).sum())
+    assert sse(st) < 0.75 * sse(st1)
+    got, back = P.pee_extract_multi(st, side)
+    np.testing.assert_array_equal(got, bits)
+    np.testing.assert_array_equal(back, img)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("ss", ["default", "slice_serial"])
 @pytest.mark.parametrize("k", _kats(), ids=_kat_id)
