@@ -3866,3 +3866,417 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
 }
 
 }  // extern "C"
+
+// ===================================================================== scheme 2: sublattices
+// Four passes (oracle/pee_cpu.py, "Scheme 2"): pass p runs the scheme above on lattice p of
+// the running image -- (odd, odd), (even, even), (odd, even), (even, odd) as (row, column)
+// parities, y >= 1, x >= 1 -- taking the next min(remaining, capacity_p) payload bits; the
+// decoder undoes them in reverse.  Each lattice's W / N / NW neighbours lie on the other
+// three, so within a pass every candidate is independent and the pass runs in place: the
+// tile kernels below read a candidate and its three neighbours and write only the candidate.
+// The passes use tile counts (1024 candidates per tile, a workgroup of 256 lanes, 4
+// consecutive candidates each) and a per-slice scan, as the two-pass scheme-1 path does;
+// a pass with no bits left for a slice skips that slice's tiles (capacity reported as -1).
+// Pass p's payload bits start at base_p = L_0 + ... + L_{p-1} of the slice (its earlier
+// passes' records, `metas` = [passes][B]).
+struct PeeLat {
+    int y0, x0, hc, wc;
+};
+__host__ __device__ __forceinline__ PeeLat pee_lattice(int lat, int H, int W) {
+    const bool ry = lat == 0 || lat == 2, rx = lat == 0 || lat == 3;
+    PeeLat g;
+    g.y0 = ry ? 1 : 2;
+    g.x0 = rx ? 1 : 2;
+    g.hc = H - g.y0 + 1 > 0 ? (H - g.y0 + 1) / 2 : 0;
+    g.wc = W - g.x0 + 1 > 0 ? (W - g.x0 + 1) / 2 : 0;
+    return g;
+}
+
+// the 4 candidates k0 .. k0 + 3 (those <= kmax) of a lane: pixel offsets, values, neighbours
+template <typename T>
+struct LatQuad {
+    size_t o[4];
+    int x[4], a[4], b[4], c[4];
+    __device__ __forceinline__ void load(const T* img, int W, const PeeLat& g, int k0, int kmax) {
+        int i = k0 / g.wc, j = k0 - (k0 / g.wc) * g.wc;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            // candidates past kmax load pixel (1, 1) instead (in bounds whenever a lattice has a
+            // candidate) and are ignored by the caller: no divergent loads
+            const bool ok = k0 + u <= kmax;
+            const size_t oo = ok ? (size_t)(g.y0 + 2 * i) * W + (size_t)(g.x0 + 2 * j) : (size_t)W + 1;
+            o[u] = oo;
+            x[u] = img[oo]; a[u] = img[oo - 1]; b[u] = img[oo - W]; c[u] = img[oo - W - 1];
+            const bool wrap = j + 1 == g.wc;   // branch-free step to candidate k0 + u + 1
+            i += wrap ? 1 : 0;
+            j = wrap ? 0 : j + 1;
+        }
+    }
+};
+
+__device__ __forceinline__ int pee_pass_base(const codec_pee_meta* metas, int pass, int B, int b) {
+    int base = 0;
+    for (int q = 0; q < pass; ++q) base += metas[(size_t)q * B + b].L;
+    return base;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_pee_lat_count(const T* __restrict__ img, int H, int W, int lat, int T0,
+                                                       int maxval, const int32_t* __restrict__ lengths,
+                                                       const codec_pee_meta* __restrict__ metas, int pass, int B,
+                                                       uint32_t* __restrict__ tile_cnt_all, int ntiles_max) {
+    __shared__ uint32_t sh[8];
+    const int b = blockIdx.y;
+    if (lengths[b] - pee_pass_base(metas, pass, B, b) <= 0) return;   // nothing left: uniform
+    const PeeLat g = pee_lattice(lat, H, W);
+    const int nc = g.hc * g.wc, ntiles = (nc + PEE_TILE - 1) / PEE_TILE;
+    const T* src = img + (size_t)b * H * W;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int k0 = t * PEE_TILE + 4 * threadIdx.x;
+        LatQuad<T> q;
+        q.load(src, W, g, k0, nc - 1);
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (k0 + u < nc) {
+                const PeeCand pc = pee_classify(q.x[u], q.a[u], q.b[u], q.c[u], T0, maxval);
+                cnt += (pc.expand && pc.safe) ? 1u : 0u;
+            }
+        const uint32_t tot = block_sum_u32<256>(cnt, sh);
+        if (threadIdx.x == 0) tile_cnt_all[(size_t)b * ntiles_max + t] = tot;
+    }
+}
+
+// per slice: tile offsets, this pass's L (min(remaining, capacity)), end, record
+template <typename T>
+__global__ __launch_bounds__(256) void k_pee_lat_locate(const T* __restrict__ img, int H, int W, int lat, int T0,
+                                                        int maxval, const int32_t* __restrict__ lengths,
+                                                        codec_pee_meta* __restrict__ metas, int pass, int B,
+                                                        const uint32_t* __restrict__ tile_cnt_all,
+                                                        uint32_t* __restrict__ tile_off_all, int ntiles_max) {
+    __shared__ uint32_t sh[8];
+    __shared__ int s_tile, s_end;
+    __shared__ uint32_t s_base;
+    const int b = blockIdx.x;
+    const PeeLat g = pee_lattice(lat, H, W);
+    const int nc = g.hc * g.wc, ntiles = (nc + PEE_TILE - 1) / PEE_TILE;
+    const int rem = max(0, lengths[b] - pee_pass_base(metas, pass, B, b));
+    codec_pee_meta* M = metas + (size_t)pass * B + b;
+    if (rem == 0) {   // nothing left for this slice: the pass leaves it untouched
+        if (threadIdx.x == 0) {
+            M->T = T0; M->maxval = maxval; M->L = 0; M->end = -1; M->nc = nc; M->ntiles = ntiles; M->tile_end = -1;
+            M->status = 0; M->capacity = -1; M->lm_count = 0; M->h = H; M->w = W; M->flags = 0;
+            M->reserved[0] = lat; M->reserved[1] = 0; M->reserved[2] = 0;
+        }
+        return;
+    }
+    const uint32_t L = (uint32_t)rem;
+    const uint32_t* cnt = tile_cnt_all + (size_t)b * ntiles_max;
+    uint32_t* off = tile_off_all + (size_t)b * ntiles_max;
+    if (threadIdx.x == 0) { s_tile = -1; s_end = -1; s_base = 0; }
+    __syncthreads();
+    uint32_t running = 0;
+    for (int base = 0; base < ntiles; base += 256) {
+        const int t = base + threadIdx.x;
+        const uint32_t c = t < ntiles ? cnt[t] : 0u;
+        uint32_t tot;
+        const uint32_t ex = running + block_excl_scan<256>(c, sh, &tot);
+        if (t < ntiles) off[t] = ex;
+        if (t < ntiles && ex < L && ex + c >= L) { s_tile = t; s_base = ex; }
+        running += tot;
+    }
+    __syncthreads();
+    const int tile = s_tile;
+    if (tile >= 0 && running >= L) {   // the L-th expandable candidate of `tile`
+        const T* src = img + (size_t)b * H * W;
+        const int k0 = tile * PEE_TILE + 4 * threadIdx.x;
+        LatQuad<T> q;
+        q.load(src, W, g, k0, nc - 1);
+        uint32_t flags = 0, local = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (k0 + u < nc) {
+                const PeeCand pc = pee_classify(q.x[u], q.a[u], q.b[u], q.c[u], T0, maxval);
+                if (pc.expand && pc.safe) { flags |= 1u << u; ++local; }
+            }
+        uint32_t tot;
+        const uint32_t pre = block_excl_scan<256>(local, sh, &tot);
+        const uint32_t need = L - s_base;
+        if (need > pre && need <= pre + local) {
+            uint32_t r = pre;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if ((flags >> u) & 1u) {
+                    ++r;
+                    if (r == need) s_end = k0 + u;
+                }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        M->T = T0; M->maxval = maxval; M->nc = nc; M->ntiles = ntiles; M->capacity = (int)running;
+        M->h = H; M->w = W; M->lm_count = 0; M->flags = 0;
+        M->reserved[0] = lat; M->reserved[1] = 0; M->reserved[2] = 0;
+        if (running < L) {   // the pass fills up: its capacity's bits, every candidate processed
+            M->L = (int)running; M->end = nc - 1; M->tile_end = ntiles - 1; M->status = 1;
+        } else {
+            M->L = (int)L; M->end = s_end; M->tile_end = tile; M->status = 0;
+        }
+    }
+}
+
+// tiles <= tile_end, in place: expansion / shifting of the candidates, this pass's location map
+template <typename T>
+__global__ __launch_bounds__(256) void k_pee_lat_embed(T* __restrict__ img, int H, int W, int lat,
+                                                       const u64* __restrict__ payload_all, int pw,
+                                                       const uint32_t* __restrict__ tile_off_all, int ntiles_max,
+                                                       codec_pee_meta* __restrict__ metas, int pass, int B,
+                                                       u64* __restrict__ lm_all, int lmw) {
+    __shared__ uint32_t sh[8];
+    __shared__ uint32_t lm32[PEE_TILE / 32];
+    const int b = blockIdx.y;
+    codec_pee_meta* M = metas + (size_t)pass * B + b;
+    const int tile_end = M->tile_end, end = M->end, Tthr = M->T, maxval = M->maxval;
+    if (tile_end < 0) return;
+    const uint32_t pbase = (uint32_t)pee_pass_base(metas, pass, B, b);
+    const PeeLat g = pee_lattice(lat, H, W);
+    T* dst = img + (size_t)b * H * W;
+    const u64* payload = payload_all + (size_t)b * pw;
+    u64* lm = lm_all + (size_t)b * lmw;
+    const uint32_t* off = tile_off_all + (size_t)b * ntiles_max;
+    for (int t = blockIdx.x; t <= tile_end; t += gridDim.x) {
+        if (threadIdx.x < PEE_TILE / 32) lm32[threadIdx.x] = 0;
+        const int k0 = t * PEE_TILE + 4 * threadIdx.x;
+        LatQuad<T> q;
+        q.load(dst, W, g, k0, end);
+        PeeCand pc[4];
+        uint32_t local = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            pc[u].expand = pc[u].safe = pc[u].right = false;
+            pc[u].x = pc[u].p = 0;
+            if (k0 + u <= end) {
+                pc[u] = pee_classify(q.x[u], q.a[u], q.b[u], q.c[u], Tthr, maxval);
+                local += (pc[u].expand && pc[u].safe) ? 1u : 0u;
+            }
+        }
+        uint32_t tot;
+        uint32_t cur = pbase + off[t] + block_excl_scan<256>(local, sh, &tot);   // also orders lm32 zeroing
+        uint32_t nib = 0, unsafe = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (k0 + u > end) continue;
+            if (!pc[u].safe) { nib |= 1u << u; ++unsafe; continue; }
+            int nv;
+            if (pc[u].expand) {
+                const int bit = (int)(cur >> 6) < pw ? (int)((payload[cur >> 6] >> (cur & 63)) & 1ull) : 0;
+                ++cur;
+                nv = pc[u].p + 2 * (pc[u].x - pc[u].p) + bit;
+            } else {
+                nv = pc[u].right ? pc[u].x + Tthr : pc[u].x - Tthr;
+            }
+            dst[q.o[u]] = (T)nv;
+        }
+        if (nib) atomicOr(&lm32[(4 * threadIdx.x) >> 5], nib << ((4 * threadIdx.x) & 31));
+        const uint32_t nun = block_sum_u32<256>(unsafe, sh);
+        if (threadIdx.x < PEE_TILE / 64) {
+            const int w = t * (PEE_TILE / 64) + threadIdx.x;
+            if (w < lmw) lm[w] = (u64)lm32[2 * threadIdx.x] | ((u64)lm32[2 * threadIdx.x + 1] << 32);
+        }
+        if (threadIdx.x == 0 && nun) atomicAdd(&M->lm_count, (int)nun);
+        __syncthreads();
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_pee_lat_dcount(const T* __restrict__ img, int H, int W, int lat,
+                                                        const codec_pee_meta* __restrict__ metas, int pass, int B,
+                                                        const u64* __restrict__ lm_all, int lmw,
+                                                        uint32_t* __restrict__ tile_cnt_all, int ntiles_max) {
+    __shared__ uint32_t sh[8];
+    const int b = blockIdx.y;
+    const codec_pee_meta* M = metas + (size_t)pass * B + b;
+    const int tile_end = M->tile_end, end = M->end, Tthr = M->T;
+    const PeeLat g = pee_lattice(lat, H, W);
+    const T* src = img + (size_t)b * H * W;
+    const u64* lm = lm_all + (size_t)b * lmw;
+    for (int t = blockIdx.x; t <= tile_end; t += gridDim.x) {
+        const int k0 = t * PEE_TILE + 4 * threadIdx.x;
+        LatQuad<T> q;
+        q.load(src, W, g, k0, end);
+        uint32_t local = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = k0 + u;
+            if (k <= end && !lm_bit(lm, k, lmw)) {
+                const int e2 = q.x[u] - med3(q.a[u], q.b[u], q.c[u]);
+                local += (e2 >= -2 * Tthr && e2 < 2 * Tthr) ? 1u : 0u;
+            }
+        }
+        const uint32_t tot = block_sum_u32<256>(local, sh);
+        if (threadIdx.x == 0) tile_cnt_all[(size_t)b * ntiles_max + t] = tot;
+    }
+}
+
+// tiles <= tile_end, in place: the pass's bits (payload words OR-ed, zeroed by the caller)
+// and the restored candidates
+template <typename T>
+__global__ __launch_bounds__(256) void k_pee_lat_recover(T* __restrict__ img, int H, int W, int lat,
+                                                         const codec_pee_meta* __restrict__ metas, int pass, int B,
+                                                         const u64* __restrict__ lm_all, int lmw,
+                                                         const uint32_t* __restrict__ tile_off_all, int ntiles_max,
+                                                         u64* __restrict__ payload_all, int pw) {
+    __shared__ uint32_t sh[8];
+    const int b = blockIdx.y;
+    const codec_pee_meta* M = metas + (size_t)pass * B + b;
+    const int tile_end = M->tile_end, end = M->end, Tthr = M->T;
+    if (tile_end < 0) return;
+    const uint32_t pbase = (uint32_t)pee_pass_base(metas, pass, B, b);
+    const uint32_t plim = pbase + (uint32_t)max(0, M->L);
+    const PeeLat g = pee_lattice(lat, H, W);
+    T* dst = img + (size_t)b * H * W;
+    const u64* lm = lm_all + (size_t)b * lmw;
+    u64* payload = payload_all + (size_t)b * pw;
+    const uint32_t* off = tile_off_all + (size_t)b * ntiles_max;
+    for (int t = blockIdx.x; t <= tile_end; t += gridDim.x) {
+        const int k0 = t * PEE_TILE + 4 * threadIdx.x;
+        LatQuad<T> q;
+        q.load(dst, W, g, k0, end);
+        int ps[4];
+        bool act[4], inner[4];
+        uint32_t local = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = k0 + u;
+            act[u] = k <= end && !lm_bit(lm, k, lmw);
+            inner[u] = false;
+            ps[u] = 0;
+            if (act[u]) {
+                ps[u] = med3(q.a[u], q.b[u], q.c[u]);
+                const int e2 = q.x[u] - ps[u];
+                inner[u] = e2 >= -2 * Tthr && e2 < 2 * Tthr;
+                local += inner[u] ? 1u : 0u;
+            }
+        }
+        uint32_t tot;
+        uint32_t cur = pbase + off[t] + block_excl_scan<256>(local, sh, &tot);
+        u64 word = 0;
+        int wi = -1;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (!act[u]) continue;
+            const int e2 = q.x[u] - ps[u];
+            int x;
+            if (inner[u]) {
+                if ((e2 & 1) && cur < plim && (int)(cur >> 6) < pw) {   // consecutive bits: one atomic per word
+                    if (wi != (int)(cur >> 6)) {
+                        if (wi >= 0 && word) atomicOr(&payload[wi], word);
+                        wi = (int)(cur >> 6);
+                        word = 0;
+                    }
+                    word |= 1ull << (cur & 63);
+                }
+                ++cur;
+                x = ps[u] + (e2 >> 1);
+            } else {
+                x = e2 >= 2 * Tthr ? q.x[u] - Tthr : q.x[u] + Tthr;
+            }
+            dst[q.o[u]] = (T)x;
+        }
+        if (wi >= 0 && word) atomicOr(&payload[wi], word);
+    }
+}
+
+static int pee_multi_check(const codec_pee_params* P, int pass) {
+    int rc = pee_check(P);
+    if (rc) return rc;
+    if (pass < 0 || pass > 3) return set_err(CODEC_EINVAL, "pass must be in 0..3");
+    if ((long long)P->B * P->H * P->W * P->bytes > (1LL << 40)) return set_err(CODEC_EINVAL, "batch too large");
+    return 0;
+}
+
+extern "C" {
+
+int codec_pee_multi_embed_pass(const codec_pee_params* P, int32_t pass, const void* cover, void* stego,
+                               const uint64_t* payload, const int32_t* lengths, codec_pee_meta* metas, uint64_t* lm,
+                               void* workspace, size_t workspace_bytes, void* stream) {
+    int rc = pee_multi_check(P, pass);
+    if (rc) return rc;
+    if (!cover || !stego || !payload || !lengths || !metas || !lm || !workspace)
+        return set_err(CODEC_EINVAL, "codec_pee_multi_embed_pass: NULL pointer argument");
+    const PeeWs L = pee_ws(P);
+    if (workspace_bytes < L.total) return set_err(CODEC_EINVAL, "workspace too small");
+    hipStream_t st = as_stream(stream);
+    HIP_TRY(pee_ws_enter(workspace, P, L, st));
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.cnt);
+    uint32_t* off = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.off);
+    if (cover != stego)   // the pass runs in place on the stego
+        HIP_TRY(hipMemcpyAsync(stego, cover, (size_t)P->B * P->H * P->W * P->bytes, hipMemcpyDeviceToDevice, st));
+    const PeeLat g = pee_lattice(pass, P->H, P->W);
+    const int nc = g.hc * g.wc, ntiles = (nc + PEE_TILE - 1) / PEE_TILE;
+    const int gx = std::max(1, std::min(ntiles, (int)knob("CODEC_PEE_LAT_WGS", 256)));
+    dim3 grid(gx, P->B);
+    {
+        ProfScope prof(st, CODEC_K_PEE_LAT_COUNT);
+#define PLC(TT) hipLaunchKernelGGL(k_pee_lat_count<TT>, grid, dim3(256), 0, st, static_cast<const TT*>(stego), P->H, P->W, \
+                                   (int)pass, P->T, P->maxval, lengths, metas, (int)pass, P->B, cnt, L.ntiles_max)
+        if (P->bytes == 2) PLC(uint16_t); else PLC(uint8_t);
+#undef PLC
+        LAUNCH_CHECK("k_pee_lat_count");
+#define PLL(TT) hipLaunchKernelGGL(k_pee_lat_locate<TT>, dim3(P->B), dim3(256), 0, st, static_cast<const TT*>(stego), P->H, \
+                                   P->W, (int)pass, P->T, P->maxval, lengths, metas, (int)pass, P->B, cnt, off, L.ntiles_max)
+        if (P->bytes == 2) PLL(uint16_t); else PLL(uint8_t);
+#undef PLL
+        LAUNCH_CHECK("k_pee_lat_locate");
+    }
+    ProfScope prof(st, CODEC_K_PEE_LAT_EMBED);
+#define PLE(TT) hipLaunchKernelGGL(k_pee_lat_embed<TT>, grid, dim3(256), 0, st, static_cast<TT*>(stego), P->H, P->W, \
+                                   (int)pass, reinterpret_cast<const u64*>(payload), P->payload_words, off, L.ntiles_max, \
+                                   metas, (int)pass, P->B, reinterpret_cast<u64*>(lm), P->lm_words)
+    if (P->bytes == 2) PLE(uint16_t); else PLE(uint8_t);
+#undef PLE
+    LAUNCH_CHECK("k_pee_lat_embed");
+    return 0;
+}
+
+int codec_pee_multi_extract_pass(const codec_pee_params* P, int32_t pass, const void* stego,
+                                 const codec_pee_meta* metas, const uint64_t* lm, void* cover_out,
+                                 uint64_t* payload_out, void* workspace, size_t workspace_bytes, void* stream) {
+    int rc = pee_multi_check(P, pass);
+    if (rc) return rc;
+    if (!stego || !metas || !lm || !cover_out || !payload_out || !workspace)
+        return set_err(CODEC_EINVAL, "codec_pee_multi_extract_pass: NULL pointer argument");
+    const PeeWs L = pee_ws(P);
+    if (workspace_bytes < L.total) return set_err(CODEC_EINVAL, "workspace too small");
+    hipStream_t st = as_stream(stream);
+    HIP_TRY(pee_ws_enter(workspace, P, L, st));
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.cnt);
+    uint32_t* off = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.off);
+    if (cover_out != stego)   // the pass runs in place on cover_out
+        HIP_TRY(hipMemcpyAsync(cover_out, stego, (size_t)P->B * P->H * P->W * P->bytes, hipMemcpyDeviceToDevice, st));
+    const PeeLat g = pee_lattice(pass, P->H, P->W);
+    const int nc = g.hc * g.wc, ntiles = (nc + PEE_TILE - 1) / PEE_TILE;
+    const int gx = std::max(1, std::min(ntiles, (int)knob("CODEC_PEE_LAT_WGS", 256)));
+    dim3 grid(gx, P->B);
+    {
+        ProfScope prof(st, CODEC_K_PEE_LAT_DCOUNT);
+#define PLD(TT) hipLaunchKernelGGL(k_pee_lat_dcount<TT>, grid, dim3(256), 0, st, static_cast<const TT*>(cover_out), P->H, \
+                                   P->W, (int)pass, metas, (int)pass, P->B, reinterpret_cast<const u64*>(lm), P->lm_words, \
+                                   cnt, L.ntiles_max)
+        if (P->bytes == 2) PLD(uint16_t); else PLD(uint8_t);
+#undef PLD
+        LAUNCH_CHECK("k_pee_lat_dcount");
+        hipLaunchKernelGGL(k_pee_offsets, dim3(P->B), dim3(256), 0, st, metas + (size_t)pass * P->B, cnt, off, L.ntiles_max);
+        LAUNCH_CHECK("k_pee_offsets");
+    }
+    ProfScope prof(st, CODEC_K_PEE_LAT_RECOVER);
+#define PLR(TT) hipLaunchKernelGGL(k_pee_lat_recover<TT>, grid, dim3(256), 0, st, static_cast<TT*>(cover_out), P->H, P->W, \
+                                   (int)pass, metas, (int)pass, P->B, reinterpret_cast<const u64*>(lm), P->lm_words, off, \
+                                   L.ntiles_max, reinterpret_cast<u64*>(payload_out), P->payload_words)
+    if (P->bytes == 2) PLR(uint16_t); else PLR(uint8_t);
+#undef PLR
+    LAUNCH_CHECK("k_pee_lat_recover");
+    return 0;
+}
+
+}  // extern "C"

@@ -4,7 +4,11 @@ oracle/pee_cpu.py (parity unpinned) and summarised in include/codec_tcc.h.
 
     codec = PeeCodec(B, H, W, dtype="uint16", T=2)
     enc = codec.embed(covers, payloads)          # stego, location map, per-slice meta
-    bits, cover = codec.extract(enc.stego, enc.meta, enc.lm, lengths=enc.lengths)
+    bits, cover = codec.decode(enc)
+
+Scheme 2 (PeeCodec(..., scheme=2), oracle/pee_cpu.py "Scheme 2"): four sublattice passes on
+the running image, about four times the capacity at one T; enc.meta / enc.lm then hold one
+record / map per pass ([4, B, ...], pass-major).
 """
 from __future__ import annotations
 
@@ -27,19 +31,40 @@ class PeeEncoded:
     lengths: List[int]
     payload_words: int
     config: dict = field(default_factory=dict)   # the PeeCodec's T / tmax / maxval (decode())
+    scheme: int = 1                              # 2: four sublattice passes (meta / lm per pass)
 
     def records(self) -> List[_lib.PeeMeta]:
+        """Scheme 1: one record per slice.  Scheme 2: 4 * B records, pass-major."""
         raw = self.meta.detach().cpu().contiguous().numpy().tobytes()
         n = len(raw) // _lib.PEE_META_BYTES
         return [_lib.PeeMeta.from_buffer_copy(raw, i * _lib.PEE_META_BYTES) for i in range(n)]
 
+    def pass_records(self) -> List[List[_lib.PeeMeta]]:
+        """Scheme 2: records[p][b] of pass p (scheme 1: one pass)."""
+        recs = self.records()
+        n = len(self.lengths)
+        return [recs[i:i + n] for i in range(0, len(recs), n)]
+
+    def embedded(self) -> List[int]:
+        """Payload bits embedded per slice (scheme 2: the passes' sum)."""
+        if self.scheme == 1:
+            return [int(min(r.L, r.capacity)) if r.status == 1 else int(r.L) for r in self.records()]
+        return [sum(int(pr[b].L) for pr in self.pass_records()) for b in range(len(self.lengths))]
+
 
 class PeeCodec:
     def __init__(self, batch: int, height: int, width: int, dtype="uint16", *, T=2, tmax: int = 16,
-                 maxval: Optional[int] = None, device=None):
+                 maxval: Optional[int] = None, device=None, scheme: int = 1):
         """T: the expansion threshold for every slice, or "auto" -- capacity control: each
         slice gets the smallest T <= tmax whose capacity holds its payload
-        (codec_pee_capacity, one extra read-only pass; meta.T records the choice)."""
+        (codec_pee_capacity, one extra read-only pass; meta.T records the choice).
+        scheme: 1 = the (odd, odd) lattice in one pass; 2 = four sublattice passes
+        (codec_pee_multi_embed_pass; integer T only)."""
+        if scheme not in (1, 2):
+            raise ValueError("scheme must be 1 or 2")
+        if scheme == 2 and isinstance(T, str):
+            raise ValueError("scheme 2 takes an integer T (capacity control is scheme 1's)")
+        self.scheme = int(scheme)
         _require_gpu()
         torch = _torch()
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -59,7 +84,7 @@ class PeeCodec:
         self.nc = (self.H // 2) * (self.W // 2)
         self.lm_words = max(1, (self.nc + 63) // 64)
         self.config = dict(method="pee", T="auto" if self.auto else self.T, tmax=self.tmax, maxval=self.maxval,
-                           dtype="uint16" if nbytes == 2 else "uint8")
+                           dtype="uint16" if nbytes == 2 else "uint8", scheme=self.scheme)
         P = self._params(1)
         ws = _lib.load().codec_pee_workspace_bytes(C.byref(P))
         if ws == 0:
@@ -127,6 +152,8 @@ class PeeCodec:
         words, lengths, lens_t = packed if packed is not None else self.pack_payloads(payloads)
         if stego is None:
             stego = torch.empty_like(covers)
+        if self.scheme == 2:
+            return self._embed_multi(covers, words, lengths, lens_t, stego, lm, meta, check)
         if lm is None:
             lm = torch.empty((self.B, self.lm_words), dtype=torch.int64, device=self.device)
         if meta is None:
@@ -156,16 +183,58 @@ class PeeCodec:
             _raise_lookback(recs)
         return enc
 
+    def _embed_multi(self, covers, words, lengths, lens_t, stego, lm, meta, check):
+        """Scheme 2: passes 0..3 (pass 0 copies cover -> stego, the others run in place)."""
+        torch = _torch()
+        if lm is None:
+            lm = torch.empty((4, self.B, self.lm_words), dtype=torch.int64, device=self.device)
+        if meta is None:
+            meta = torch.empty((4, self.B, _lib.PEE_META_BYTES), dtype=torch.uint8, device=self.device)
+        if tuple(lm.shape) != (4, self.B, self.lm_words) or tuple(meta.shape) != (4, self.B, _lib.PEE_META_BYTES):
+            raise ValueError("scheme 2 takes lm [4, B, lm_words] and meta [4, B, PEE_META_BYTES]")
+        P = self._params(words.shape[1])
+        lib = _lib.load()
+
+        def launch():
+            for p in range(4):
+                src = covers if p == 0 else stego
+                _lib.check(lib.codec_pee_multi_embed_pass(C.byref(P), p, src.data_ptr(), stego.data_ptr(),
+                                                          words.data_ptr(), lens_t.data_ptr(), meta.data_ptr(),
+                                                          lm[p].data_ptr(), self.workspace.data_ptr(),
+                                                          self.workspace.numel(), _stream()),
+                           "codec_pee_multi_embed_pass")
+        self._guarded(launch)
+        return PeeEncoded(stego=stego, lm=lm, meta=meta, lengths=list(lengths), payload_words=int(words.shape[1]),
+                          config=self.config, scheme=2)
+
     def extract(self, stego, meta, lm, *, payload_words: int, cover=None, payload=None):
         torch = _torch()
         if cover is None:
             cover = torch.empty_like(stego)
         if payload is None:
             payload = torch.empty((self.B, int(payload_words)), dtype=torch.int64, device=self.device)
+        if self.scheme == 2:
+            return self._extract_multi(stego, meta, lm, payload_words, cover, payload)
         P = self._params(payload_words)
         self._guarded(lambda: _lib.check(_lib.load().codec_pee_extract(
             C.byref(P), stego.data_ptr(), meta.data_ptr(), lm.data_ptr(), cover.data_ptr(), payload.data_ptr(),
             self.workspace.data_ptr(), self.workspace.numel(), _stream()), "codec_pee_extract"))
+        return payload, cover
+
+    def _extract_multi(self, stego, meta, lm, payload_words, cover, payload):
+        """Scheme 2: passes 3..0 (pass 3 copies stego -> cover, the others run in place)."""
+        P = self._params(payload_words)
+        lib = _lib.load()
+
+        def launch():
+            payload.zero_()
+            for p in (3, 2, 1, 0):
+                src = stego if p == 3 else cover
+                _lib.check(lib.codec_pee_multi_extract_pass(C.byref(P), p, src.data_ptr(), meta.data_ptr(),
+                                                            lm[p].data_ptr(), cover.data_ptr(), payload.data_ptr(),
+                                                            self.workspace.data_ptr(), self.workspace.numel(),
+                                                            _stream()), "codec_pee_multi_extract_pass")
+        self._guarded(launch)
         return payload, cover
 
     def lookback_failed(self, payload_words: int = 1) -> bool:
@@ -187,6 +256,16 @@ class PeeCodec:
 
     def decode(self, enc: PeeEncoded):
         """(list of 0/1 bit vectors, restored cover tensor); raises if a slice overflowed."""
+        if enc.scheme != self.scheme:
+            raise ValueError(f"a scheme-{enc.scheme} embedding given to a scheme-{self.scheme} codec")
+        if self.scheme == 2:
+            got = enc.embedded()
+            short = [i for i, (g, n) in enumerate(zip(got, enc.lengths)) if g < n]
+            if short:
+                raise ValueError(f"payload exceeds PEE capacity in slices {short} (scheme 2, T={self.T})")
+            words, cover = self.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words)
+            host = words.cpu().numpy()
+            return [framing.unpack_bits(host[i], enc.lengths[i]) for i in range(self.B)], cover
         recs = enc.records()
         _raise_lookback(recs)
         _raise_status(recs, f"T={'auto, tmax=%d' % self.tmax if self.auto else self.T}")
@@ -211,14 +290,14 @@ def clear_codec_cache():
     _CODECS.clear()
 
 
-def _codec_for(shape, dtype: str, *, T, tmax: int, maxval: Optional[int]) -> PeeCodec:
+def _codec_for(shape, dtype: str, *, T, tmax: int, maxval: Optional[int], scheme: int = 1) -> PeeCodec:
     torch = _torch()
     if maxval is None:
         maxval = 65535 if "16" in dtype else 255
-    key = (tuple(shape), dtype, T, int(tmax), int(maxval), torch.cuda.current_device())
+    key = (tuple(shape), dtype, T, int(tmax), int(maxval), int(scheme), torch.cuda.current_device())
     c = _CODECS.get(key)
     if c is None:
-        c = PeeCodec(*shape, dtype=dtype, T=T, tmax=tmax, maxval=maxval)
+        c = PeeCodec(*shape, dtype=dtype, T=T, tmax=tmax, maxval=maxval, scheme=scheme)
         _CODECS[key] = c
         while len(_CODECS) > _CODECS_MAX:
             _CODECS.popitem(last=False)
@@ -260,11 +339,13 @@ def _config_from_records(enc: "PeeEncoded") -> dict:
     return dict(method="pee", T=T, tmax=min(tmax, 64), maxval=maxvals.pop(), dtype=dt)
 
 
-def encode(covers, payloads: Sequence, *, T=2, tmax: int = 16, maxval: Optional[int] = None) -> PeeEncoded:
+def encode(covers, payloads: Sequence, *, T=2, tmax: int = 16, maxval: Optional[int] = None,
+           scheme: int = 1) -> PeeEncoded:
     """MED-PEE embed of one payload per slice (the package's `encode(..., method="pee")`).
     covers: [B,H,W] / [H,W] uint8/uint16 torch tensor or numpy array; T: expansion threshold
     or "auto" (smallest T <= tmax whose capacity holds each slice's payload); maxval: the
-    largest legal pixel value (e.g. 4095 for 12-bit DICOM; default the dtype's maximum).
+    largest legal pixel value (e.g. 4095 for 12-bit DICOM; default the dtype's maximum);
+    scheme 2: four sublattice passes (integer T).
     Raises ValueError when a payload exceeds its slice's capacity."""
     from .codec import _as_batch
     _require_gpu()
@@ -272,9 +353,14 @@ def encode(covers, payloads: Sequence, *, T=2, tmax: int = 16, maxval: Optional[
     if isinstance(payloads, (str, bytes, bytearray)):
         payloads = [payloads]
     dt = "uint16" if _elem_bytes(covers) == 2 else "uint8"
-    codec = _codec_for(tuple(covers.shape), dt, T=T, tmax=tmax, maxval=maxval)
+    codec = _codec_for(tuple(covers.shape), dt, T=T, tmax=tmax, maxval=maxval, scheme=scheme)
     enc = codec.embed(covers, payloads)
-    _raise_status(enc.records(), f"T={T}, tmax={tmax}")
+    if scheme == 2:
+        short = [i for i, (g, n) in enumerate(zip(enc.embedded(), enc.lengths)) if g < n]
+        if short:
+            raise ValueError(f"payload exceeds PEE capacity in slices {short} (scheme 2, T={T})")
+    else:
+        _raise_status(enc.records(), f"T={T}, tmax={tmax}")
     return enc
 
 
@@ -285,7 +371,7 @@ def decode(enc: PeeEncoded, *, restore: bool = True):
     _require_gpu()
     cfg = enc.config or _config_from_records(enc)
     codec = _codec_for(tuple(enc.stego.shape), cfg.get("dtype", "uint16"), T=cfg.get("T", 2),
-                       tmax=cfg.get("tmax", 16), maxval=cfg.get("maxval"))
+                       tmax=cfg.get("tmax", 16), maxval=cfg.get("maxval"), scheme=int(getattr(enc, "scheme", 1)))
     bits, cover = codec.decode(enc)
     return bits, (cover if restore else None)
 
@@ -297,8 +383,12 @@ def _raise_lookback(recs):
                            "their pixels are not a valid stego")
 
 
-def lm_bits(enc: PeeEncoded, b: int) -> np.ndarray:
-    """Location map of slice b as a bool vector over candidates 0..end."""
-    r = enc.records()[b]
-    raw = enc.lm[b].cpu().numpy().view(np.uint8)
+def lm_bits(enc: PeeEncoded, b: int, p: int = 0) -> np.ndarray:
+    """Location map of slice b (scheme 2: of pass p) as a bool vector over candidates 0..end."""
+    if enc.scheme == 2:
+        r = enc.pass_records()[p][b]
+        raw = enc.lm[p, b].cpu().numpy().view(np.uint8)
+    else:
+        r = enc.records()[b]
+        raw = enc.lm[b].cpu().numpy().view(np.uint8)
     return np.unpackbits(raw, bitorder="little")[: r.end + 1].astype(bool)

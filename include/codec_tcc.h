@@ -338,6 +338,31 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
                       const uint64_t* lm, void* cover_out, uint64_t* payload_out, void* workspace,
                       size_t workspace_bytes, void* stream);
 
+/* ---- MED-PEE scheme 2: four sublattice passes (oracle/pee_cpu.py "Scheme 2"; the version-16
+ * container's scheme byte 1).  Pass p (0..3) runs the scheme above on lattice p -- (odd, odd),
+ * (even, even), (odd, even), (even, odd) as (row, column) parities, pixels with y >= 1 and
+ * x >= 1, candidate (i, j) at (y0 + 2i, x0 + 2j) with y0 / x0 = 1 for an odd parity, 2 for an
+ * even one -- on the RUNNING image, taking the next min(remaining, capacity_p) payload bits
+ * of each slice: about four times scheme 1's capacity at one T.  Decoding runs the passes in
+ * reverse.  metas: [4][B] codec_pee_meta (pass-major), written by the embed passes in
+ * order and read by later passes (pass p's payload bits start at meta[0][b].L + ... +
+ * meta[p-1][b].L); a pass with no bits left for a slice leaves it untouched (L 0, end -1,
+ * capacity -1).  meta.L is the number of bits the pass embedded; meta.status 1 = the pass
+ * filled up (every candidate processed); meta.reserved[0] = the lattice.  lm: this pass's
+ * [B][lm_words] location map.  The PEE workspace (codec_pee_workspace_bytes) is shared with
+ * scheme 1.  Passes are ordered calls on one stream. */
+/* embed pass `pass`: stego = cover (copied when they differ), then the pass in place on
+ * stego.  Pass 0 with cover != stego, passes 1..3 with cover == stego. */
+int codec_pee_multi_embed_pass(const codec_pee_params* P, int32_t pass, const void* cover, void* stego,
+                               const uint64_t* payload, const int32_t* lengths, codec_pee_meta* metas,
+                               uint64_t* lm, void* workspace, size_t workspace_bytes, void* stream);
+/* extract pass `pass` (call 3, 2, 1, 0): cover_out = stego (copied when they differ), then
+ * the pass restores its lattice in place and ORs its bits into payload_out (zero it before
+ * the first pass). */
+int codec_pee_multi_extract_pass(const codec_pee_params* P, int32_t pass, const void* stego,
+                                 const codec_pee_meta* metas, const uint64_t* lm, void* cover_out,
+                                 uint64_t* payload_out, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- exchange records of the MED-PEE side information (north star: "an RCCL all-gather of
  * per-slice location maps"; no reference counterpart -- the reference is
  * single-process).  Record b = CODEC_PEE_RECORD_HDR_WORDS uint64 words holding slice b's
@@ -400,6 +425,10 @@ int codec_quality_moments(int32_t B, int32_t H, int32_t W, int32_t bytes, const 
 #define CODEC_K_PEE_EMBED_SS_AUTO 26
 #define CODEC_K_PEE_EMBED_RES 27   /* resident auto embed: slice read once, kept on the CU */
 #define CODEC_K_SCAN_DECIDE 28     /* fused scan + decide + embed (one workgroup per slice)  */
+#define CODEC_K_PEE_LAT_COUNT 29   /* scheme 2: one pass's tile counts + per-slice locate      */
+#define CODEC_K_PEE_LAT_EMBED 30   /* scheme 2: one pass's in-place embed                      */
+#define CODEC_K_PEE_LAT_DCOUNT 31  /* scheme 2: one pass's decodable-bit counts + offsets      */
+#define CODEC_K_PEE_LAT_RECOVER 32 /* scheme 2: one pass's in-place recovery                   */
 int codec_profile_begin(int32_t capacity);
 /* after the stream has been synchronised: fills ms[i], tag[i] for the recorded pairs and
  * returns their count (closes the window and frees the events). */

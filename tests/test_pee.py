@@ -1136,3 +1136,105 @@ def test_gpu_capacity_pass_forced_reorder(per_wg, delay, monkeypatch):
     for i in range(bsz):
         T = P.select_T(covers[i], lens[i], tmax)
         assert enc.records()[i].T == T and t_dev[i] == T, (i, T)
+
+
+# ---- scheme 2 on the GPU: four sublattice passes (codec_pee_multi_embed_pass / _extract_pass)
+def _check_multi_vs_oracle(enc, covers, bits_list, T, mv, stego=None):
+    """Every slice of a scheme-2 embedding equals pee_embed_multi: stego, per pass L / end /
+    status / capacity (passes that embedded) and location map up to end."""
+    from codec_tcc_amd.pee import lm_bits
+    st = (enc.stego if stego is None else stego).cpu().numpy()
+    prs = enc.pass_records()
+    for b, (cov, bits) in enumerate(zip(covers, bits_list)):
+        exp, side = P.pee_embed_multi(cov, bits, T, maxval=mv)
+        np.testing.assert_array_equal(st[b], exp)
+        for p, ps in enumerate(side["passes"]):
+            r = prs[p][b]
+            assert (r.L, r.end, r.status, r.T, r.reserved[0]) == (ps["L"], ps["end"], ps["status"], T, p), (b, p)
+            if r.capacity >= 0:   # -1: nothing was left for the pass (it skipped the slice)
+                assert r.capacity == ps["capacity"], (b, p)
+            else:
+                assert ps["L"] == 0
+            np.testing.assert_array_equal(lm_bits(enc, b, p), ps["lm"])
+        assert enc.embedded()[b] == side["L"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", _multi_kats(), ids=_kat_id)
+def test_gpu_matches_multipass_kats(k):
+    """Scheme 2's HIP passes on each known-answer input: stego digest and every pass's record
+    and location map equal the committed answers; the reverse passes return payload and cover."""
+    import hashlib
+    torch = pytest.importorskip("torch")
+    from codec_tcc_amd import framing
+    from codec_tcc_amd.pee import PeeCodec
+    img, bits, mv = _multi_kat_inputs(k)
+    codec = PeeCodec(1, k["h"], k["w"], dtype=str(img.dtype), T=k["T"], maxval=mv, scheme=2)
+    enc = codec.embed(torch.from_numpy(img[None]).cuda(), [bits])
+    assert hashlib.sha256(enc.stego[0].cpu().numpy().tobytes()).hexdigest() == k["stego_sha256"]
+    for pr, kp in zip(enc.pass_records(), k["passes"]):
+        assert (pr[0].L, pr[0].end, pr[0].status) == (kp["L"], kp["end"], kp["status"])
+    assert enc.embedded() == [k["L"]]
+    _check_multi_vs_oracle(enc, img[None], [bits], k["T"], mv)
+    words, cover = codec.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words)
+    np.testing.assert_array_equal(framing.unpack_bits(words[0].cpu().numpy(), k["L"]), bits[: k["L"]])
+    np.testing.assert_array_equal(cover[0].cpu().numpy(), img)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,h,w,bsz,T", [("ct12", 64, 96, 5, 2), ("ct12", 67, 45, 3, 1), ("u8", 40, 33, 4, 2),
+                                             ("u16", 31, 64, 3, 3), ("ct12", 512, 512, 4, 2), ("u8", 3, 2, 2, 1)])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_gpu_multipass_batch_vs_oracle(kind, h, w, bsz, T, inplace):
+    """Batches of mixed payloads (empty, one pass, several passes, beyond every pass) on even
+    and odd shapes: every slice equals the oracle, in place or not, and decodes exactly."""
+    torch = pytest.importorskip("torch")
+    from codec_tcc_amd.pee import PeeCodec
+    covers = np.stack([synth.GENERATORS[kind](h, w, 300 + i) for i in range(bsz)])
+    mv = 4095 if kind == "ct12" else int(np.iinfo(covers.dtype).max)
+    rng = np.random.default_rng(7)
+    bits_list = []
+    for i in range(bsz):
+        cap0 = P.capacity(covers[i], T, mv)
+        n = [0, cap0 // 2, cap0 + 5, 3 * cap0 + 17, 5 * cap0 + 50][i % 5]
+        bits_list.append(rng.integers(0, 2, n).astype(np.uint8))
+    codec = PeeCodec(bsz, h, w, dtype=str(covers.dtype), T=T, maxval=mv, scheme=2)
+    cov_t = torch.from_numpy(covers).cuda()
+    work = cov_t.clone() if inplace else None
+    enc = codec.embed(work if inplace else cov_t, bits_list, stego=work)
+    _check_multi_vs_oracle(enc, covers, bits_list, T, mv)
+    from codec_tcc_amd import framing
+    out = enc.stego.clone() if inplace else None
+    words, cover = codec.extract(enc.stego if not inplace else out, enc.meta, enc.lm, payload_words=enc.payload_words,
+                                 cover=out)
+    host = words.cpu().numpy()
+    for i, bits in enumerate(bits_list):
+        n = enc.embedded()[i]
+        np.testing.assert_array_equal(framing.unpack_bits(host[i], n), bits[:n])
+    np.testing.assert_array_equal(cover.cpu().numpy(), covers)
+
+
+@pytest.mark.gpu
+def test_gpu_multipass_c3_1kb_at_t2():
+    """VERDICT r5 item 8's bar: C3's 1 KB payload per 512^2 slice fits at T <= 2 under scheme 2
+    (scheme 1 needs T = 4 there), decodes exactly through the package surface, and the stego's
+    PSNR beats scheme 1's at its T (codec_tcc_amd.quality)."""
+    torch = pytest.importorskip("torch")
+    import codec_tcc_amd as ct
+    from codec_tcc_amd import quality
+    from codec_tcc_amd.pee import encode, decode
+    B = 16
+    covers = torch.from_numpy(np.stack([synth.ct12(512, 512, 40 + i) for i in range(B)])).cuda()
+    msgs = [synth.payload(1024, 600 + i) for i in range(B)]
+    enc2 = encode(covers, msgs, T=2, maxval=4095, scheme=2)
+    bits, cover = decode(enc2)
+    assert torch.equal(cover, covers)
+    from codec_tcc_amd import framing
+    for i, m in enumerate(msgs):
+        np.testing.assert_array_equal(bits[i], framing.to_bits(m))
+    enc1 = encode(covers, msgs, T="auto", maxval=4095)
+    assert min(r.T for r in enc1.records()) >= 3
+    q2 = quality.quality(covers, enc2.stego, max_value=4095)
+    q1 = quality.quality(covers, enc1.stego, max_value=4095)
+    assert np.mean([r["psnr"] for r in q2]) > np.mean([r["psnr"] for r in q1])
+    assert isinstance(enc2, ct.PeeEncoded) and enc2.scheme == 2
