@@ -658,7 +658,63 @@ def bench_c3(args, torch, dist, world, dev, rank):
     lsb = bench_lsb(args, torch, dist, 1, rank, dev, covers, B, H, W, steps=4 * args.steps, seed0=5000)
     lsb.pop("_stego", None)
     res["lsb"] = lsb
+    if args.kind == "ct12":   # scheme 2 at T = 2 (a ct12 slice's 1 KB fits in two passes)
+        res["pee_scheme2"] = bench_pee2(args, torch, dev, covers, B, H, W, steps=4 * args.steps, T=2)
     return res
+
+
+def bench_pee2(args, torch, dev, covers, B, H, W, steps, T=2):
+    """MED-PEE scheme 2 (four sublattice passes on the running image, oracle/pee_cpu.py) on
+    the C3 batch: embed + extract per step at a fixed T (the passes that have bits left run;
+    the rest skip their slices), the exact round trip, the passes each slice used, and the
+    stego's PSNR (src/mse.py metric, peak 4095 for ct12) beside scheme 1's with capacity
+    control on the same payloads."""
+    from codec_tcc_amd import _lib, synth
+    from codec_tcc_amd import quality as Q
+    from codec_tcc_amd.pee import PeeCodec
+    codec = PeeCodec(B, H, W, dtype="uint16", T=T, maxval=4095, device=dev, scheme=2)
+    pay = [synth.payload(args.payload_chars, 99 + i) for i in range(B)]
+    packed = codec.pack_payloads(pay)
+    stego = torch.empty_like(covers)
+    cov2 = torch.empty_like(covers)
+    lm = torch.empty((4, B, codec.lm_words), dtype=torch.int64, device=dev)
+    meta = torch.empty((4, B, _lib.PEE_META_BYTES), dtype=torch.uint8, device=dev)
+    pw = packed[0].shape[1]
+    outw = torch.empty((B, pw), dtype=torch.int64, device=dev)
+    box = {}
+
+    def step():
+        box["enc"] = codec.embed(covers, None, stego=stego, lm=lm, meta=meta, packed=packed, check=False)
+        codec.extract(stego, meta, lm, payload_words=pw, cover=cov2, payload=outw)
+
+    for _ in range(args.warmup):
+        step()
+    el = _timed(torch, None, 1, dev, step, steps)
+    enc = box["enc"]
+    got = enc.embedded()
+    cover_ok = bool(torch.equal(cov2.view(torch.int16), covers.view(torch.int16)))
+    pay_ok = payload_equal(outw, packed[0], got)
+    full = all(g == n for g, n in zip(got, packed[1]))
+    prs = enc.pass_records()
+    used = [sum(1 for p in range(4) if prs[p][b].L > 0) for b in range(B)]
+    kern = _profile(_lib.load(), _lib, step, steps) if not args.no_profile else {}
+    q2 = Q.quality(covers, stego, max_value=4095)
+    c1 = PeeCodec(B, H, W, dtype="uint16", T="auto", maxval=4095, device=dev)
+    e1 = c1.embed(covers, None, packed=packed)
+    q1 = Q.quality(covers, e1.stego, max_value=4095)
+    return {"scheme": 2, "T": T, "value": round(B * H * W * steps / el / 1e6, 1), "unit": "Mpixels/s",
+            "ms_per_step": round(el / steps * 1e3, 4), "roundtrip_ok": cover_ok and pay_ok and full,
+            "cover_ok": cover_ok, "payload_ok": pay_ok, "all_bits_embedded": full,
+            "passes_used": {str(n): int(sum(1 for u in used if u == n)) for n in sorted(set(used))},
+            "psnr_db_mean": round(float(np.mean([r["psnr"] for r in q2])), 3),
+            "pixels_changed_mean": float(np.mean([r["pixels_diferentes"] for r in q2])),
+            "scheme1": {"T_chosen": {str(t): int(sum(1 for r in e1.records() if r.T == t))
+                                     for t in sorted({r.T for r in e1.records()})},
+                        "psnr_db_mean": round(float(np.mean([r["psnr"] for r in q1])), 3),
+                        "pixels_changed_mean": float(np.mean([r["pixels_diferentes"] for r in q1]))},
+            "kernels_ms": {k: round(v, 4) for k, v in kern.items()},
+            "path": "count/locate/embed per pass and dcount/offsets/recover per pass, in place on the "
+                    "running image; scalar loads (not the headline's vectorised single-pass kernels)"}
 
 
 def bench_c4(args, torch, dist, world, rank, dev):

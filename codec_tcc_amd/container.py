@@ -18,10 +18,19 @@ negative sizes) and stores the real offset:
 MED-PEE files (this build's scheme; the reference has no PEE format) use
 the same magic and framing with version 16:
 
-    header pee = >BBBB (version=16, codec_id, bytes per pixel, reserved)
+    header pee = >BBBB (version=16, codec_id, bytes per pixel, scheme byte 0)
                  + >II (width, height) + >iiiii (T, L = embedded bits, end, maxval, status)
                  + >I lm_blob_size
     body       = zlib(location-map bits of candidates 0..end, LSB-first) | compressed stego
+
+MED-PEE scheme 2 (four sublattice passes, oracle/pee_cpu.py) sets the scheme byte to 2:
+
+    header pee2 = >BBBB (version=16, codec_id, bytes per pixel, 2)
+                  + >II (width, height) + >iiii (T, maxval, L = embedded bits, status)
+                  + 4 x >iiiI (L_p, end_p, status_p, lm_blob_size_p)
+    body        = the 4 passes' zlib location maps in pass order | compressed stego
+
+so a reader of scheme-1 files (scheme byte 0) refuses scheme-2 files instead of misreading.
 
 Stego payload codecs: the reference's ids (png 1, j2k 2, jls 3, jxl 4) are kept; id 0
 ("raw", unknown to the reference) stores the stego pixels little-endian, uncompressed.
@@ -147,14 +156,60 @@ def lm_from_blob(blob: bytes, end: int) -> np.ndarray:
     return np.unpackbits(raw, bitorder="little")[: end + 1].astype(bool)
 
 
-def parse_pee_bytes(data: bytes) -> Tuple[Dict, bytes, bytes]:
-    """A version-16 STGC file -> (side information, lm_blob, stego bytes)."""
+_PEE2_FMT = ">BBBBIIiiii"
+_PEE2_PASS = ">iiiI"
+PEE_SCHEME2 = 2
+
+
+def create_pee2_header(codec: str, bytes_per_px: int, width: int, height: int, T: int, maxval: int, L: int,
+                       status: int, passes: Sequence[Tuple[int, int, int, int]]) -> bytes:
+    """Scheme-2 header; passes = 4 x (L_p, end_p, status_p, lm_blob_size_p)."""
+    if len(passes) != 4:
+        raise ValueError("scheme 2 has four passes")
+    hdr = struct.pack(_PEE2_FMT, PEE_VERSION, CODEC_IDS.get(codec.lower(), 0), int(bytes_per_px), PEE_SCHEME2,
+                      width, height, int(T), int(maxval), int(L), int(status))
+    return hdr + b"".join(struct.pack(_PEE2_PASS, int(a), int(b), int(c), int(d)) for a, b, c, d in passes)
+
+
+def pee_scheme(data: bytes) -> int:
+    """1 or 2: the MED-PEE scheme of a version-16 STGC file (its scheme byte)."""
     if data[:4] != MAGIC:
         raise ValueError("Arquivo inválido ou com assinatura incorreta.")   # codec.py:698
     (hlen,) = struct.unpack(">I", data[4:8])
     hdr = data[8:8 + hlen]
-    if not hdr or hdr[0] != PEE_VERSION:
+    if len(hdr) < 4 or hdr[0] != PEE_VERSION:
         raise ValueError("not a MED-PEE container (version 16)")
+    if hdr[3] not in (0, PEE_SCHEME2):
+        raise ValueError(f"unknown MED-PEE scheme byte {hdr[3]}")
+    return 2 if hdr[3] == PEE_SCHEME2 else 1
+
+
+def parse_pee2_bytes(data: bytes) -> Tuple[Dict, List[bytes], bytes]:
+    """A scheme-2 version-16 STGC file -> (side information with 'passes', 4 lm blobs, stego bytes)."""
+    if pee_scheme(data) != 2:
+        raise ValueError("not a scheme-2 MED-PEE container")
+    (hlen,) = struct.unpack(">I", data[4:8])
+    hdr = data[8:8 + hlen]
+    n0 = struct.calcsize(_PEE2_FMT)
+    (_v, cid, bpp, _s, width, height, T, maxval, L, status) = struct.unpack(_PEE2_FMT, hdr[:n0])
+    passes, blobs, body, pos = [], [], data[8 + hlen:], 0
+    for p in range(4):
+        Lp, endp, stp, nb = struct.unpack(_PEE2_PASS, hdr[n0 + 16 * p: n0 + 16 * (p + 1)])
+        passes.append({"L": Lp, "end": endp, "status": stp})
+        blobs.append(body[pos:pos + nb])
+        pos += nb
+    md = {"version": PEE_VERSION, "scheme": 2, "codec": CODEC_NAMES.get(cid, "raw" if cid == 0 else "unknown"),
+          "bytes": bpp, "width": width, "height": height, "T": T, "maxval": maxval, "L": L, "status": status,
+          "passes": passes}
+    return md, blobs, body[pos:]
+
+
+def parse_pee_bytes(data: bytes) -> Tuple[Dict, bytes, bytes]:
+    """A version-16 STGC file of scheme 1 -> (side information, lm_blob, stego bytes)."""
+    if pee_scheme(data) != 1:
+        raise ValueError("a scheme-2 MED-PEE container: use parse_pee2_bytes")
+    (hlen,) = struct.unpack(">I", data[4:8])
+    hdr = data[8:8 + hlen]
     (_v, cid, bpp, _r, width, height, T, L, end, maxval, status, blob_size) = struct.unpack(
         _PEE_FMT, hdr[:struct.calcsize(_PEE_FMT)])
     body = data[8 + hlen:]

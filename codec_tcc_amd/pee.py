@@ -23,6 +23,14 @@ from . import _lib, framing
 from .codec import _elem_bytes, _require_gpu, _stream, _torch
 
 
+def lattice_geometry(lattice: int, H: int, W: int):
+    """(y0, x0, hc, wc) of scheme 2's lattice p: candidate (i, j) is pixel (y0 + 2i, x0 + 2j),
+    i < hc, j < wc (include/codec_tcc.h, codec_pee_multi_embed_pass)."""
+    ry, rx = ((1, 1), (0, 0), (1, 0), (0, 1))[lattice]
+    y0, x0 = (1 if ry else 2), (1 if rx else 2)
+    return y0, x0, max(0, (H - y0 + 1) // 2), max(0, (W - x0 + 1) // 2)
+
+
 @dataclass
 class PeeEncoded:
     stego: object      # torch [B,H,W]

@@ -138,12 +138,13 @@ def decode_bin_exact(filepath: str, search_block_size: Optional[int] = None) -> 
 
 # ------------------------------------------------------------------ MED-PEE files
 def encode_file_pee(image, payload, out_path: str, *, T=2, tmax: int = 16, maxval: Optional[int] = None,
-                    codec: str = "raw") -> Dict:
+                    codec: str = "raw", scheme: int = 1) -> Dict:
     """MED-PEE embed of one slice into a version-16 STGC file.  `image` is an array or a
     DICOM path; maxval defaults to the DICOM's full scale 2**BitsStored - 1 (4095 for the
     reference's 12-bit pe.dcm), else the dtype maximum.  T = 'auto' picks the smallest
     T <= tmax whose capacity holds the payload.  A payload beyond the capacity is truncated
-    (status 1, 'L' = bits embedded); the file stays exactly reversible."""
+    (status 1, 'L' = bits embedded); the file stays exactly reversible.  scheme 2: four
+    sublattice passes (integer T; container scheme byte 2)."""
     from .pee import PeeCodec, lm_bits
     _require_gpu()
     torch = _torch()
@@ -157,8 +158,20 @@ def encode_file_pee(image, payload, out_path: str, *, T=2, tmax: int = 16, maxva
         raise ValueError("A imagem deve ser 2D uint8 ou uint16.")
     h, w = img.shape
     bits = framing.to_bits(payload)
-    pc = PeeCodec(1, h, w, dtype=str(img.dtype), T=T, tmax=tmax, maxval=maxval)
+    pc = PeeCodec(1, h, w, dtype=str(img.dtype), T=T, tmax=tmax, maxval=maxval, scheme=scheme)
     enc = pc.embed(torch.from_numpy(np.ascontiguousarray(img)[None]).cuda(), [bits])
+    if scheme == 2:
+        prs = [pr[0] for pr in enc.pass_records()]
+        blobs = [container.lm_blob(lm_bits(enc, 0, p)) if prs[p].end >= 0 else b"" for p in range(4)]
+        embedded = enc.embedded()[0]
+        status = 1 if embedded < len(bits) else 0
+        stego = enc.stego.cpu().numpy()[0]
+        hdr = container.create_pee2_header(codec, img.dtype.itemsize, w, h, pc.T, pc.maxval, embedded, status,
+                                           [(r.L, r.end, r.status, len(b)) for r, b in zip(prs, blobs)])
+        size = container.create_binary_file(out_path, hdr, _compress(stego, codec), b"".join(blobs))
+        return {"path": out_path, "bytes": size, "T": pc.T, "L": embedded, "maxval": pc.maxval, "status": status,
+                "scheme": 2, "passes": [{"L": r.L, "end": r.end, "status": r.status, "lm_count": r.lm_count}
+                                        for r in prs], "stego": stego}
     r = enc.records()[0]
     embedded = min(len(bits), r.capacity) if r.status == 1 else len(bits)
     lmb = container.lm_blob(lm_bits(enc, 0)) if r.end >= 0 else b""
@@ -176,7 +189,10 @@ def decode_bin_pee(filepath: str) -> Tuple[np.ndarray, np.ndarray]:
     _require_gpu()
     torch = _torch()
     with open(filepath, "rb") as f:
-        md, blob, data = container.parse_pee_bytes(f.read())
+        raw = f.read()
+    if container.pee_scheme(raw) == 2:
+        return _decode_pee2(raw)
+    md, blob, data = container.parse_pee_bytes(raw)
     h, w = md["height"], md["width"]
     stego = _decompress(data, md["codec"], h, w)
     if stego.dtype.itemsize != md["bytes"]:
@@ -196,4 +212,37 @@ def decode_bin_pee(filepath: str) -> Tuple[np.ndarray, np.ndarray]:
     pw = max(1, (md["L"] + 63) // 64)
     words, cover = pc.extract(torch.from_numpy(np.ascontiguousarray(stego)[None]).cuda(), meta, lm_t,
                               payload_words=pw)
+    return framing.unpack_bits(words.cpu().numpy()[0], md["L"]), cover.cpu().numpy()[0]
+
+
+def _decode_pee2(raw: bytes) -> Tuple[np.ndarray, np.ndarray]:
+    """Scheme-2 file: the passes' records rebuilt from the header, then the reverse passes."""
+    from .pee import PeeCodec, PeeEncoded, lattice_geometry
+    torch = _torch()
+    md, blobs, data = container.parse_pee2_bytes(raw)
+    h, w = md["height"], md["width"]
+    stego = _decompress(data, md["codec"], h, w)
+    if stego.dtype.itemsize != md["bytes"]:
+        raise ValueError("stego pixel size does not match the MED-PEE header")
+    pc = PeeCodec(1, h, w, dtype=str(stego.dtype), T=max(1, md["T"]), maxval=md["maxval"], scheme=2)
+    lm = np.zeros((4, 1, pc.lm_words * 64), dtype=bool)
+    metas = bytearray()
+    for p, ps in enumerate(md["passes"]):
+        if ps["end"] >= 0:
+            lm[p, 0, : ps["end"] + 1] = container.lm_from_blob(blobs[p], ps["end"])
+        _y0, _x0, hc, wc = lattice_geometry(p, h, w)
+        m = _lib.PeeMeta()
+        nc = hc * wc
+        m.T, m.maxval, m.L, m.end = md["T"], md["maxval"], ps["L"], ps["end"]
+        m.nc, m.ntiles = nc, (nc + 1023) // 1024
+        m.tile_end = ps["end"] // 1024 if ps["end"] >= 0 else -1
+        m.status, m.capacity, m.h, m.w = ps["status"], ps["L"], h, w
+        m.reserved[0] = p
+        metas += bytes(m)
+    meta_t = torch.frombuffer(metas, dtype=torch.uint8).view(4, 1, -1).cuda()
+    lm_t = torch.from_numpy(np.packbits(lm, axis=-1, bitorder="little").view(np.int64).copy()).cuda()
+    pw = max(1, (md["L"] + 63) // 64)
+    enc = PeeEncoded(stego=torch.from_numpy(np.ascontiguousarray(stego)[None]).cuda(), lm=lm_t, meta=meta_t,
+                     lengths=[md["L"]], payload_words=pw, config=pc.config, scheme=2)
+    words, cover = pc.extract(enc.stego, enc.meta, enc.lm, payload_words=pw)
     return framing.unpack_bits(words.cpu().numpy()[0], md["L"]), cover.cpu().numpy()[0]

@@ -339,7 +339,7 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
                       size_t workspace_bytes, void* stream);
 
 /* ---- MED-PEE scheme 2: four sublattice passes (oracle/pee_cpu.py "Scheme 2"; the version-16
- * container's scheme byte 1).  Pass p (0..3) runs the scheme above on lattice p -- (odd, odd),
+ * container's scheme byte 2).  Pass p (0..3) runs the scheme above on lattice p -- (odd, odd),
  * (even, even), (odd, even), (even, odd) as (row, column) parities, pixels with y >= 1 and
  * x >= 1, candidate (i, j) at (y0 + 2i, x0 + 2j) with y0 / x0 = 1 for an odd parity, 2 for an
  * even one -- on the RUNNING image, taking the next min(remaining, capacity_p) payload bits

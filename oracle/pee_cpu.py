@@ -30,7 +30,7 @@ Scheme (integer only):
   decoding    e' = x' - pred; LM -> unchanged; -2T <= e' < 2T -> bit = e' & 1,
               x = pred + (e' >> 1); e' >= 2T -> x = x' - T; else x = x' + T.
 
-Scheme 2, four sublattice passes (the version-16 container's scheme byte 1):
+Scheme 2, four sublattice passes (the version-16 container's scheme byte 2):
   lattices    pass 0 (odd, odd) -- scheme 1's candidates; pass 1 (even, even); pass 2 (odd, even);
               pass 3 (even, odd), as (row, column) parities, with y >= 1 and x >= 1 (so every
               candidate has its W / N / NW neighbours).  Each lattice's three MED neighbours lie on

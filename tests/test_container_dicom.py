@@ -168,6 +168,40 @@ def test_pee_container_roundtrip(tmp_path):
         container.parse_pee_bytes(b"STGC" + struct.pack(">I", 1) + b"\x01")
 
 
+def test_pee2_container_roundtrip(tmp_path):
+    """Scheme 2's header (scheme byte 2, four passes' records and maps) round-trips, and each
+    scheme's parser refuses the other's files."""
+    rng = np.random.default_rng(4)
+    lms = [rng.random(n) < 0.1 for n in (300, 17, 0, 5)]
+    blobs = [container.lm_blob(m) if m.size else b"" for m in lms]
+    passes = [(120, 299, 1, len(blobs[0])), (40, 16, 0, len(blobs[1])), (0, -1, 0, 0), (9, 4, 0, len(blobs[3]))]
+    hdr = container.create_pee2_header("raw", 2, 64, 48, 2, 4095, 169, 0, passes)
+    path = str(tmp_path / "p2.bin")
+    container.create_binary_file(path, hdr, b"stego-bytes", b"".join(blobs))
+    raw = open(path, "rb").read()
+    assert container.pee_scheme(raw) == 2
+    md, bl, st = container.parse_pee2_bytes(raw)
+    assert (md["codec"], md["bytes"], md["width"], md["height"], md["T"], md["maxval"], md["L"], md["status"]) == \
+        ("raw", 2, 64, 48, 2, 4095, 169, 0)
+    assert st == b"stego-bytes"
+    for p, (ps, m) in enumerate(zip(md["passes"], lms)):
+        assert (ps["L"], ps["end"], ps["status"]) == passes[p][:3]
+        if ps["end"] >= 0:
+            np.testing.assert_array_equal(container.lm_from_blob(bl[p], ps["end"]), m[: ps["end"] + 1])
+    with pytest.raises(ValueError, match="scheme-2"):
+        container.parse_pee_bytes(raw)
+    one = container.create_pee_header("raw", 2, 8, 8, 2, 0, -1, 4095, 0, 0)
+    container.create_binary_file(path, one, b"x", b"")
+    assert container.pee_scheme(open(path, "rb").read()) == 1
+    with pytest.raises(ValueError):
+        container.parse_pee2_bytes(open(path, "rb").read())
+    bad = bytearray(hdr)
+    bad[3] = 7
+    container.create_binary_file(path, bytes(bad), b"x", b"")
+    with pytest.raises(ValueError, match="scheme byte"):
+        container.pee_scheme(open(path, "rb").read())
+
+
 def test_j2k_jls_raise_clearly():
     from codec_tcc_amd import pipeline
     for c in ("j2k", "jls"):
@@ -237,6 +271,32 @@ def test_pee_file_pipeline_gpu(name, codec, T, tmp_path):
     np.testing.assert_array_equal(cover, img)
     if name == "pe":
         assert info["lm_count"] > 0 or side["lm"].sum() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,codec,T", [("pe", "raw", 1), ("torax", "png", 2)])
+def test_pee2_file_pipeline_gpu(name, codec, T, tmp_path):
+    """C5 with scheme 2: the reference's DICOMs, four sublattice passes, a version-16 file with
+    scheme byte 2 (every pass's record and map), recovered exactly from the file alone; the
+    stego equals the oracle's."""
+    pytest.importorskip("torch")
+    from codec_tcc_amd import framing, pipeline
+    from oracle import pee_cpu as P
+    src = str(tmp_path / f"{name}.dcm")
+    open(src, "wb").write(_dicom_file(name))
+    img = golden_io.images()[name]
+    maxval = 4095 if name == "pe" else 255
+    payload = "".join(chr(32 + (i * 11) % 95) for i in range(900))
+    bits = framing.to_bits(payload)
+    out = str(tmp_path / "pee2.bin")
+    info = pipeline.encode_file_pee(src, payload, out, T=T, codec=codec, scheme=2)
+    st, side = P.pee_embed_multi(img, bits, T, maxval=maxval)
+    assert info["scheme"] == 2 and info["status"] == side["status"] and info["L"] == side["L"]
+    assert [p["L"] for p in info["passes"]] == [p["L"] for p in side["passes"]]
+    np.testing.assert_array_equal(info["stego"], st)
+    got, cover = pipeline.decode_bin_pee(out)
+    np.testing.assert_array_equal(got, bits[: side["L"]])
+    np.testing.assert_array_equal(cover, img)
 
 
 _FAKE_CJXL = '''import sys
