@@ -353,7 +353,7 @@ def _as_batch(covers):
 
 def encode(covers, payloads: Sequence, *, method: str = "lsb", beta: float = 0.4, block: int = 16,
            align: bool = False, mode: str = "hybrid", nbits: Optional[int] = None, T=2, tmax: int = 16,
-           maxval: Optional[int] = None):
+           maxval: Optional[int] = None, scheme: int = 1):
     """Embed one payload per slice.
 
     method="lsb" (default): the reference's bit-plane scheme, bit-exact with src/codec.py;
@@ -361,12 +361,13 @@ def encode(covers, payloads: Sequence, *, method: str = "lsb", beta: float = 0.4
     Returns an Encoded.
     method="pee": MED-predictor prediction-error expansion (the north star's algorithm; the
     reference has none): T = expansion threshold or "auto" (capacity control,
-    smallest T <= tmax per slice), maxval = largest legal pixel value (4095 for 12-bit data).
+    smallest T <= tmax per slice), maxval = largest legal pixel value (4095 for 12-bit data),
+    scheme = 1 (the (odd, odd) lattice) or 2 (four sublattice passes, integer T).
     Returns a pee.PeeEncoded; beta/block/align/mode/nbits do not apply.
     decode() takes either result."""
     if method == "pee":
         from . import pee
-        return pee.encode(covers, payloads, T=T, tmax=tmax, maxval=maxval)
+        return pee.encode(covers, payloads, T=T, tmax=tmax, maxval=maxval, scheme=scheme)
     if method != "lsb":
         raise ValueError("method must be 'lsb' or 'pee'")
     _require_gpu()

@@ -1222,12 +1222,12 @@ def test_gpu_multipass_c3_1kb_at_t2():
     torch = pytest.importorskip("torch")
     import codec_tcc_amd as ct
     from codec_tcc_amd import quality
-    from codec_tcc_amd.pee import encode, decode
+    from codec_tcc_amd.pee import encode
     B = 16
     covers = torch.from_numpy(np.stack([synth.ct12(512, 512, 40 + i) for i in range(B)])).cuda()
     msgs = [synth.payload(1024, 600 + i) for i in range(B)]
-    enc2 = encode(covers, msgs, T=2, maxval=4095, scheme=2)
-    bits, cover = decode(enc2)
+    enc2 = ct.encode(covers, msgs, method="pee", T=2, maxval=4095, scheme=2)
+    bits, cover = ct.decode(enc2)
     assert torch.equal(cover, covers)
     from codec_tcc_amd import framing
     for i, m in enumerate(msgs):
