@@ -65,6 +65,17 @@ class PeeMeta(C.Structure):
                 ("flags", C.c_int32), ("reserved", C.c_int32 * 3)]
 
 
+def tuning_knob(name: str, default: int) -> int:
+    """A Python-side launch-shape knob, honoured like the library's (include/codec_tcc.h,
+    codec_set_tuning): the environment value only when CODEC_TUNING=1, else the default."""
+    if os.environ.get("CODEC_TUNING", "0") != "1":
+        return default
+    try:
+        return int(os.environ.get(name, default))
+    except ValueError:
+        return default
+
+
 PEE_PARTIAL = 1
 PEE_RECORD_HDR_WORDS = 8   # CODEC_PEE_RECORD_HDR_WORDS: codec_pee_meta in uint64 words
 META_BYTES = C.sizeof(SliceMeta)

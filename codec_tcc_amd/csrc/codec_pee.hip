@@ -4187,6 +4187,16 @@ __global__ __launch_bounds__(256) void k_pee_lat_recover(T* __restrict__ img, in
     }
 }
 
+// pass 0 is scheme 1 on its own lattice: its record keeps the number of bits it embedded in L
+// (scheme 1 keeps the requested length there and its capacity when it fills up)
+__global__ __launch_bounds__(256) void k_pee_pass0_fix(codec_pee_meta* __restrict__ metas, int B) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= B) return;
+    codec_pee_meta* M = metas + b;
+    if (M->status == 1) M->L = M->capacity;
+    M->reserved[0] = 0;
+}
+
 static int pee_multi_check(const codec_pee_params* P, int pass) {
     int rc = pee_check(P);
     if (rc) return rc;
@@ -4207,6 +4217,16 @@ int codec_pee_multi_embed_pass(const codec_pee_params* P, int32_t pass, const vo
     const PeeWs L = pee_ws(P);
     if (workspace_bytes < L.total) return set_err(CODEC_EINVAL, "workspace too small");
     hipStream_t st = as_stream(stream);
+    if (pass == 0 && knob("CODEC_PEE_MULTI_P0", 1) != 0) {
+        // lattice 0 is scheme 1's: its embed paths (copy fused, 16-B items, look-back or
+        // slice-serial) take the pass, and the records are made scheme 2's
+        rc = codec_pee_embed_ts(P, cover, stego, payload, lengths, nullptr, metas, lm, workspace, workspace_bytes,
+                                stream);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_pee_pass0_fix, dim3((unsigned)((P->B + 255) / 256)), dim3(256), 0, st, metas, P->B);
+        LAUNCH_CHECK("k_pee_pass0_fix");
+        return 0;
+    }
     HIP_TRY(pee_ws_enter(workspace, P, L, st));
     uint32_t* cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.cnt);
     uint32_t* off = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + L.off);

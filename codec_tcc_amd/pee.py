@@ -212,8 +212,14 @@ class PeeCodec:
                                                           self.workspace.numel(), _stream()),
                            "codec_pee_multi_embed_pass")
         self._guarded(launch)
-        return PeeEncoded(stego=stego, lm=lm, meta=meta, lengths=list(lengths), payload_words=int(words.shape[1]),
-                          config=self.config, scheme=2)
+        enc = PeeEncoded(stego=stego, lm=lm, meta=meta, lengths=list(lengths), payload_words=int(words.shape[1]),
+                         config=self.config, scheme=2)
+        if check:   # pass 0 in place runs scheme 1's look-back embed
+            recs = enc.pass_records()[0]
+            if any(r.status not in (0, 1) for r in recs):
+                self.reset()
+            _raise_lookback(recs)
+        return enc
 
     def extract(self, stego, meta, lm, *, payload_words: int, cover=None, payload=None):
         torch = _torch()
@@ -234,14 +240,26 @@ class PeeCodec:
         P = self._params(payload_words)
         lib = _lib.load()
 
+        # pass 0 is scheme 1 on its lattice: its in-place extract (scheme 1's kernels) into a
+        # buffer of its own, OR-ed in (it writes whole payload words); CODEC_PEE_MULTI_P0=0
+        # keeps it on the lattice kernels
+        p0 = _lib.tuning_knob("CODEC_PEE_MULTI_P0", 1) != 0
+        torch = _torch()
+
         def launch():
             payload.zero_()
-            for p in (3, 2, 1, 0):
+            for p in ((3, 2, 1) if p0 else (3, 2, 1, 0)):
                 src = stego if p == 3 else cover
                 _lib.check(lib.codec_pee_multi_extract_pass(C.byref(P), p, src.data_ptr(), meta.data_ptr(),
                                                             lm[p].data_ptr(), cover.data_ptr(), payload.data_ptr(),
                                                             self.workspace.data_ptr(), self.workspace.numel(),
                                                             _stream()), "codec_pee_multi_extract_pass")
+            if p0:
+                tmp = torch.empty_like(payload)
+                _lib.check(lib.codec_pee_extract(C.byref(P), cover.data_ptr(), meta[0].data_ptr(), lm[0].data_ptr(),
+                                                 cover.data_ptr(), tmp.data_ptr(), self.workspace.data_ptr(),
+                                                 self.workspace.numel(), _stream()), "codec_pee_extract")
+                payload.bitwise_or_(tmp)
         self._guarded(launch)
         return payload, cover
 
@@ -273,6 +291,10 @@ class PeeCodec:
                 raise ValueError(f"payload exceeds PEE capacity in slices {short} (scheme 2, T={self.T})")
             words, cover = self.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words)
             host = words.cpu().numpy()
+            if self.lookback_failed(enc.payload_words):   # pass 0's in-place extract (scheme 1's)
+                self.reset()
+                raise RuntimeError("codec_pee_extract: in-place cursor look-back timed out; the recovered "
+                                   "payload is invalid (the restored cover is exact)")
             return [framing.unpack_bits(host[i], enc.lengths[i]) for i in range(self.B)], cover
         recs = enc.records()
         _raise_lookback(recs)

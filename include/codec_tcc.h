@@ -352,13 +352,17 @@ int codec_pee_extract(const codec_pee_params* P, const void* stego, const codec_
  * [B][lm_words] location map.  The PEE workspace (codec_pee_workspace_bytes) is shared with
  * scheme 1.  Passes are ordered calls on one stream. */
 /* embed pass `pass`: stego = cover (copied when they differ), then the pass in place on
- * stego.  Pass 0 with cover != stego, passes 1..3 with cover == stego. */
+ * stego.  Pass 0 with cover != stego, passes 1..3 with cover == stego.  Pass 0 is scheme 1 on
+ * its lattice and runs through codec_pee_embed_ts (its record's L made the embedded count;
+ * an in-place pass 0 can report CODEC_PEE_ELOOKBACK like codec_pee_embed). */
 int codec_pee_multi_embed_pass(const codec_pee_params* P, int32_t pass, const void* cover, void* stego,
                                const uint64_t* payload, const int32_t* lengths, codec_pee_meta* metas,
                                uint64_t* lm, void* workspace, size_t workspace_bytes, void* stream);
 /* extract pass `pass` (call 3, 2, 1, 0): cover_out = stego (copied when they differ), then
  * the pass restores its lattice in place and ORs its bits into payload_out (zero it before
- * the first pass). */
+ * the first pass).  For pass 0 a caller may use codec_pee_extract (in place, with the pass-0
+ * records and map) into a separate payload buffer and OR it in -- scheme 1's faster kernels,
+ * what PeeCodec does. */
 int codec_pee_multi_extract_pass(const codec_pee_params* P, int32_t pass, const void* stego,
                                  const codec_pee_meta* metas, const uint64_t* lm, void* cover_out,
                                  uint64_t* payload_out, void* workspace, size_t workspace_bytes, void* stream);
