@@ -4102,13 +4102,15 @@ __global__ __launch_bounds__(256) void k_pee_lat_dcount(const T* __restrict__ im
     const u64* lm = lm_all + (size_t)b * lmw;
     for (int t = blockIdx.x; t <= tile_end; t += gridDim.x) {
         const int k0 = t * PEE_TILE + 4 * threadIdx.x;
+        // the 4 candidates' location-map bits share one word (k0 % 4 == 0)
+        const u64 lmw4 = (k0 >> 6) < lmw ? lm[k0 >> 6] : 0ull;
         LatQuad<T> q;
         q.load(src, W, g, k0, end);
         uint32_t local = 0;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int k = k0 + u;
-            if (k <= end && !lm_bit(lm, k, lmw)) {
+            if (k <= end && !((lmw4 >> (k & 63)) & 1ull)) {
                 const int e2 = q.x[u] - med3(q.a[u], q.b[u], q.c[u]);
                 local += (e2 >= -2 * Tthr && e2 < 2 * Tthr) ? 1u : 0u;
             }
@@ -4140,6 +4142,8 @@ __global__ __launch_bounds__(256) void k_pee_lat_recover(T* __restrict__ img, in
     const uint32_t* off = tile_off_all + (size_t)b * ntiles_max;
     for (int t = blockIdx.x; t <= tile_end; t += gridDim.x) {
         const int k0 = t * PEE_TILE + 4 * threadIdx.x;
+        // the 4 candidates' location-map bits share one word (k0 % 4 == 0)
+        const u64 lmw4 = (k0 >> 6) < lmw ? lm[k0 >> 6] : 0ull;
         LatQuad<T> q;
         q.load(dst, W, g, k0, end);
         int ps[4];
@@ -4148,7 +4152,7 @@ __global__ __launch_bounds__(256) void k_pee_lat_recover(T* __restrict__ img, in
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int k = k0 + u;
-            act[u] = k <= end && !lm_bit(lm, k, lmw);
+            act[u] = k <= end && !((lmw4 >> (k & 63)) & 1ull);
             inner[u] = false;
             ps[u] = 0;
             if (act[u]) {
