@@ -603,7 +603,9 @@ __device__ __noinline__ void hist16_fix(uint32_t* ghist, uint32_t v, uint32_t cn
 // merged into one add (constant regions), the 8 LDS atomics are issued back to back and
 // their returned values are checked for 16-bit wraps only afterwards, so the adds
 // pipeline instead of each waiting for its return.
-template <typename T, typename V>
+// NORET: the workgroup counts fewer than 65 536 pixels, so no 16-bit field can wrap and the
+// adds need no return (ds_add_u32 instead of ds_add_rtn_u32)
+template <typename T, typename V, bool NORET = false>
 __device__ __forceinline__ void hist_add8(uint32_t* lds, uint32_t* ghist, const V& vec, uint32_t* wrapf = nullptr) {
     uint32_t px[8];
     if constexpr (sizeof(T) == 2) {
@@ -622,7 +624,11 @@ __device__ __forceinline__ void hist_add8(uint32_t* lds, uint32_t* ghist, const 
         run = eq ? run + 1u : 1u;
     }
     cnt[7] = run;
-    if constexpr (sizeof(T) == 2) {
+    if constexpr (sizeof(T) == 2 && NORET) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (cnt[k]) atomicAdd(&lds[px[k] >> 1], (px[k] & 1u) ? (cnt[k] << 16) : cnt[k]);
+    } else if constexpr (sizeof(T) == 2) {
         uint32_t old[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -656,7 +662,7 @@ __device__ __forceinline__ void hist_add8(uint32_t* lds, uint32_t* ghist, const 
 // Work item = (band of SB rows, 8-pixel column chunk); a wave covers 64 consecutive
 // chunks of one band, so every load instruction reads 1 KiB (u16) contiguously; the
 // SB/8 lanes of one block column combine their LSB counts with shuffles.
-template <typename T, int SB, bool NT, bool HIST>
+template <typename T, int SB, bool NT, bool HIST, bool NORET = false>
 __device__ __forceinline__ void scan_fast_body(const T* __restrict__ cover, T* __restrict__ stego,
                                                int H, int W, int bands_per_wg,
                                                uint32_t* __restrict__ ghist_all,
@@ -725,7 +731,7 @@ __device__ __forceinline__ void scan_fast_body(const T* __restrict__ cover, T* _
                 for (int k = 0; k < RB; ++k) {
                     ones += lsb_count(v[k]);
                     vor |= vor_of(v[k]);
-                    if constexpr (HIST) hist_add8<T>(lds, ghist, v[k]);
+                    if constexpr (HIST) hist_add8<T, typename Vec8<T>::type, NORET>(lds, ghist, v[k]);
                 }
             }
             for (; r < rows; ++r) {
@@ -733,7 +739,7 @@ __device__ __forceinline__ void scan_fast_body(const T* __restrict__ cover, T* _
                 if (d) stv<NT>(d + (size_t)r * stride, v0);
                 ones += lsb_count(v0);
                 vor |= vor_of(v0);
-                if constexpr (HIST) hist_add8<T>(lds, ghist, v0);
+                if constexpr (HIST) hist_add8<T, typename Vec8<T>::type, NORET>(lds, ghist, v0);
             }
         }
 #pragma unroll
@@ -766,12 +772,12 @@ __device__ __forceinline__ void scan_fast_body(const T* __restrict__ cover, T* _
     }
 }
 
-template <typename T, int SB, bool NT, bool HIST = true>
+template <typename T, int SB, bool NT, bool HIST = true, bool NORET = false>
 __global__ __launch_bounds__(1024) void k_scan_fast(const T* __restrict__ cover, T* __restrict__ stego,
                                                     int H, int W, int bands_per_wg,
                                                     uint32_t* __restrict__ ghist_all,
                                                     u64* __restrict__ gkey, uint32_t* __restrict__ gor, int csplit) {
-    scan_fast_body<T, SB, NT, HIST>(cover, stego, H, W, bands_per_wg, ghist_all, gkey, gor, csplit);
+    scan_fast_body<T, SB, NT, HIST, NORET>(cover, stego, H, W, bands_per_wg, ghist_all, gkey, gor, csplit);
 }
 
 // read-only variant (plan only, or in place where the stego copy is the cover itself); a
@@ -3401,11 +3407,18 @@ static int launch_scan_fast(const codec_params* P, const void* cover, void* steg
         LAUNCH_CHECK("k_scan_read");
         return 0;
     }
+    // workgroups counting fewer than 65 536 pixels (e.g. a lone 2048^2 slice: one 16-row band
+    // each) cannot wrap a 16-bit LDS field: their histogram adds need no return
+    const int CRp_ = (P->W / 8 + sb / 8 - 1) / (sb / 8) * (sb / 8);
+    const long long seg_cols = (long long)((CRp_ / (sb / 8) + csplit - 1) / csplit) * (sb / 8) * 8;
+    const bool noret = sizeof(T) == 2 && (long long)bpw * sb * std::min<long long>(P->W, seg_cols) < 65536 &&
+                       knob("CODEC_SCAN_NORET", 1) != 0;
     ProfScope prof(st, CODEC_K_SCAN_FAST);
     switch (sb) {
         case 8: if (nt) hipLaunchKernelGGL((k_scan_fast<T, 8, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv, csplit);
                 else hipLaunchKernelGGL((k_scan_fast<T, 8, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv, csplit); break;
         case 16: if (knob("CODEC_DIAG_NOHIST", 0)) hipLaunchKernelGGL((k_scan_fast<T, 16, true, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv, csplit);   // timing diagnostics only: s is wrong
+                else if (nt && noret) hipLaunchKernelGGL((k_scan_fast<T, 16, true, true, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv, csplit);
                 else if (nt) hipLaunchKernelGGL((k_scan_fast<T, 16, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv, csplit);
                 else hipLaunchKernelGGL((k_scan_fast<T, 16, false>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv, csplit); break;
         case 32: if (nt) hipLaunchKernelGGL((k_scan_fast<T, 32, true>), grid, dim3(1024), 0, st, c, s, P->H, P->W, bpw, hist, keys, orv, csplit);
