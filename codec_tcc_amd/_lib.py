@@ -117,6 +117,8 @@ _SIGS = {
                                              C.c_size_t, _VP]),
     "codec_pee_multi_extract_pass": (C.c_int, [C.POINTER(PeeParams), C.c_int32, _VP, _VP, _VP, _VP, _VP, _VP,
                                                C.c_size_t, _VP]),
+    "codec_pee_multi_embed": (C.c_int, [C.POINTER(PeeParams), _VP, _VP, _VP, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),
+    "codec_pee_multi_extract": (C.c_int, [C.POINTER(PeeParams), _VP, _VP, _VP, _VP, _VP, _VP, C.c_size_t, _VP]),
     "codec_pee_pack_records": (C.c_int, [C.c_int32, C.c_int32, _VP, _VP, C.c_int32, _VP, _VP]),
     "codec_pee_unpack_records": (C.c_int, [C.c_int32, C.c_int32, _VP, C.c_int32, _VP, _VP, _VP]),
     "codec_quality_moments": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP, _VP, _VP, _VP]),
@@ -132,7 +134,8 @@ KERNEL_TAGS = {1: "k_scan_fast", 2: "k_scan_generic", 3: "k_block_exact", 4: "k_
                19: "k_scan_rows", 20: "k_scan_rows_read", 21: "k_quality", 22: "k_decide_embed",
                23: "k_pee_capacity", 24: "k_pee_embed_ss", 25: "k_pee_extract_ss",
                26: "k_pee_embed_ss_auto", 27: "k_pee_embed_res", 28: "k_scan_decide",
-               29: "k_pee_lat_count", 30: "k_pee_lat_embed", 31: "k_pee_lat_dcount", 32: "k_pee_lat_recover"}
+               29: "k_pee_lat_count", 30: "k_pee_lat_embed", 31: "k_pee_lat_dcount", 32: "k_pee_lat_recover",
+               33: "k_pee_lat_ss_embed", 34: "k_pee_lat_ss_extract"}
 EXPORTS = tuple(_SIGS)
 
 _lib = None

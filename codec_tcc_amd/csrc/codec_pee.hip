@@ -4191,6 +4191,267 @@ __global__ __launch_bounds__(256) void k_pee_lat_recover(T* __restrict__ img, in
     }
 }
 
+// ---- scheme 2, slice-serial: one 1024-thread workgroup per slice runs the (optional) copy and
+// then every pass of the slice in one launch -- embed passes p_first..3 ascending, extract
+// passes 3..0 descending -- with the payload cursor in a register.  The tile path above needs
+// per pass a full-lattice count, a per-slice scan and the prefix pass (three launches) plus a
+// stream copy; here a pass reads only the candidates up to its `end` (and the embed stops
+// counting there: capacity is then the count through that chunk, flagged CODEC_PEE_PARTIAL
+// like scheme 1's single pass).  Same records, pixels, maps and bits as the tile kernels
+// (tests/test_pee.py runs both against the oracle).  A chunk = 4096 candidates, 4
+// consecutive ones per lane (LatQuad's layout: lane t of chunk c holds candidates
+// 4096 c + 4 t .. + 3, so the map's 64-candidate words are the 16-lane DPP rows); the next
+// chunk's loads are issued before this one's scan (within a pass no candidate is a neighbour
+// of another, so they never read a pixel the pass writes).  Passes are separated by a
+// __syncthreads (workgroup-scope release/acquire: the next lattice reads this one's pixels).
+#define LSS_THREADS 1024
+#define LSS_CHUNK (4 * LSS_THREADS)
+#define LSS_PAD_WORDS (21 * 1024)
+   // 84 KB static LDS: one workgroup per CU, as k_pee_embed_ss
+
+template <typename T>
+__device__ __forceinline__ void lss_copy(const T* __restrict__ s, T* __restrict__ d, size_t npx, int mode) {
+    const int tid = threadIdx.x;
+    if (mode == 1) {   // 16-B vectors (slice bytes % 16 == 0, both bases aligned): 8 in flight per lane
+        const size_t nv = npx * sizeof(T) / 16;
+        const uint4* sv = reinterpret_cast<const uint4*>(s);
+        uint4* dv = reinterpret_cast<uint4*>(d);
+        size_t i = tid;
+        for (; i + 7 * LSS_THREADS < nv; i += 8 * LSS_THREADS) {
+            uint4 r[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) r[u] = ldv<true>(sv + i + u * LSS_THREADS);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) dv[i + u * LSS_THREADS] = r[u];
+        }
+        for (; i < nv; i += LSS_THREADS) dv[i] = ldv<true>(sv + i);
+    } else if (mode == 2) {
+        for (size_t i = tid; i < npx; i += LSS_THREADS) d[i] = s[i];
+    }
+}
+
+// PL: the slice's payload row staged in LDS (embed: read from it; extract: OR-ed into it, then
+// written out whole) when 2 pw 32-bit words fit the pad; else global loads / atomics.  Every
+// global store is unconditional -- a store that must not land goes to the wave's sink slot in
+// the workspace, as in k_pee_embed_ss -- so hipcc's vmcnt counting stays exact and waiting for
+// the next chunk's loads never drains this chunk's stores.
+#define LSS_PAY_BASE 64
+#define LSS_PAY_MAXW ((LSS_PAD_WORDS - LSS_PAY_BASE) / 2)
+template <typename T, bool EXTRACT, bool PL, bool PF>
+__global__ __launch_bounds__(LSS_THREADS) void k_pee_lat_ss(const T* __restrict__ src, T* dst, int H, int W, int T0,
+                                                            int maxval, int copy_mode, int p_first,
+                                                            u64* payload_all, int pw, const int32_t* __restrict__ lengths,
+                                                            codec_pee_meta* metas, int B, u64* lm_all, int lmw,
+                                                            char* __restrict__ sink) {
+    __shared__ uint32_t pad[LSS_PAD_WORDS];   // [0..31]: wave totals (2 x 16), [32]: end, [33]: unsafe count
+    uint32_t (*wtot)[16] = reinterpret_cast<uint32_t (*)[16]>(pad);
+    uint32_t* pay32 = pad + LSS_PAY_BASE;
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const size_t npx = (size_t)H * W;
+    T* img = dst + (size_t)b * npx;
+    T* const sink_px = reinterpret_cast<T*>(sink + SS_SINK_SLOT(b, tid));
+    u64* const sink_w = reinterpret_cast<u64*>(sink + SS_SINK_SLOT(b, tid) + 32);
+    u64* payload = payload_all + (size_t)b * pw;
+    if (PL) {   // embed: the payload row; extract: zeroed words the passes OR their bits into
+        for (int w = tid; w < 2 * pw; w += LSS_THREADS)
+            pay32[w] = EXTRACT ? 0u : reinterpret_cast<const uint32_t*>(payload)[w];
+    } else if (EXTRACT) {
+        for (int w = tid; w < pw; w += LSS_THREADS) payload[w] = 0ull;
+    }
+    if (copy_mode) lss_copy<T>(src + (size_t)b * npx, img, npx, copy_mode);
+    __syncthreads();
+    const uint32_t nbits = 64u * (uint32_t)pw;
+    uint32_t base = 0;   // embed: payload bits taken by the passes before this one
+    if (!EXTRACT)
+        for (int q = 0; q < p_first; ++q) base += (uint32_t)max(0, metas[(size_t)q * B + b].L);
+    int par = 0;
+    for (int step = 0; step < (EXTRACT ? 4 : 4 - p_first); ++step) {
+        const int p = EXTRACT ? 3 - step : p_first + step;
+        const PeeLat g = pee_lattice(p, H, W);
+        const int nc = g.hc * g.wc, ntiles = (nc + PEE_TILE - 1) / PEE_TILE;
+        codec_pee_meta* M = metas + (size_t)p * B + b;
+        u64* lm = lm_all + ((size_t)p * B + b) * lmw;
+        int end, Tt;
+        uint32_t pbase, lim;   // embed: lim = bits left; extract: lim = pbase + L
+        if (EXTRACT) {
+            if (M->tile_end < 0) continue;   // uniform
+            end = M->end;
+            Tt = M->T;
+            pbase = 0;
+            for (int q = 0; q < p; ++q) pbase += (uint32_t)max(0, metas[(size_t)q * B + b].L);
+            lim = pbase + (uint32_t)max(0, M->L);
+        } else {
+            const int rem = lengths[b] - (int)base;
+            if (rem <= 0) {   // nothing left: the pass leaves the slice untouched
+                if (tid == 0) {
+                    M->T = T0; M->maxval = maxval; M->L = 0; M->end = -1; M->nc = nc; M->ntiles = ntiles;
+                    M->tile_end = -1; M->status = 0; M->capacity = -1; M->lm_count = 0; M->h = H; M->w = W;
+                    M->flags = 0; M->reserved[0] = p; M->reserved[1] = 0; M->reserved[2] = 0;
+                }
+                continue;
+            }
+            end = nc - 1;   // until the chunk holding the rem-th expandable candidate is found
+            Tt = T0;
+            pbase = base;
+            lim = (uint32_t)rem;
+        }
+        if (!EXTRACT && tid == 0) pad[33] = 0;
+        const int kstop = EXTRACT ? end : nc - 1;   // last candidate a chunk may need
+        const int nch = kstop >= 0 ? kstop / LSS_CHUNK + 1 : 0;
+        uint32_t cursor = 0, unsafe = 0;   // rank of the chunk's first candidate (uniform); lane's unsafe count
+        int c_done = nch;                  // embed: chunks walked
+        bool found = false;
+        // PF: the next chunk's loads are issued before this one is processed (one chunk in
+        // flight; two in flight measured slower: 0.248 -> 0.324 ms C3 step).  extract: the 4
+        // candidates' map word (k0 % 4 == 0) rides with the pixels; its index is clamped
+        // (lmw * 64 >= nc > end: a lane past lmw has no active candidate)
+        LatQuad<T> qa;
+        u64 la = 0;
+        auto request = [&](LatQuad<T>& qq, u64& ll, int c) {
+            const int k0 = c * LSS_CHUNK + 4 * tid;
+            qq.load(img, W, g, k0, kstop);   // clamped past kstop
+            if (EXTRACT) ll = lm[min(k0 >> 6, lmw - 1)];
+        };
+        // one chunk; true when the embed has found `end` (the pass stops)
+        auto chunk = [&](const LatQuad<T>& cur, const u64 lmw4, const int c) -> bool {
+            const int k0 = c * LSS_CHUNK + 4 * tid;
+                uint32_t n = 0, fl = 0;
+                int ps[4];
+    #pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k = k0 + u;
+                    ps[u] = med3(cur.a[u], cur.b[u], cur.c[u]);
+                    const int e = cur.x[u] - ps[u];
+                    if (EXTRACT) {
+                        const bool act = k <= end && !((lmw4 >> (k & 63)) & 1ull);
+                        const bool inner = act && e >= -2 * Tt && e < 2 * Tt;
+                        fl |= (act ? 1u : 0u) << u | (inner ? 16u : 0u) << u;
+                        n += inner ? 1u : 0u;
+                    } else {
+                        const PeeCand pc = pee_classify(cur.x[u], cur.a[u], cur.b[u], cur.c[u], Tt, maxval);
+                        const bool in = k < nc;
+                        fl |= ((in & pc.expand & pc.safe) ? 1u : 0u) << u | ((in & pc.safe) ? 16u : 0u) << u |
+                              ((in & pc.right) ? 256u : 0u) << u | (in ? 4096u : 0u) << u;
+                        n += (in & pc.expand & pc.safe) ? 1u : 0u;
+                    }
+                }
+                uint32_t ex, tot, wb;
+                ss_scan_small(n, wtot, par, &ex, &tot, &wb);
+                par ^= 1;
+                const uint32_t r0 = cursor + ex;   // rank of this lane's first counted candidate
+                if (EXTRACT) {
+                    uint32_t r = pbase + r0;
+                    uint32_t word = 0;
+                    int wi = -1;
+    #pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const bool act = (fl >> u) & 1u, inner = (fl >> (4 + u)) & 1u;
+                        const int e2 = cur.x[u] - ps[u];
+                        if (inner) {
+                            if ((e2 & 1) && r < lim && r < nbits) {   // consecutive bits: one atomic per word
+                                if (wi != (int)(r >> 5)) {
+                                    if (wi >= 0 && word) {
+                                        if (PL) atomicOr(&pay32[wi], word);
+                                        else atomicOr(reinterpret_cast<uint32_t*>(payload) + wi, word);
+                                    }
+                                    wi = (int)(r >> 5);
+                                    word = 0;
+                                }
+                                word |= 1u << (r & 31);
+                            }
+                            ++r;
+                        }
+                        const int x = inner ? ps[u] + (e2 >> 1) : (e2 >= 2 * Tt ? cur.x[u] - Tt : cur.x[u] + Tt);
+                        *(act ? img + cur.o[u] : sink_px) = (T)x;
+                    }
+                    if (wi >= 0 && word) {
+                        if (PL) atomicOr(&pay32[wi], word);
+                        else atomicOr(reinterpret_cast<uint32_t*>(payload) + wi, word);
+                    }
+                    cursor += tot;
+                    return false;
+                }
+                // embed: candidate k is processed iff fewer than lim expandable ones precede it
+                const bool last = cursor + tot >= lim;   // this chunk holds the lim-th (uniform)
+                uint32_t r = r0, nib = 0;
+    #pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const bool proc = ((fl >> (12 + u)) & 1u) && r < lim;   // before nc and up to end
+                    const bool safe = (fl >> (4 + u)) & 1u, es = (fl >> u) & 1u;
+                    nib |= (proc && !safe) ? 1u << u : 0u;
+                    unsafe += (proc && !safe) ? 1u : 0u;
+                    const uint32_t bi = pbase + r;
+                    uint32_t bit;
+                    if (PL) {
+                        const uint32_t wv = pay32[min(bi >> 5, (uint32_t)(2 * pw - 1))];
+                        bit = bi < nbits ? (wv >> (bi & 31)) & 1u : 0u;
+                    } else {
+                        bit = (proc && es && bi < nbits) ? (uint32_t)((payload[bi >> 6] >> (bi & 63)) & 1ull) : 0u;
+                    }
+                    if (proc && es && r + 1 == lim) pad[32] = (uint32_t)(k0 + u);
+                    const int nv = es ? ps[u] + 2 * (cur.x[u] - ps[u]) + (int)bit
+                                      : (((fl >> (8 + u)) & 1u) ? cur.x[u] + Tt : cur.x[u] - Tt);
+                    *(proc && safe ? img + cur.o[u] : sink_px) = (T)nv;
+                    r += (proc && es) ? 1u : 0u;
+                }
+                // this chunk's map words (its 16-lane rows); in the chunk holding `end` only those of
+                // tiles <= end's tile (the tile path writes whole tiles up to tile_end)
+                const u64 word = row_or16_64((u64)nib << (4 * (lane & 15)));
+                int tile_lim = ntiles - 1;
+                if (last) {
+                    lds_barrier();   // pad[32] (end) visible
+                    end = (int)pad[32];
+                    tile_lim = end / PEE_TILE;
+                    found = true;
+                }
+                const int w = k0 >> 6;
+                *((lane & 15) == 0 && w < lmw && (k0 / PEE_TILE) <= tile_lim ? lm + w : sink_w) = word;
+                cursor += tot;
+                if (last) { c_done = c + 1; return true; }
+                return false;
+        };
+        if (PF && nch > 0) request(qa, la, 0);
+        for (int c = 0; c < nch; ++c) {
+            LatQuad<T> cur;
+            u64 lw = 0;
+            if (PF) {
+                cur = qa;
+                lw = la;
+                request(qa, la, c + 1);
+            } else {
+                request(cur, lw, c);
+            }
+            if (chunk(cur, lw, c)) break;
+        }
+        if (EXTRACT) {
+            __syncthreads();   // the next (lower) pass reads this lattice's restored pixels
+            continue;
+        }
+        if (unsafe) atomicAdd(&pad[33], unsafe);   // rare: candidates whose transform would overflow
+        __syncthreads();   // pad[33] complete; the next pass reads this lattice's pixels
+        if (tid == 0) {
+            M->T = T0; M->maxval = maxval; M->nc = nc; M->ntiles = ntiles; M->h = H; M->w = W;
+            M->lm_count = (int)pad[33];
+            M->reserved[0] = p; M->reserved[1] = 0; M->reserved[2] = 0;
+            if (!found) {   // the pass fills up: its capacity's bits, every candidate processed
+                M->L = (int)cursor; M->end = nc - 1; M->tile_end = ntiles - 1; M->status = 1;
+                M->capacity = (int)cursor; M->flags = 0;
+            } else {
+                M->L = (int)lim; M->end = end; M->tile_end = end / PEE_TILE; M->status = 0;
+                M->capacity = (int)cursor;   // counted through end's chunk: exact only if it is the last
+                M->flags = c_done < (nc + LSS_CHUNK - 1) / LSS_CHUNK ? CODEC_PEE_PARTIAL : 0;
+            }
+        }
+        base += found ? lim : cursor;
+        __syncthreads();   // pad[32..33] reusable
+    }
+    if (EXTRACT && PL) {   // the payload row, whole (the passes' last barrier ordered the ORs)
+        __syncthreads();
+        for (int w = tid; w < pw; w += LSS_THREADS)
+            payload[w] = (u64)pay32[2 * w] | ((u64)pay32[2 * w + 1] << 32);
+    }
+}
+
 // pass 0 is scheme 1 on its own lattice: its record keeps the number of bits it embedded in L
 // (scheme 1 keeps the requested length there and its capacity when it fills up)
 __global__ __launch_bounds__(256) void k_pee_pass0_fix(codec_pee_meta* __restrict__ metas, int B) {
@@ -4300,6 +4561,120 @@ int codec_pee_multi_extract_pass(const codec_pee_params* P, int32_t pass, const 
     if (P->bytes == 2) PLR(uint16_t); else PLR(uint8_t);
 #undef PLR
     LAUNCH_CHECK("k_pee_lat_recover");
+    return 0;
+}
+
+}  // extern "C"
+
+// the slice-serial scheme-2 launch (k_pee_lat_ss) where a chip-filling batch gives every CU a
+// slice, as for scheme 1 (pee_use_slice_serial); slices up to CODEC_PEE_LAT_SS_MAXPX pixels (one
+// CU streams its slice's copy).  CODEC_PEE_LAT_SS=0/1 forces the tile path / this one.
+static bool pee_multi_use_ss(const codec_pee_params* P) {
+    const long long k = knob("CODEC_PEE_LAT_SS", -1);
+    if (k == 0) return false;
+    if (k == 1) return true;
+    const long long ncu = device_cu_count();
+    if (P->B < ncu) return false;
+    const long long rounds = (P->B + ncu - 1) / ncu;
+    if ((double)P->B / (double)(rounds * ncu) < 0.85) return false;
+    return (long long)P->H * P->W <= knob("CODEC_PEE_LAT_SS_MAXPX", 1LL << 20);
+}
+// 0: in place (no copy); 1: 16-B vector copy; 2: element copy (unaligned or ragged slices)
+static int pee_lss_copy_mode(const codec_pee_params* P, const void* s, const void* d) {
+    if (s == d) return 0;
+    const size_t sb = (size_t)P->H * P->W * P->bytes;
+    return (sb % 16 == 0 && (uintptr_t)s % 16 == 0 && (uintptr_t)d % 16 == 0) ? 1 : 2;
+}
+
+extern "C" {
+
+int codec_pee_multi_embed(const codec_pee_params* P, const void* cover, void* stego, const uint64_t* payload,
+                          const int32_t* lengths, codec_pee_meta* metas, uint64_t* lm, void* workspace,
+                          size_t workspace_bytes, void* stream) {
+    int rc = pee_multi_check(P, 0);
+    if (rc) return rc;
+    if (!cover || !stego || !payload || !lengths || !metas || !lm || !workspace)
+        return set_err(CODEC_EINVAL, "codec_pee_multi_embed: NULL pointer argument");
+    if (workspace_bytes < pee_ws(P).total) return set_err(CODEC_EINVAL, "workspace too small");
+    const size_t lmp = (size_t)P->B * P->lm_words;   // one pass's map
+    if (!pee_multi_use_ss(P)) {
+        for (int p = 0; p < 4; ++p) {
+            rc = codec_pee_multi_embed_pass(P, p, p == 0 ? cover : stego, stego, payload, lengths, metas, lm + p * lmp,
+                                            workspace, workspace_bytes, stream);
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    hipStream_t st = as_stream(stream);
+    // pass 0 through scheme 1's kernels (copy fused) unless CODEC_PEE_LAT_SS_P0=0, which runs the
+    // copy and all four passes in the one slice-serial launch
+    const bool p0s1 = knob("CODEC_PEE_LAT_SS_P0", 1) != 0 && knob("CODEC_PEE_MULTI_P0", 1) != 0;
+    if (p0s1) {
+        rc = codec_pee_multi_embed_pass(P, 0, cover, stego, payload, lengths, metas, lm, workspace, workspace_bytes,
+                                        stream);
+        if (rc) return rc;
+    }
+    const int cm = p0s1 ? 0 : pee_lss_copy_mode(P, cover, stego);
+    ProfScope prof(st, CODEC_K_PEE_LAT_SS_EMBED);
+    char* sink = static_cast<char*>(workspace) + pee_ws(P).sink;
+    const bool pl = P->payload_words <= LSS_PAY_MAXW && knob("CODEC_PEE_LAT_SS_PL", 1) != 0;
+#define PLSE(TT, PLV) hipLaunchKernelGGL((k_pee_lat_ss<TT, false, PLV, true>), dim3((unsigned)P->B), dim3(LSS_THREADS), 0, st, \
+                                    static_cast<const TT*>(cover), static_cast<TT*>(stego), P->H, P->W, P->T, P->maxval, cm, \
+                                    p0s1 ? 1 : 0, const_cast<u64*>(reinterpret_cast<const u64*>(payload)), P->payload_words, \
+                                    lengths, metas, P->B, reinterpret_cast<u64*>(lm), P->lm_words, sink)
+    const bool pf = knob("CODEC_PEE_LAT_SS_PF", 1) != 0;
+    if (P->bytes == 2) {
+        if (!pf) hipLaunchKernelGGL((k_pee_lat_ss<uint16_t, false, true, false>), dim3((unsigned)P->B), dim3(LSS_THREADS), 0,
+                                    st, static_cast<const uint16_t*>(cover), static_cast<uint16_t*>(stego), P->H, P->W, P->T,
+                                    P->maxval, cm, p0s1 ? 1 : 0, const_cast<u64*>(reinterpret_cast<const u64*>(payload)),
+                                    P->payload_words, lengths, metas, P->B, reinterpret_cast<u64*>(lm), P->lm_words, sink);
+        else if (pl) PLSE(uint16_t, true);
+        else PLSE(uint16_t, false);
+    }
+    else { if (pl) PLSE(uint8_t, true); else PLSE(uint8_t, false); }
+#undef PLSE
+    LAUNCH_CHECK("k_pee_lat_ss<embed>");
+    return 0;
+}
+
+int codec_pee_multi_extract(const codec_pee_params* P, const void* stego, const codec_pee_meta* metas,
+                            const uint64_t* lm, void* cover_out, uint64_t* payload_out, void* workspace,
+                            size_t workspace_bytes, void* stream) {
+    int rc = pee_multi_check(P, 0);
+    if (rc) return rc;
+    if (!stego || !metas || !lm || !cover_out || !payload_out || !workspace)
+        return set_err(CODEC_EINVAL, "codec_pee_multi_extract: NULL pointer argument");
+    if (workspace_bytes < pee_ws(P).total) return set_err(CODEC_EINVAL, "workspace too small");
+    hipStream_t st = as_stream(stream);
+    const size_t lmp = (size_t)P->B * P->lm_words;
+    if (!pee_multi_use_ss(P)) {
+        HIP_TRY(hipMemsetAsync(payload_out, 0, (size_t)P->B * P->payload_words * 8, st));
+        for (int p = 3; p >= 0; --p) {
+            rc = codec_pee_multi_extract_pass(P, p, p == 3 ? stego : cover_out, metas, lm + p * lmp, cover_out,
+                                              payload_out, workspace, workspace_bytes, stream);
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    const int cm = pee_lss_copy_mode(P, stego, cover_out);
+    ProfScope prof(st, CODEC_K_PEE_LAT_SS_EXTRACT);
+    char* sink = static_cast<char*>(workspace) + pee_ws(P).sink;
+    const bool pl = P->payload_words <= LSS_PAY_MAXW && knob("CODEC_PEE_LAT_SS_PL", 1) != 0;
+#define PLSX(TT, PLV, PFV) hipLaunchKernelGGL((k_pee_lat_ss<TT, true, PLV, PFV>), dim3((unsigned)P->B), dim3(LSS_THREADS), 0, st, \
+                                    static_cast<const TT*>(stego), static_cast<TT*>(cover_out), P->H, P->W, P->T, P->maxval, cm, \
+                                    0, reinterpret_cast<u64*>(payload_out), P->payload_words, nullptr, \
+                                    const_cast<codec_pee_meta*>(metas), P->B, const_cast<u64*>(reinterpret_cast<const u64*>(lm)), \
+                                    P->lm_words, sink)
+    const bool pf = knob("CODEC_PEE_LAT_SS_PF", 1) != 0;
+    if (P->bytes == 2) {
+        if (!pf) PLSX(uint16_t, true, false);
+        else if (pl) PLSX(uint16_t, true, true);
+        else PLSX(uint16_t, false, true);
+    } else {
+        if (pl) PLSX(uint8_t, true, true); else PLSX(uint8_t, false, true);
+    }
+#undef PLSX
+    LAUNCH_CHECK("k_pee_lat_ss<extract>");
     return 0;
 }
 

@@ -192,7 +192,9 @@ class PeeCodec:
         return enc
 
     def _embed_multi(self, covers, words, lengths, lens_t, stego, lm, meta, check):
-        """Scheme 2: passes 0..3 (pass 0 copies cover -> stego, the others run in place)."""
+        """Scheme 2: passes 0..3 in one library call (codec_pee_multi_embed: one slice-serial
+        launch after scheme 1's pass 0 on chip-filling batches, per-pass tile launches
+        otherwise); pass 0 copies cover -> stego, the others run in place."""
         torch = _torch()
         if lm is None:
             lm = torch.empty((4, self.B, self.lm_words), dtype=torch.int64, device=self.device)
@@ -200,18 +202,13 @@ class PeeCodec:
             meta = torch.empty((4, self.B, _lib.PEE_META_BYTES), dtype=torch.uint8, device=self.device)
         if tuple(lm.shape) != (4, self.B, self.lm_words) or tuple(meta.shape) != (4, self.B, _lib.PEE_META_BYTES):
             raise ValueError("scheme 2 takes lm [4, B, lm_words] and meta [4, B, PEE_META_BYTES]")
+        if not (lm.is_contiguous() and meta.is_contiguous()):
+            raise ValueError("scheme 2's lm and meta must be contiguous")
         P = self._params(words.shape[1])
         lib = _lib.load()
-
-        def launch():
-            for p in range(4):
-                src = covers if p == 0 else stego
-                _lib.check(lib.codec_pee_multi_embed_pass(C.byref(P), p, src.data_ptr(), stego.data_ptr(),
-                                                          words.data_ptr(), lens_t.data_ptr(), meta.data_ptr(),
-                                                          lm[p].data_ptr(), self.workspace.data_ptr(),
-                                                          self.workspace.numel(), _stream()),
-                           "codec_pee_multi_embed_pass")
-        self._guarded(launch)
+        self._guarded(lambda: _lib.check(lib.codec_pee_multi_embed(
+            C.byref(P), covers.data_ptr(), stego.data_ptr(), words.data_ptr(), lens_t.data_ptr(), meta.data_ptr(),
+            lm.data_ptr(), self.workspace.data_ptr(), self.workspace.numel(), _stream()), "codec_pee_multi_embed"))
         enc = PeeEncoded(stego=stego, lm=lm, meta=meta, lengths=list(lengths), payload_words=int(words.shape[1]),
                          config=self.config, scheme=2)
         if check:   # pass 0 in place runs scheme 1's look-back embed
@@ -236,31 +233,15 @@ class PeeCodec:
         return payload, cover
 
     def _extract_multi(self, stego, meta, lm, payload_words, cover, payload):
-        """Scheme 2: passes 3..0 (pass 3 copies stego -> cover, the others run in place)."""
+        """Scheme 2: passes 3..0 in one library call (codec_pee_multi_extract; the first copies
+        stego -> cover, the others run in place; payload written whole)."""
+        if not (lm.is_contiguous() and meta.is_contiguous()):
+            raise ValueError("scheme 2's lm and meta must be contiguous")
         P = self._params(payload_words)
         lib = _lib.load()
-
-        # pass 0 is scheme 1 on its lattice: its in-place extract (scheme 1's kernels) into a
-        # buffer of its own, OR-ed in (it writes whole payload words); CODEC_PEE_MULTI_P0=0
-        # keeps it on the lattice kernels
-        p0 = _lib.tuning_knob("CODEC_PEE_MULTI_P0", 1) != 0
-        torch = _torch()
-
-        def launch():
-            payload.zero_()
-            for p in ((3, 2, 1) if p0 else (3, 2, 1, 0)):
-                src = stego if p == 3 else cover
-                _lib.check(lib.codec_pee_multi_extract_pass(C.byref(P), p, src.data_ptr(), meta.data_ptr(),
-                                                            lm[p].data_ptr(), cover.data_ptr(), payload.data_ptr(),
-                                                            self.workspace.data_ptr(), self.workspace.numel(),
-                                                            _stream()), "codec_pee_multi_extract_pass")
-            if p0:
-                tmp = torch.empty_like(payload)
-                _lib.check(lib.codec_pee_extract(C.byref(P), cover.data_ptr(), meta[0].data_ptr(), lm[0].data_ptr(),
-                                                 cover.data_ptr(), tmp.data_ptr(), self.workspace.data_ptr(),
-                                                 self.workspace.numel(), _stream()), "codec_pee_extract")
-                payload.bitwise_or_(tmp)
-        self._guarded(launch)
+        self._guarded(lambda: _lib.check(lib.codec_pee_multi_extract(
+            C.byref(P), stego.data_ptr(), meta.data_ptr(), lm.data_ptr(), cover.data_ptr(), payload.data_ptr(),
+            self.workspace.data_ptr(), self.workspace.numel(), _stream()), "codec_pee_multi_extract"))
         return payload, cover
 
     def lookback_failed(self, payload_words: int = 1) -> bool:
@@ -290,11 +271,7 @@ class PeeCodec:
             if short:
                 raise ValueError(f"payload exceeds PEE capacity in slices {short} (scheme 2, T={self.T})")
             words, cover = self.extract(enc.stego, enc.meta, enc.lm, payload_words=enc.payload_words)
-            host = words.cpu().numpy()
-            if self.lookback_failed(enc.payload_words):   # pass 0's in-place extract (scheme 1's)
-                self.reset()
-                raise RuntimeError("codec_pee_extract: in-place cursor look-back timed out; the recovered "
-                                   "payload is invalid (the restored cover is exact)")
+            host = words.cpu().numpy()   # the extract passes have no look-back (tile or slice-serial)
             return [framing.unpack_bits(host[i], enc.lengths[i]) for i in range(self.B)], cover
         recs = enc.records()
         _raise_lookback(recs)

@@ -361,11 +361,27 @@ int codec_pee_multi_embed_pass(const codec_pee_params* P, int32_t pass, const vo
 /* extract pass `pass` (call 3, 2, 1, 0): cover_out = stego (copied when they differ), then
  * the pass restores its lattice in place and ORs its bits into payload_out (zero it before
  * the first pass).  For pass 0 a caller may use codec_pee_extract (in place, with the pass-0
- * records and map) into a separate payload buffer and OR it in -- scheme 1's faster kernels,
- * what PeeCodec does. */
+ * records and map) into a separate payload buffer and OR it in (scheme 1's kernels). */
 int codec_pee_multi_extract_pass(const codec_pee_params* P, int32_t pass, const void* stego,
                                  const codec_pee_meta* metas, const uint64_t* lm, void* cover_out,
                                  uint64_t* payload_out, void* workspace, size_t workspace_bytes, void* stream);
+/* Scheme 2, all four passes in one call each way (what PeeCodec(scheme=2) calls).  lm is the
+ * [4][B][lm_words] maps of the four passes (pass-major), metas [4][B].  The embed runs passes
+ * 0..3 (stego = cover first when they differ); the extract runs passes 3..0 (cover_out = stego
+ * first when they differ) and writes payload_out [B][payload_words] whole (bits of every pass,
+ * zero past them).  Results equal the per-pass calls above.  Where a chip-filling batch gives
+ * every CU a slice (B >= the CU count, the last round >= 85 % full, H * W <= 2^20) a slice-
+ * serial kernel takes each slice's passes in one launch (the embed's pass 0 through scheme 1's
+ * copy-fused kernels first); a pass then stops counting at its `end` chunk and its capacity
+ * carries CODEC_PEE_PARTIAL as scheme 1's single pass does.  Otherwise the per-pass tile
+ * launches run.  No reference counterpart (the reference has no PEE code; oracle/pee_cpu.py
+ * pee_embed_multi / pee_extract_multi is the specification). */
+int codec_pee_multi_embed(const codec_pee_params* P, const void* cover, void* stego, const uint64_t* payload,
+                          const int32_t* lengths, codec_pee_meta* metas, uint64_t* lm, void* workspace,
+                          size_t workspace_bytes, void* stream);
+int codec_pee_multi_extract(const codec_pee_params* P, const void* stego, const codec_pee_meta* metas,
+                            const uint64_t* lm, void* cover_out, uint64_t* payload_out, void* workspace,
+                            size_t workspace_bytes, void* stream);
 
 /* ---- exchange records of the MED-PEE side information (north star: "an RCCL all-gather of
  * per-slice location maps"; no reference counterpart -- the reference is
@@ -433,6 +449,8 @@ int codec_quality_moments(int32_t B, int32_t H, int32_t W, int32_t bytes, const 
 #define CODEC_K_PEE_LAT_EMBED 30   /* scheme 2: one pass's in-place embed                      */
 #define CODEC_K_PEE_LAT_DCOUNT 31  /* scheme 2: one pass's decodable-bit counts + offsets      */
 #define CODEC_K_PEE_LAT_RECOVER 32 /* scheme 2: one pass's in-place recovery                   */
+#define CODEC_K_PEE_LAT_SS_EMBED 33   /* scheme 2 slice-serial: copy + embed passes, one launch  */
+#define CODEC_K_PEE_LAT_SS_EXTRACT 34 /* scheme 2 slice-serial: copy + every extract pass         */
 int codec_profile_begin(int32_t capacity);
 /* after the stream has been synchronised: fills ms[i], tag[i] for the recorded pairs and
  * returns their count (closes the window and frees the events). */

@@ -229,6 +229,8 @@ int main() {
         EXPECT_NEG(codec_pee_extract(&P, p, pmeta, w64, p, w64, p, 1u << 30, nullptr));
         EXPECT_NEG(codec_pee_multi_embed_pass(&P, 0, p, p, w64, i32, pmeta, w64, p, 1u << 30, nullptr));
         EXPECT_NEG(codec_pee_multi_extract_pass(&P, 0, p, pmeta, w64, p, w64, p, 1u << 30, nullptr));
+        EXPECT_NEG(codec_pee_multi_embed(&P, p, p, w64, i32, pmeta, w64, p, 1u << 30, nullptr));
+        EXPECT_NEG(codec_pee_multi_extract(&P, p, pmeta, w64, p, w64, p, 1u << 30, nullptr));
     }
     {
         const codec_pee_params P = good_pee();
@@ -279,6 +281,21 @@ int main() {
         EXPECT_NEG(codec_pee_multi_extract_pass(&P, 2, p, pmeta, w64, p, nullptr, p, ws, nullptr));
         EXPECT_NEG(codec_pee_multi_extract_pass(&P, 2, p, pmeta, w64, p, w64, nullptr, ws, nullptr));
         EXPECT_NEG(codec_pee_multi_extract_pass(&P, 2, p, pmeta, w64, p, w64, p, ws - 1, nullptr));
+        EXPECT_NEG(codec_pee_multi_embed(&P, nullptr, p, w64, i32, pmeta, w64, p, ws, nullptr));
+        EXPECT_NEG(codec_pee_multi_embed(&P, p, nullptr, w64, i32, pmeta, w64, p, ws, nullptr));
+        EXPECT_NEG(codec_pee_multi_embed(&P, p, p, nullptr, i32, pmeta, w64, p, ws, nullptr));
+        EXPECT_NEG(codec_pee_multi_embed(&P, p, p, w64, nullptr, pmeta, w64, p, ws, nullptr));
+        EXPECT_NEG(codec_pee_multi_embed(&P, p, p, w64, i32, nullptr, w64, p, ws, nullptr));
+        EXPECT_NEG(codec_pee_multi_embed(&P, p, p, w64, i32, pmeta, nullptr, p, ws, nullptr));
+        EXPECT_NEG(codec_pee_multi_embed(&P, p, p, w64, i32, pmeta, w64, nullptr, ws, nullptr));
+        EXPECT_NEG(codec_pee_multi_embed(&P, p, p, w64, i32, pmeta, w64, p, ws - 1, nullptr));
+        EXPECT_NEG(codec_pee_multi_extract(&P, nullptr, pmeta, w64, p, w64, p, ws, nullptr));
+        EXPECT_NEG(codec_pee_multi_extract(&P, p, nullptr, w64, p, w64, p, ws, nullptr));
+        EXPECT_NEG(codec_pee_multi_extract(&P, p, pmeta, nullptr, p, w64, p, ws, nullptr));
+        EXPECT_NEG(codec_pee_multi_extract(&P, p, pmeta, w64, nullptr, w64, p, ws, nullptr));
+        EXPECT_NEG(codec_pee_multi_extract(&P, p, pmeta, w64, p, nullptr, p, ws, nullptr));
+        EXPECT_NEG(codec_pee_multi_extract(&P, p, pmeta, w64, p, w64, nullptr, ws, nullptr));
+        EXPECT_NEG(codec_pee_multi_extract(&P, p, pmeta, w64, p, w64, p, ws - 1, nullptr));
         EXPECT_NEG(codec_pee_reset(nullptr, p, ws, nullptr));
         EXPECT_NEG(codec_pee_reset(&P, nullptr, ws, nullptr));
         EXPECT_NEG(codec_pee_reset(&P, p, ws - 1, nullptr));

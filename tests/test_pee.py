@@ -1148,6 +1148,15 @@ def multi_p0(request, monkeypatch):
     return request.param
 
 
+@pytest.fixture(params=["tile", "ss"])
+def lat_ss(request, monkeypatch):
+    """Scheme 2 through the per-pass tile launches (CODEC_PEE_LAT_SS=0, what batches smaller
+    than the chip take) or the slice-serial one-launch kernel (=1, what chip-filling batches
+    take): both bit-exact."""
+    monkeypatch.setenv("CODEC_PEE_LAT_SS", "0" if request.param == "tile" else "1")
+    return request.param
+
+
 def _check_multi_vs_oracle(enc, covers, bits_list, T, mv, stego=None):
     """Every slice of a scheme-2 embedding equals pee_embed_multi: stego, per pass L / end /
     status / capacity (passes that embedded) and location map up to end."""
@@ -1173,7 +1182,7 @@ def _check_multi_vs_oracle(enc, covers, bits_list, T, mv, stego=None):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("k", _multi_kats(), ids=_kat_id)
-def test_gpu_matches_multipass_kats(k, multi_p0):
+def test_gpu_matches_multipass_kats(k, multi_p0, lat_ss):
     """Scheme 2's HIP passes on each known-answer input: stego digest and every pass's record
     and location map equal the committed answers; the reverse passes return payload and cover."""
     import hashlib
@@ -1197,7 +1206,7 @@ def test_gpu_matches_multipass_kats(k, multi_p0):
 @pytest.mark.parametrize("kind,h,w,bsz,T", [("ct12", 64, 96, 5, 2), ("ct12", 67, 45, 3, 1), ("u8", 40, 33, 4, 2),
                                              ("u16", 31, 64, 3, 3), ("ct12", 512, 512, 4, 2), ("u8", 3, 2, 2, 1)])
 @pytest.mark.parametrize("inplace", [False, True])
-def test_gpu_multipass_batch_vs_oracle(kind, h, w, bsz, T, inplace, multi_p0):
+def test_gpu_multipass_batch_vs_oracle(kind, h, w, bsz, T, inplace, multi_p0, lat_ss):
     """Batches of mixed payloads (empty, one pass, several passes, beyond every pass) on even
     and odd shapes: every slice equals the oracle, in place or not, and decodes exactly."""
     torch = pytest.importorskip("torch")
