@@ -713,8 +713,9 @@ def bench_pee2(args, torch, dev, covers, B, H, W, steps, T=2):
                         "psnr_db_mean": round(float(np.mean([r["psnr"] for r in q1])), 3),
                         "pixels_changed_mean": float(np.mean([r["pixels_diferentes"] for r in q1]))},
             "kernels_ms": {k: round(v, 4) for k, v in kern.items()},
-            "path": "count/locate/embed per pass and dcount/offsets/recover per pass, in place on the "
-                    "running image; scalar loads (not the headline's vectorised single-pass kernels)"}
+            "path": "codec_pee_multi_embed / _extract: pass 0 on scheme 1's copy-fused embed, then one "
+                    "slice-serial launch per direction for the other passes (the extract with its copy), in "
+                    "place on the running image"}
 
 
 def bench_c4(args, torch, dist, world, rank, dev):
