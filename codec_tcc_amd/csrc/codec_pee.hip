@@ -4262,8 +4262,14 @@ __global__ __launch_bounds__(LSS_THREADS) void k_pee_lat_ss(const T* __restrict_
     __syncthreads();
     const uint32_t nbits = 64u * (uint32_t)pw;
     uint32_t base = 0;   // embed: payload bits taken by the passes before this one
-    if (!EXTRACT)
-        for (int q = 0; q < p_first; ++q) base += (uint32_t)max(0, metas[(size_t)q * B + b].L);
+    if (!EXTRACT && p_first == 1) {
+        // pass 0 ran on scheme 1's kernels: its record is made scheme 2's here (k_pee_pass0_fix's
+        // rule, idempotent -- L = the bits embedded, capacity when it filled up; lattice 0)
+        codec_pee_meta* M0 = metas + b;
+        const int L0 = M0->status == 1 ? M0->capacity : M0->L;
+        base = (uint32_t)max(0, L0);
+        if (tid == 0) { M0->L = L0; M0->reserved[0] = 0; }
+    }
     int par = 0;
     for (int step = 0; step < (EXTRACT ? 4 : 4 - p_first); ++step) {
         const int p = EXTRACT ? 3 - step : p_first + step;
@@ -4609,9 +4615,9 @@ int codec_pee_multi_embed(const codec_pee_params* P, const void* cover, void* st
     // pass 0 through scheme 1's kernels (copy fused) unless CODEC_PEE_LAT_SS_P0=0, which runs the
     // copy and all four passes in the one slice-serial launch
     const bool p0s1 = knob("CODEC_PEE_LAT_SS_P0", 1) != 0 && knob("CODEC_PEE_MULTI_P0", 1) != 0;
-    if (p0s1) {
-        rc = codec_pee_multi_embed_pass(P, 0, cover, stego, payload, lengths, metas, lm, workspace, workspace_bytes,
-                                        stream);
+    if (p0s1) {   // scheme 1's embed; the slice-serial launch below fixes pass 0's records
+        rc = codec_pee_embed_ts(P, cover, stego, payload, lengths, nullptr, metas, lm, workspace, workspace_bytes,
+                                stream);
         if (rc) return rc;
     }
     const int cm = p0s1 ? 0 : pee_lss_copy_mode(P, cover, stego);
